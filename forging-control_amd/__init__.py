@@ -1,0 +1,10 @@
+"""forging-control_amd — MI355X-native (gfx950) unsupervised-MPC rollout engine.
+
+Drop-in for the hot path of marcowus/forging-control: ``MPCLoss`` (the batched closed-loop rollout of
+the FNN controller through the 3-layer LSTM plant surrogate, Functions.py:1336-1472) and its
+backward, as hand-written HIP kernels behind the C ABI in include/fcr.h.
+"""
+from . import _native, distributed, rollout
+from .functions import FNNModel, LSTMModel, MPCLoss, NeuralNetwork
+
+__all__ = ["FNNModel", "LSTMModel", "MPCLoss", "NeuralNetwork", "rollout", "distributed", "_native"]

@@ -1,0 +1,87 @@
+"""ctypes binding of the C ABI in include/fcr.h (libfcr.so, built for gfx950).
+
+The library is the only compute path of this package: if it is missing or fails to load, every
+entry point raises — there is no CPU or eager-PyTorch fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_LIB_NAME = "libfcr.so"
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", _LIB_NAME)
+
+FCR_OK = 0
+ABI_VERSION = 1
+ERRORS = {-1: "FCR_EINVAL", -2: "FCR_EWORKSPACE", -3: "FCR_EHIP", -4: "FCR_EUNSUPPORTED"}
+
+# Every symbol include/fcr.h declares (tests check the .so exports exactly these).
+EXPORTS = ("fcr_workspace_size", "fcr_forward", "fcr_backward", "fcr_last_error", "fcr_abi_version")
+
+
+class FcrDims(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int32), ("N", ctypes.c_int32), ("L", ctypes.c_int32), ("H", ctypes.c_int32),
+        ("layers", ctypes.c_int32), ("in_dim", ctypes.c_int32), ("out_dim", ctypes.c_int32),
+        ("ctrl_in", ctypes.c_int32), ("ctrl_hidden", ctypes.c_int32), ("alpha", ctypes.c_float),
+    ]
+
+
+class FcrWeights(ctypes.Structure):
+    _fields_ = [
+        ("ctrl_w_inp", ctypes.c_void_p), ("ctrl_b_inp", ctypes.c_void_p), ("ctrl_w_out", ctypes.c_void_p),
+        ("w_ih", ctypes.c_void_p * 3), ("w_hh", ctypes.c_void_p * 3),
+        ("fc_w", ctypes.c_void_p), ("fc_b", ctypes.c_void_p),
+    ]
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load() -> ctypes.CDLL:
+    """Load libfcr.so once (raises NativeError with build instructions if absent)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(hipcc --offload-arch=gfx950). There is no fallback path.")
+        lib = ctypes.CDLL(LIB_PATH)
+        vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+        lib.fcr_workspace_size.argtypes = [ctypes.POINTER(FcrDims), i32, ctypes.POINTER(sz)]
+        lib.fcr_workspace_size.restype = i32
+        lib.fcr_forward.argtypes = [ctypes.POINTER(FcrDims), ctypes.POINTER(FcrWeights),
+                                    vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, sz, vp]
+        lib.fcr_forward.restype = i32
+        lib.fcr_backward.argtypes = [ctypes.POINTER(FcrDims), vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp]
+        lib.fcr_backward.restype = i32
+        lib.fcr_last_error.argtypes = []
+        lib.fcr_last_error.restype = ctypes.c_char_p
+        lib.fcr_abi_version.argtypes = []
+        lib.fcr_abi_version.restype = i32
+        if lib.fcr_abi_version() != ABI_VERSION:
+            raise NativeError(f"libfcr ABI {lib.fcr_abi_version()} != expected {ABI_VERSION}")
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != FCR_OK:
+        msg = load().fcr_last_error().decode(errors="replace")
+        raise NativeError(f"{what} failed ({ERRORS.get(rc, rc)}): {msg}")
+
+
+def workspace_bytes(dims: FcrDims, with_backward: bool) -> int:
+    out = ctypes.c_size_t(0)
+    check(load().fcr_workspace_size(ctypes.byref(dims), int(bool(with_backward)), ctypes.byref(out)),
+          "fcr_workspace_size")
+    return int(out.value)

@@ -1,0 +1,288 @@
+// fcr_abi.hip — host side and C ABI (include/fcr.h) of the gfx950 rollout engine.
+//
+// Replaces the torch work behind `loss_function(...)` / `loss.backward()` at
+// /root/reference/Unsupervised Learning/Functions.py:646 and :655. All launches are stream-ordered on
+// the caller's stream; nothing here allocates or synchronises.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "fcr.h"
+#include "fcr_bwd.h"
+#include "fcr_common.h"
+#include "fcr_fwd.h"
+#include "fcr_pack.h"
+
+namespace fcr {
+namespace {
+
+thread_local char g_err[512] = "no error";
+
+int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+struct Layout {
+    int HS, nw, nw_pad, NB0, NB1;
+    size_t fa[3], ba[3], fcp, fcb, fnp, xhat, loss_part, fnn_part, gates, cstore, dseq, total;
+};
+
+size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int check_dims(const fcr_dims *d) {
+    if (!d) return fail(FCR_EINVAL, "dims is NULL");
+    if (d->B < 1) return fail(FCR_EINVAL, "B=%d must be >= 1", d->B);
+    if (d->N < 1) return fail(FCR_EINVAL, "N=%d must be >= 1", d->N);
+    if (d->L != kL) return fail(FCR_EUNSUPPORTED, "L=%d: the rollout window is fixed at 10 rows", d->L);
+    if (d->layers != kLayers) return fail(FCR_EUNSUPPORTED, "layers=%d: built for 3", d->layers);
+    if (d->in_dim != kIn || d->out_dim != kOut || d->ctrl_in != kCtrlIn)
+        return fail(FCR_EUNSUPPORTED, "in/out/ctrl_in = %d/%d/%d: built for 5/4/3", d->in_dim,
+                    d->out_dim, d->ctrl_in);
+    if (d->ctrl_hidden < 1 || d->ctrl_hidden > 4 * kMS)
+        return fail(FCR_EUNSUPPORTED, "ctrl_hidden=%d: built for 1..52", d->ctrl_hidden);
+    if (!(d->H == 16 || d->H == 32 || d->H == 50 || d->H == 64))
+        return fail(FCR_EUNSUPPORTED, "H=%d: built for 16, 32, 50, 64", d->H);
+    if ((long long)d->B * d->N > (1LL << 31)) return fail(FCR_EINVAL, "B*N too large");
+    return FCR_OK;
+}
+
+Layout make_layout(const fcr_dims *d, int with_backward) {
+    Layout L{};
+    L.HS = (d->H + 3) / 4;
+    L.nw = (d->B + kTile - 1) / kTile;
+    constexpr int kPad = kFwdWaves > kBwdWaves ? kFwdWaves : kBwdWaves;
+    L.nw_pad = (L.nw + kPad - 1) / kPad * kPad;  // covers both launch geometries
+    L.NB0 = (L.HS + 2 + 3) / 4;
+    L.NB1 = (2 * L.HS + 3) / 4;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += align_up(bytes);
+        return o;
+    };
+    const int HS = L.HS;
+    const int KQ0 = (2 + HS + 3) / 4 * 4, KQ1 = (2 * HS + 3) / 4 * 4;
+    L.fa[0] = take(sizeof(float) * HS * KQ0 * kWave);
+    L.fa[1] = take(sizeof(float) * HS * KQ1 * kWave);
+    L.fa[2] = take(sizeof(float) * HS * KQ1 * kWave);
+    L.ba[0] = take(sizeof(float) * L.NB0 * 4 * HS * kWave);
+    L.ba[1] = take(sizeof(float) * L.NB1 * 4 * HS * kWave);
+    L.ba[2] = take(sizeof(float) * L.NB1 * 4 * HS * kWave);
+    L.fcp = take(sizeof(float) * kOut * HS * 4);
+    L.fcb = take(sizeof(float) * kOut);
+    L.fnp = take(sizeof(float) * kMS * 4 * kFnpStride);
+    L.xhat = take(sizeof(float) * (size_t)d->B * d->N * kOut);
+    L.loss_part = take(sizeof(float) * L.nw_pad);
+    L.fnn_part = take(sizeof(float) * (size_t)L.nw_pad * d->ctrl_hidden * 5);
+    if (with_backward) {
+        const size_t cells = (size_t)L.nw_pad * d->N * kLayers * kL * HS * kWave;
+        L.gates = take(sizeof(f32x4) * cells);
+        L.cstore = take(sizeof(float) * cells);
+        L.dseq = take(sizeof(float) * (size_t)L.nw_pad * d->N * 2 * kL * HS * kWave);
+    }
+    L.total = off;
+    return L;
+}
+
+Packed packed_ptrs(const Layout &L, char *ws) {
+    Packed p;
+    for (int l = 0; l < kLayers; ++l) {
+        p.fa[l] = (const float *)(ws + L.fa[l]);
+        p.ba[l] = (const float *)(ws + L.ba[l]);
+    }
+    p.fcp = (const float *)(ws + L.fcp);
+    p.fcb = (const float *)(ws + L.fcb);
+    p.fnp = (const float *)(ws + L.fnp);
+    return p;
+}
+
+int launch_check(const char *what) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(FCR_EHIP, "launch of %s failed: %s", what, hipGetErrorString(e));
+    return FCR_OK;
+}
+
+template <int HS, bool STORE>
+int launch_fwd_t(const FwdArgs &fa, const Layout &L, hipStream_t s) {
+    const int lds = Geo<HS>::LDS_FWD;
+    static bool attr_set = false;
+    if (!attr_set) {
+        const hipError_t e = hipFuncSetAttribute((const void *)fcr_fwd_kernel<HS, STORE>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(fwd): %s", hipGetErrorString(e));
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((fcr_fwd_kernel<HS, STORE>), dim3(L.nw_pad / kFwdWaves), dim3(kFwdWaves * kWave),
+                       lds, s, fa);
+    return launch_check("fcr_fwd_kernel");
+}
+
+template <int HS>
+int launch_fwd(const FwdArgs &fa, const Layout &L, hipStream_t s) {
+    return fa.gates ? launch_fwd_t<HS, true>(fa, L, s) : launch_fwd_t<HS, false>(fa, L, s);
+}
+
+template <int HS>
+int launch_bwd(const BwdArgs &ba, const Layout &L, hipStream_t s) {
+    const int lds = Geo<HS>::LDS_BWD;
+    static bool attr_set = false;
+    if (!attr_set) {
+        const hipError_t e = hipFuncSetAttribute((const void *)fcr_bwd_kernel<HS>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(bwd): %s", hipGetErrorString(e));
+        attr_set = true;
+    }
+    hipLaunchKernelGGL(fcr_bwd_kernel<HS>, dim3(L.nw_pad / kBwdWaves), dim3(kBwdWaves * kWave), lds, s, ba);
+    return launch_check("fcr_bwd_kernel");
+}
+
+}  // namespace
+}  // namespace fcr
+
+using namespace fcr;
+
+extern "C" {
+
+const char *fcr_last_error(void) { return g_err; }
+
+int fcr_abi_version(void) { return FCR_ABI_VERSION; }
+
+int fcr_workspace_size(const fcr_dims *dims, int with_backward, size_t *bytes) {
+    int rc = check_dims(dims);
+    if (rc) return rc;
+    if (!bytes) return fail(FCR_EINVAL, "bytes is NULL");
+    *bytes = make_layout(dims, with_backward).total;
+    return FCR_OK;
+}
+
+int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const float *u0,
+                const float *states, const float *noise, float *loss, float *cost, float *command,
+                float *error, float *prediction, float *xhat, int with_backward, void *ws,
+                size_t ws_bytes, void *stream) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    if (!w || !X || !u0 || !states || !loss || !cost || !command || !error || !prediction || !ws)
+        return fail(FCR_EINVAL, "fcr_forward: a required pointer is NULL");
+    for (int l = 0; l < kLayers; ++l)
+        if (!w->w_ih[l] || !w->w_hh[l])
+            return fail(FCR_EINVAL, "fcr_forward: LSTM weight of layer %d is NULL", l);
+    if (!w->fc_w || !w->fc_b || !w->ctrl_w_inp || !w->ctrl_b_inp || !w->ctrl_w_out)
+        return fail(FCR_EINVAL, "fcr_forward: a weight pointer is NULL");
+    if (((uintptr_t)ws) & 255) return fail(FCR_EINVAL, "fcr_forward: ws must be 256-byte aligned");
+    const Layout L = make_layout(d, with_backward);
+    if (ws_bytes < L.total)
+        return fail(FCR_EWORKSPACE, "fcr_forward: ws has %zu bytes, needs %zu", ws_bytes, L.total);
+    hipStream_t s = (hipStream_t)stream;
+    char *base = (char *)ws;
+
+    PackArgs pa{};
+    pa.H = d->H;
+    pa.HS = L.HS;
+    pa.CH = d->ctrl_hidden;
+    for (int l = 0; l < kLayers; ++l) {
+        pa.wih[l] = w->w_ih[l];
+        pa.whh[l] = w->w_hh[l];
+        pa.fa[l] = (float *)(base + L.fa[l]);
+        pa.ba[l] = (float *)(base + L.ba[l]);
+    }
+    pa.fcw = w->fc_w;
+    pa.fcb = w->fc_b;
+    pa.cwi = w->ctrl_w_inp;
+    pa.cbi = w->ctrl_b_inp;
+    pa.cwo = w->ctrl_w_out;
+    pa.fcp = (float *)(base + L.fcp);
+    pa.fcbo = (float *)(base + L.fcb);
+    pa.fnp = (float *)(base + L.fnp);
+    for (int l = 0; l < kLayers; ++l) {
+        const int nf = L.HS * (l == 0 ? (2 + L.HS + 3) / 4 * 4 : (2 * L.HS + 3) / 4 * 4) * kWave;
+        hipLaunchKernelGGL(pack_fwd_kernel, dim3((nf + 255) / 256), dim3(256), 0, s, pa, l);
+        if ((rc = launch_check("pack_fwd_kernel"))) return rc;
+        if (with_backward) {
+            const int nb = (l == 0 ? L.NB0 : L.NB1) * 4 * L.HS * kWave;
+            hipLaunchKernelGGL(pack_bwd_kernel, dim3((nb + 255) / 256), dim3(256), 0, s, pa, l);
+            if ((rc = launch_check("pack_bwd_kernel"))) return rc;
+        }
+    }
+    hipLaunchKernelGGL(pack_misc_kernel, dim3(2), dim3(256), 0, s, pa);
+    if ((rc = launch_check("pack_misc_kernel"))) return rc;
+
+    FwdArgs fa{};
+    fa.B = d->B;
+    fa.N = d->N;
+    fa.alpha = d->alpha;
+    fa.X = X;
+    fa.u0 = u0;
+    fa.states = states;
+    fa.noise = noise;
+    fa.cost = cost;
+    fa.command = command;
+    fa.error = error;
+    fa.prediction = prediction;
+    fa.xhat_user = xhat;
+    fa.xhat_ws = (float *)(base + L.xhat);
+    fa.loss_part = (float *)(base + L.loss_part);
+    fa.gates = with_backward ? (f32x4 *)(base + L.gates) : nullptr;
+    fa.cstore = with_backward ? (float *)(base + L.cstore) : nullptr;
+    fa.p = packed_ptrs(L, base);
+    switch (d->H) {
+        case 16: rc = launch_fwd<4>(fa, L, s); break;
+        case 32: rc = launch_fwd<8>(fa, L, s); break;
+        case 50: rc = launch_fwd<13>(fa, L, s); break;
+        case 64: rc = launch_fwd<16>(fa, L, s); break;
+        default: rc = fail(FCR_EUNSUPPORTED, "H=%d", d->H);
+    }
+    if (rc) return rc;
+    hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(256), 0, s, (const float *)fa.loss_part,
+                       L.nw_pad, d->B, loss);
+    return launch_check("loss_reduce_kernel");
+}
+
+int fcr_backward(const fcr_dims *d, const float *X, const float *states, const float *prediction,
+                 const float *dloss, float *g_u0, float *g_w_inp, float *g_b_inp, float *g_w_out,
+                 void *ws, size_t ws_bytes, void *stream) {
+    int rc = check_dims(d);
+    if (rc) return rc;
+    if (!X || !states || !prediction || !dloss || !g_u0 || !g_w_inp || !g_b_inp || !g_w_out || !ws)
+        return fail(FCR_EINVAL, "fcr_backward: a required pointer is NULL");
+    if (((uintptr_t)ws) & 255) return fail(FCR_EINVAL, "fcr_backward: ws must be 256-byte aligned");
+    const Layout L = make_layout(d, 1);
+    if (ws_bytes < L.total)
+        return fail(FCR_EWORKSPACE, "fcr_backward: ws has %zu bytes, needs %zu", ws_bytes, L.total);
+    hipStream_t s = (hipStream_t)stream;
+    char *base = (char *)ws;
+    BwdArgs ba{};
+    ba.B = d->B;
+    ba.N = d->N;
+    ba.hidden = d->ctrl_hidden;
+    ba.alpha = d->alpha;
+    ba.X = X;
+    ba.states = states;
+    ba.prediction = prediction;
+    ba.xhat = (const float *)(base + L.xhat);
+    ba.dloss = dloss;
+    ba.gates = (const f32x4 *)(base + L.gates);
+    ba.cstore = (const float *)(base + L.cstore);
+    ba.dseq = (float *)(base + L.dseq);
+    ba.g_u0 = g_u0;
+    ba.fnn_part = (float *)(base + L.fnn_part);
+    ba.p = packed_ptrs(L, base);
+    switch (d->H) {
+        case 16: rc = launch_bwd<4>(ba, L, s); break;
+        case 32: rc = launch_bwd<8>(ba, L, s); break;
+        case 50: rc = launch_bwd<13>(ba, L, s); break;
+        case 64: rc = launch_bwd<16>(ba, L, s); break;
+        default: rc = fail(FCR_EUNSUPPORTED, "H=%d", d->H);
+    }
+    if (rc) return rc;
+    hipLaunchKernelGGL(grad_reduce_kernel, dim3(d->ctrl_hidden * 5), dim3(256), 0, s,
+                       (const float *)ba.fnn_part, L.nw_pad, d->ctrl_hidden, g_w_inp, g_b_inp, g_w_out);
+    return launch_check("grad_reduce_kernel");
+}
+
+}  // extern "C"

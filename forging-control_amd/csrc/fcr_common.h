@@ -1,0 +1,147 @@
+// fcr_common.h — shared constants, device helpers and kernel argument blocks.
+//
+// Fragment geometry (H = LSTM hidden, HS = ceil(H/4) "unit slots"; unit u = 4*slot + q where
+// q = lane>>4 is the lane group):
+//   forward  tile r (16 D rows = units 4r..4r+3 x gates i,f,g,o), fragments [r][k/4][lane][k%4], k-steps:
+//       layer 0 : KS0 = 2 + HS   (2 steps over the 5 window columns, HS over h_{t-1})
+//       layer>=1: KS1 = 2 * HS   (HS over the layer-below h_t, HS over h_{t-1})
+//   backward output tile tau (16 D rows = 4 slots x 4 lane groups), fragments [tau][r][lane][gamma],
+//       k-steps KB = 4 * HS
+//       (slot r, gate gamma) -> s' = 4r + gamma:
+//       layer 0 : NB0 = ceil((HS+2)/4) tiles  (slots < HS: dh_prev; slot HS: dx col q; HS+1: dx col 4)
+//       layer>=1: NB1 = ceil(2HS/4) tiles     (slots < HS: dx; HS..2HS-1: dh_prev)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace fcr {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+constexpr int kTile = 16;        // trajectories per wave (MFMA 16x16x4 column count)
+constexpr int kL = 10;           // window rows (Functions.py:1434 hard-codes 1:10)
+constexpr int kLayers = 3;       // UL/Main.py:147 (width_dim passed as layer_dim)
+constexpr int kIn = 5;           // [y_dot, p1, p2, z, u]
+constexpr int kOut = 4;          // [y_dot, p1, p2, z]
+constexpr int kCtrlIn = 3;       // [y_dot, z, ref]
+constexpr int kMS = 13;          // controller hidden slots (units 4m+q), hidden <= 52
+constexpr int kFnpStride = 8;    // floats per (m, q) controller record: W0 W1 W2 b wout 0 0 0
+constexpr int kFwdWaves = 4;     // waves per forward workgroup (1 per SIMD, 512 VGPRs)
+constexpr int kBwdWaves = 4;     // waves per backward workgroup (1 per SIMD, 512 VGPRs)
+constexpr float kP1Max = 2.122366f;  // Functions.py:1411 (32e6 / p1 max_abs_)
+constexpr float kP2Max = 1.036233f;  // Functions.py:1411 (32e6 / p2 max_abs_)
+
+template <int HS>
+struct Geo {
+    static constexpr int KS0 = 2 + HS;
+    static constexpr int KS1 = 2 * HS;
+    static constexpr int KB = 4 * HS;
+    static constexpr int NB0 = (HS + 2 + 3) / 4;
+    static constexpr int NB1 = (2 * HS + 3) / 4;
+    static constexpr int KQ0 = (KS0 + 3) / 4 * 4;  // k-steps padded to whole k-quads
+    static constexpr int KQ1 = (KS1 + 3) / 4 * 4;
+    static constexpr int FA0 = HS * KQ0 * kWave;  // floats
+    static constexpr int FA1 = HS * KQ1 * kWave;
+    static constexpr int BA0 = NB0 * KB * kWave;
+    static constexpr int BA1 = NB1 * KB * kWave;
+    static constexpr int LDS_FWD = (FA0 > FA1 ? FA0 : FA1) * 4;  // bytes
+    static constexpr int LDS_BWD = (BA0 > BA1 ? BA0 : BA1) * 4;
+};
+
+struct Packed {                    // device pointers into the workspace
+    const float *fa[3];            // forward fragments  [r][s][64]
+    const float *ba[3];            // backward fragments [tau][s'][64]
+    const float *fcp;              // fc.weight in lane layout [o][slot][q]
+    const float *fcb;              // fc.bias [4]
+    const float *fnp;              // controller records [m][q][8]
+};
+
+struct FwdArgs {
+    int B, N;
+    float alpha;
+    const float *X, *u0, *states, *noise;
+    float *cost, *command, *error, *prediction, *xhat_user, *xhat_ws, *loss_part;
+    f32x4 *gates;    // [wave][j][l][t][slot][64] post-activation (i,f,g,o), or null
+    float *cstore;   // [wave][j][l][t][slot][64] c_t, or null
+    Packed p;
+};
+
+struct BwdArgs {
+    int B, N, hidden;
+    float alpha;
+    const float *X, *states, *prediction, *xhat, *dloss;
+    const f32x4 *gates;
+    const float *cstore;
+    float *dseq;     // [wave][j][2][t][slot][64] dx of layers 2 and 1 (inputs of layers 1 and 0)
+    float *g_u0, *fnn_part;
+    Packed p;
+};
+
+// ------------------------------------------------------------------------------------------------
+// device helpers
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ f32x4 mfma(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+// logistic and tanh on v_exp_f32 / v_rcp_f32 (saturate correctly at +-inf)
+__device__ __forceinline__ float sigm(float x) {
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
+}
+__device__ __forceinline__ float tanh_f(float x) {
+    return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * 2.8853900817779268f));
+}
+__device__ __forceinline__ float relu(float x) { return x > 0.0f ? x : 0.0f; }
+__device__ __forceinline__ float sq(float x) { return x * x; }
+__device__ __forceinline__ float hardtanh(float v) { return fminf(fmaxf(v, -1.0f), 1.0f); }
+__device__ __forceinline__ float sel4(int q, float a, float b, float c, float d) {
+    return q == 0 ? a : (q == 1 ? b : (q == 2 ? c : d));
+}
+// sum over the 4 lane groups that share one trajectory
+__device__ __forceinline__ float xor_sum_q(float v) {
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    return v;
+}
+__device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+
+// ds_read_b128 of fragment quad `idx` (units of 16 B per lane-slot, i.e. element idx*64+lane of an
+// f32x4 array). ds_* immediate offsets are 16-bit, so fragment blocks beyond 64 KB would each need a
+// materialised address VGPR (which the compiler then hoists out of every loop and spills). Two
+// bases, 48 KB apart, keep every compile-time offset inside the immediate field.
+__device__ __forceinline__ f32x4 lds_quad(const float *lw, int idx, int lane) {
+    constexpr int kSplit = 48 * 1024;
+    const int byte = idx * kWave * 16;
+    const char *lo = reinterpret_cast<const char *>(lw) + lane * 16;
+    if (byte < kSplit) return *reinterpret_cast<const f32x4 *>(lo + byte);
+    const char *hi = lo + kSplit;
+    return *reinterpret_cast<const f32x4 *>(hi + (byte - kSplit));
+}
+
+// Copy the current phase's fragment block (global, L2-resident) into LDS. Every wave of the
+// workgroup calls this at the same program point.
+__device__ __forceinline__ void lds_fill(float *lw, const float *__restrict__ src, int nfloats) {
+    __syncthreads();
+    const float4 *s4 = reinterpret_cast<const float4 *>(src);
+    float4 *d4 = reinterpret_cast<float4 *>(lw);
+    for (int i = threadIdx.x; i < nfloats / 4; i += blockDim.x) d4[i] = s4[i];
+    __syncthreads();
+}
+
+// Controller pre-activation (FNNModel.forward, Functions.py:261-289): lane group q evaluates hidden
+// units 4m+q; returns the pre-Hardtanh output (identical arithmetic in forward and backward).
+__device__ __forceinline__ float fnn_pre(const float *__restrict__ fnp, int q, float a, float b,
+                                         float r, float (&z)[kMS]) {
+    float part = 0.0f;
+#pragma unroll
+    for (int m = 0; m < kMS; ++m) {
+        const float *p = fnp + (m * 4 + q) * kFnpStride;
+        const float zz = p[0] * a + p[1] * b + p[2] * r + p[3];
+        z[m] = zz;
+        part += p[4] * relu(zz);
+    }
+    return xor_sum_q(part);
+}
+
+}  // namespace fcr

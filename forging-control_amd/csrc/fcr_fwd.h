@@ -1,0 +1,233 @@
+// fcr_fwd.h — forward rollout kernel (MPCLoss.forward, Functions.py:1353-1472).
+//
+// One wave = 16 trajectories; one workgroup = kFwdWaves waves sharing one LDS-resident layer of
+// MFMA fragments. Each window (horizon step) runs three layer PHASES (layer-major): the current
+// layer's fragments are copied into LDS, then the wave steps t = 0..9 through that layer, keeping
+// the layer's 10 outputs in a register ring that becomes the next phase's input.
+#pragma once
+#include "fcr_common.h"
+
+namespace fcr {
+
+// Cell update for one unit slot: a = D fragment (i,f,g,o pre-activations of unit 4r+q).
+template <bool FIRST, bool STORE>
+__device__ __forceinline__ void fwd_pointwise(f32x4 a, float &c, float &h, f32x4 *gs, float *cs,
+                                              int lane) {
+    const float i = sigm(a[0]);
+    const float f = sigm(a[1]);
+    const float g = tanh_f(a[2]);
+    const float o = sigm(a[3]);
+    const float cn = FIRST ? i * g : f * c + i * g;   // c_{-1} = 0 (Functions.py:349-350)
+    c = cn;
+    h = o * tanh_f(cn);
+    if (STORE) {
+        gs[lane] = f32x4{i, f, g, o};
+        cs[lane] = cn;
+    }
+}
+
+// One LSTM cell for 16 trajectories. L0: input is the window row (x0: column q in lane group q,
+// x1: column 4 in lane group 0); otherwise x = the layer-below h_t. FIRST: t = 0 (h_{t-1} = 0, so the
+// recurrent product is skipped). lw = this layer's fragments in LDS, [r][k-quad][lane][4]: one
+// ds_read_b128 feeds four MFMAs. Each k-quad is its own scheduling region (bounded register use);
+// the cell update of tile r-1 is issued in the first region of tile r, beside its MFMAs.
+template <int HS, bool L0, bool FIRST, bool STORE>
+__device__ __forceinline__ void fwd_cell(const float *__restrict__ lw, int lane, float x0, float x1,
+                                         const float (&x)[HS], const float (&hp)[HS], float (&c)[HS],
+                                         float (&hout)[HS], f32x4 *gs, float *cs) {
+    constexpr int NX = L0 ? 2 : HS;                 // k-steps over the input
+    constexpr int NK = FIRST ? NX : NX + HS;        // k-steps used (h_{t-1} part skipped at t = 0)
+    constexpr int QR = (NX + HS + 3) / 4;           // k-quads per fragment row
+    constexpr int QN = (NK + 3) / 4;                // k-quads used
+    f32x4 cur = lds_quad(lw, 0, lane);
+    f32x4 prev = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int r = 0; r < HS; ++r) {
+        f32x4 va[4];   // four accumulation chains over the k-steps (MFMA dependent latency)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) va[u] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int qd = 0; qd < QN; ++qd) {
+            sched_fence();
+            f32x4 nxt = cur;
+            if (qd + 1 < QN) nxt = lds_quad(lw, r * QR + qd + 1, lane);
+            else if (r + 1 < HS) nxt = lds_quad(lw, (r + 1) * QR, lane);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int s = 4 * qd + e;
+                if (s < NK) {
+                    float bop;
+                    if (s < NX) bop = L0 ? (s == 0 ? x0 : x1) : x[s < NX ? s : 0];
+                    else bop = hp[s - NX < HS ? s - NX : 0];
+                    va[e] = mfma(cur[e], bop, va[e]);
+                }
+            }
+            if (qd == 0 && r > 0)
+                fwd_pointwise<FIRST, STORE>(prev, c[r - 1], hout[r - 1], gs + (r - 1) * kWave,
+                                            cs + (r - 1) * kWave, lane);
+            cur = nxt;
+        }
+        prev = (va[0] + va[1]) + (va[2] + va[3]);
+    }
+    sched_fence();
+    fwd_pointwise<FIRST, STORE>(prev, c[HS - 1], hout[HS - 1], gs + (HS - 1) * kWave,
+                                cs + (HS - 1) * kWave, lane);
+}
+
+template <int HS>
+__device__ __forceinline__ void ring_push(float (&ring)[kL][HS], const float (&v)[HS]) {
+#pragma unroll
+    for (int k = 0; k < kL - 1; ++k)
+#pragma unroll
+        for (int r = 0; r < HS; ++r) ring[k][r] = ring[k + 1][r];
+#pragma unroll
+    for (int r = 0; r < HS; ++r) ring[kL - 1][r] = v[r];
+}
+
+__device__ __forceinline__ void rot_left(float (&w)[kL]) {
+    const float t0 = w[0];
+#pragma unroll
+    for (int k = 0; k < kL - 1; ++k) w[k] = w[k + 1];
+    w[kL - 1] = t0;
+}
+
+template <int HS, bool STORE>
+__global__ __launch_bounds__(kFwdWaves * kWave, 1) void fcr_fwd_kernel(FwdArgs a) {
+    using G = Geo<HS>;
+    extern __shared__ __attribute__((aligned(16))) float lw[];
+    const int lane = threadIdx.x & 63;
+    const int q = lane >> 4, sl = lane & 15;
+    // wave-uniform by construction; readfirstlane lets the compiler keep every address base in SGPRs
+    const int wave = blockIdx.x * kFwdWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = wave * kTile + sl;
+    const bool valid = b < a.B;
+    const int bc = valid ? b : a.B - 1;   // out-of-range lanes recompute the last trajectory
+    const int N = a.N;
+    const float alpha = a.alpha;
+
+    const float ref = a.X[(size_t)bc * kCtrlIn + 2];                 // Functions.py:1392
+    const float *st = a.states + (size_t)bc * kL * kIn;
+    float w0[kL], w1[kL];                                             // window ring, B-operand layout
+#pragma unroll
+    for (int t = 0; t < kL; ++t) {
+        w0[t] = st[t * kIn + q];
+        w1[t] = (q == 0) ? st[t * kIn + 4] : 0.0f;
+    }
+    const float u0 = a.u0[bc];
+    if (q == 0) w1[kL - 1] = u0;                                      // Functions.py:1396
+    float u_prev = u0;
+    float cmd_j = alpha * sq(st[(kL - 2) * kIn + 4] - u0);            // Functions.py:1405
+    float cmd_sum = 0.0f, err_sum = 0.0f, tot_sum = 0.0f;
+    float xh0 = 0.0f, xh1 = 0.0f, xh2 = 0.0f, xh3 = 0.0f;
+
+    float ring[kL][HS];   // outputs of the current layer for t = 0..9 (next phase's inputs)
+    float c[HS], hout[HS];
+#pragma unroll
+    for (int k = 0; k < kL; ++k)
+#pragma unroll
+        for (int r = 0; r < HS; ++r) ring[k][r] = 0.0f;
+    const size_t cell = (size_t)HS * kWave;
+    const size_t cells_per_wave = (size_t)N * kLayers * kL;
+
+    for (int j = 0; j < N; ++j) {
+        float pred = u0;
+        if (j > 0) {                                                   // Functions.py:1421-1434
+            float z[kMS];
+            const float un = hardtanh(fnn_pre(a.p.fnp, q, xh0, xh3, ref, z));
+            cmd_j = alpha * sq(u_prev - un);                           // Functions.py:1446
+#pragma unroll
+            for (int k = 0; k < kL - 1; ++k) {
+                w0[k] = w0[k + 1];
+                w1[k] = w1[k + 1];
+            }
+            w0[kL - 1] = sel4(q, xh0, xh1, xh2, xh3);
+            w1[kL - 1] = (q == 0) ? un : 0.0f;
+            u_prev = un;
+            pred = un;
+        }
+        if (valid && q == 0) a.prediction[(size_t)b * N + j] = pred;   // Functions.py:1455,1466
+
+        f32x4 *gs = a.gates;
+        float *cs = a.cstore;
+        if (STORE) {
+            const size_t base = ((size_t)wave * cells_per_wave + (size_t)j * kLayers * kL) * cell;
+            gs += base;
+            cs += base;
+        }
+#define FCR_G(l, t) (gs + (STORE ? (size_t)((l) * kL + (t)) * cell : 0))
+#define FCR_C(l, t) (cs + (STORE ? (size_t)((l) * kL + (t)) * cell : 0))
+        // ---- layer 0 over the window (Functions.py:374) ----
+        lds_fill(lw, a.p.fa[0], G::FA0);
+        {
+            const float x0 = w0[0], x1 = w1[0];
+            rot_left(w0);
+            rot_left(w1);
+            fwd_cell<HS, true, true, STORE>(lw, lane, x0, x1, hout, hout, c, hout, FCR_G(0, 0), FCR_C(0, 0));
+            ring_push<HS>(ring, hout);
+        }
+        for (int t = 1; t < kL; ++t) {
+            const float x0 = w0[0], x1 = w1[0];
+            rot_left(w0);
+            rot_left(w1);
+            fwd_cell<HS, true, false, STORE>(lw, lane, x0, x1, hout, ring[kL - 1], c, hout, FCR_G(0, t),
+                                      FCR_C(0, t));
+            ring_push<HS>(ring, hout);
+        }
+        // ---- layers 1, 2 ----
+#pragma unroll
+        for (int l = 1; l < kLayers; ++l) {
+            lds_fill(lw, a.p.fa[l], G::FA1);
+            fwd_cell<HS, false, true, STORE>(lw, lane, 0.0f, 0.0f, ring[0], ring[0], c, hout, FCR_G(l, 0),
+                                      FCR_C(l, 0));
+            ring_push<HS>(ring, hout);
+            for (int t = 1; t < kL; ++t) {
+                fwd_cell<HS, false, false, STORE>(lw, lane, 0.0f, 0.0f, ring[0], ring[kL - 1], c, hout,
+                                           FCR_G(l, t), FCR_C(l, t));
+                ring_push<HS>(ring, hout);
+            }
+        }
+#undef FCR_G
+#undef FCR_C
+        // ---- readout fc(h_9 of layer 2) (Functions.py:377) ----
+        float xo[kOut];
+#pragma unroll
+        for (int o = 0; o < kOut; ++o) {
+            float p = 0.0f;
+#pragma unroll
+            for (int r = 0; r < HS; ++r) p += a.p.fcp[(o * HS + r) * 4 + q] * ring[kL - 1][r];
+            xo[o] = xor_sum_q(p) + a.p.fcb[o];
+        }
+        if (a.noise) {                                                 // Functions.py:1400-1402
+            const float *nz = a.noise + ((size_t)bc * N + j) * kOut;
+#pragma unroll
+            for (int o = 0; o < kOut; ++o) xo[o] += nz[o];
+        }
+        xh0 = xo[0];
+        xh1 = xo[1];
+        xh2 = xo[2];
+        xh3 = xo[3];
+        if (valid) {
+            const float mine = sel4(q, xh0, xh1, xh2, xh3);
+            a.xhat_ws[((size_t)b * N + j) * kOut + q] = mine;
+            if (a.xhat_user) a.xhat_user[((size_t)b * N + j) * kOut + q] = mine;
+        }
+        // ---- step cost (Functions.py:1405-1414, 1443-1452) ----
+        const float err = sq(xh0 - ref);
+        const float con = relu(-xh1) + relu(-xh2) + relu(xh1 - kP1Max) + relu(xh2 - kP2Max);
+        tot_sum += (err + cmd_j) + con;
+        err_sum += err;
+        cmd_sum += cmd_j;
+    }
+    const float cost = tot_sum / (float)N;                             // Functions.py:1458-1460
+    if (valid && q == 0) {
+        a.cost[b] = cost;
+        a.command[b] = cmd_sum / (float)N;
+        a.error[b] = err_sum / (float)N;
+    }
+    float part = (valid && q == 0) ? cost : 0.0f;                      // per-wave loss partial
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) part += __shfl_xor(part, m);
+    if (lane == 0) a.loss_part[wave] = part;
+}
+
+}  // namespace fcr

@@ -1,0 +1,56 @@
+"""Data-parallel rollout across the GPUs of one node: one process per GPU, RCCL over xGMI.
+
+The rollout shards trivially by trajectory (no cross-sample op before the batch mean,
+Functions.py:1387-1463). Each rank runs the fused forward/backward on its B_local trajectories; the
+only exchange is ONE all-reduce of the packed controller gradients (250 floats) plus the loss (one
+float) per optimizer step — about 1 KB, latency-bound, so it is a single flat bucket, not a
+bandwidth-tuned ring schedule. AdamW then runs identically on every rank (same reduced gradients,
+same deterministic update), so no parameter broadcast is needed after the first sync.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def shard_range(B_global: int, rank: int, world: int):
+    """Contiguous shard [lo, hi) of the global batch owned by `rank` (equal shards when divisible)."""
+    base, rem = divmod(B_global, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def broadcast_params(module: torch.nn.Module, src: int = 0, group=None) -> None:
+    """Make every rank start from rank `src`'s controller weights."""
+    for p in module.parameters():
+        dist.broadcast(p.data, src=src, group=group)
+
+
+class GradAllReduce:
+    """Callable grad hook for NeuralNetwork.train_model(grad_sync=...).
+
+    Each rank's loss is the mean over its B_local trajectories; the global loss is the mean over
+    B_global = sum(B_local). So each rank scales its gradient by B_local / B_global before the SUM
+    all-reduce, which makes the reduced gradient exactly d(global mean)/d(theta).
+    """
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def __call__(self, module: torch.nn.Module, b_local: int | None = None, b_global: int | None = None,
+                 loss: torch.Tensor | None = None):
+        params = [p for p in module.parameters() if p.grad is not None]
+        if not params:
+            return loss
+        world = dist.get_world_size(self.group)
+        scale = (b_local / b_global) if (b_local is not None and b_global) else 1.0 / world
+        flat = torch.cat([p.grad.reshape(-1) for p in params]
+                         + ([loss.detach().reshape(1)] if loss is not None else []))
+        flat.mul_(scale)
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+        off = 0
+        for p in params:
+            n = p.grad.numel()
+            p.grad.copy_(flat[off:off + n].view_as(p.grad))
+            off += n
+        return flat[off] if loss is not None else None

@@ -1,0 +1,196 @@
+"""Host-side mirror of the reference's hot-path interface (Unsupervised Learning/Functions.py).
+
+Same class names, constructor/forward signatures, parameter names (so reference ``state_dict``s load
+unchanged) and return conventions as the reference; the rollout inside :class:`MPCLoss` runs on the
+gfx950 kernels through :mod:`.rollout` — there is no CPU path for it.
+
+* :class:`FNNModel`     <- Functions.py:215-289
+* :class:`LSTMModel`    <- Functions.py:295-379
+* :class:`MPCLoss`      <- Functions.py:1336-1472 (the hot path, now HIP)
+* :class:`NeuralNetwork` train_model / validate_model / train_loop <- Functions.py:594-717, 825-923
+"""
+from __future__ import annotations
+
+import logging
+import time
+
+import torch
+from torch import nn
+
+from .rollout import rollout
+
+logger = logging.getLogger("forging_control_amd")
+
+
+class FNNModel(nn.Module):
+    """Controller: Linear(in->hidden)+act, (width-1) x [Linear(hidden->hidden)+act], Linear(hidden->out,
+    no bias), Hardtanh. Xavier-normal weights, zero biases (Functions.py:239-259)."""
+
+    def __init__(self, input_dim: int, hidden_dim: int, output_dim: int, width_dim: int,
+                 activation_fn=nn.ReLU, bias=True):
+        super().__init__()
+        self.width_dim = width_dim
+        self.activation = activation_fn()
+        self.constraint = nn.Hardtanh()
+        self.fc_inp = nn.Linear(input_dim, hidden_dim, bias=bias)
+        self.fc_int = nn.Linear(hidden_dim, hidden_dim, bias=bias)
+        self.fc_out = nn.Linear(hidden_dim, output_dim, bias=False)
+        for layer in (self.fc_inp, self.fc_int, self.fc_out):
+            nn.init.xavier_normal_(layer.weight)
+        for layer in (self.fc_inp, self.fc_int):
+            if layer.bias is not None:
+                nn.init.zeros_(layer.bias)
+
+    def forward(self, x):
+        y = self.activation(self.fc_inp(x))
+        for _ in range(self.width_dim - 1):
+            y = self.activation(self.fc_int(y))
+        return self.constraint(self.fc_out(y))
+
+
+class LSTMModel(nn.Module):
+    """Plant surrogate: stacked ``nn.LSTM`` (batch-first, no bias by default) from a zero state, then a
+    linear readout of the last step (Functions.py:317-379)."""
+
+    def __init__(self, input_dim: int, hidden_dim: int, output_dim: int, layer_dim: int, bias=False,
+                 device: torch.device = "cpu"):
+        super().__init__()
+        self.hidden_dim = hidden_dim
+        self.layer_dim = layer_dim
+        self.lstm = nn.LSTM(input_dim, hidden_dim, layer_dim, batch_first=True, bias=bias)
+        self.fc = nn.Linear(hidden_dim, output_dim)
+
+    def initialize_hidden_states(self, batch_size: int, device: torch.device):
+        shape = (self.layer_dim, batch_size, self.hidden_dim)
+        return (torch.zeros(shape, device=device).requires_grad_(),
+                torch.zeros(shape, device=device).requires_grad_())
+
+    def forward(self, x: torch.Tensor, device: torch.device):
+        h0, c0 = self.initialize_hidden_states(x.shape[0], device)
+        seq, _ = self.lstm(x, (h0.detach(), c0.detach()))
+        return self.fc(seq[:, -1, :])
+
+
+def _controller_params(controller):
+    if not isinstance(controller, FNNModel) and not all(hasattr(controller, a) for a in ("fc_inp", "fc_out")):
+        raise TypeError("MPCLoss: controller must be an FNNModel (fc_inp / fc_out)")
+    if getattr(controller, "width_dim", 1) != 1:
+        raise NotImplementedError("MPCLoss rollout kernel is built for width_dim=1 (UL/Main.py:183)")
+    if not isinstance(getattr(controller, "activation", nn.ReLU()), nn.ReLU):
+        raise NotImplementedError("MPCLoss rollout kernel is built for the ReLU controller (UL/Main.py:188)")
+    if controller.fc_inp.bias is None:
+        raise NotImplementedError("MPCLoss rollout kernel expects fc_inp with bias (UL/Main.py:188)")
+    return controller.fc_inp.weight, controller.fc_inp.bias, controller.fc_out.weight
+
+
+def _simulator_params(simulator):
+    lstm = simulator.lstm
+    if lstm.bias:
+        raise NotImplementedError("MPCLoss rollout kernel is built for the bias-free LSTM (Functions.py:317)")
+    if lstm.num_layers != 3 or lstm.input_size != 5 or simulator.fc.out_features != 4:
+        raise NotImplementedError("MPCLoss rollout kernel is built for LSTM(5, H, 3) -> Linear(H, 4)")
+    w_ih = [getattr(lstm, f"weight_ih_l{k}") for k in range(3)]
+    w_hh = [getattr(lstm, f"weight_hh_l{k}") for k in range(3)]
+    return w_ih, w_hh, simulator.fc.weight, simulator.fc.bias
+
+
+class MPCLoss(nn.Module):
+    """Drop-in for the reference MPCLoss (Functions.py:1336-1472): the N-step closed-loop rollout of the
+    controller through the LSTM surrogate and its quadratic speed-tracking cost, fused on gfx950.
+
+    ``forward`` returns ``(loss, {'loss', 'command', 'error', 'prediction'})`` with the reference's
+    shapes. ``enable_noise`` draws ``randn_like(x0) * 0.01`` per horizon step from the device's default
+    generator in the reference's order (Functions.py:1401, 1439); a pre-drawn ``noise`` (B, N, 4) can be
+    passed instead. After each call ``self.last_trajectory`` holds the (B, N, 4) LSTM predictions.
+    """
+
+    def __init__(self, prediction_horizon=10, alpha=0.1):
+        super().__init__()
+        self.N = prediction_horizon
+        self.alpha = alpha
+        self.activation = nn.ReLU()
+        self.last_trajectory = None
+
+    def forward(self, simulator: nn.Module, controller: nn.Module, input_controller: torch.Tensor,
+                output_controller: torch.Tensor, states: torch.Tensor, device: torch.device,
+                enable_noise=False, noise: torch.Tensor | None = None):
+        X = input_controller
+        dev = torch.device(device)
+        if dev.type != X.device.type or (dev.index is not None and dev.index != X.device.index):
+            raise RuntimeError(f"MPCLoss: inputs are on {X.device}, device argument is {device}")
+        B = X.shape[0]
+        if enable_noise and noise is None:
+            noise = torch.stack([torch.randn(B, 4, device=X.device) * 0.01 for _ in range(self.N)], dim=1)
+        elif not enable_noise:
+            noise = None
+        loss, cost, command, error, prediction, xhat = rollout(
+            X, output_controller, states, _controller_params(controller), _simulator_params(simulator),
+            self.N, self.alpha, noise)
+        self.last_trajectory = xhat
+        return loss, {"loss": cost, "command": command, "error": error, "prediction": prediction}
+
+
+class NeuralNetwork:
+    """Training driver with the reference's call surface (Functions.py:594-923)."""
+
+    @staticmethod
+    def train_model(data_loader, simulator, model, loss_function, optimizer, device, enable_noise=False,
+                    grad_sync=None):
+        """One epoch (Functions.py:594-676). ``grad_sync`` (optional) is called between backward and the
+        optimizer step — the data-parallel hook (see :mod:`.distributed`)."""
+        model.train()
+        total = 0.0
+        feats = {"loss": [], "command": [], "error": [], "prediction": []}
+        n_batches = 0
+        for X, _, z in data_loader:
+            X, z = X.to(device), z.to(device)
+            optimizer.zero_grad()
+            output = model(X)
+            loss, f = loss_function(simulator, model, X, output, z, device, enable_noise)
+            for k in feats:
+                feats[k].append(f[k])
+            loss.backward()
+            if grad_sync is not None:
+                grad_sync(model)
+            optimizer.step()
+            total += loss.item()
+            n_batches += 1
+        feats = {k: torch.cat(v, dim=0) for k, v in feats.items()}
+        return total / max(n_batches, 1), feats
+
+    @staticmethod
+    def validate_model(data_loader, model, loss_function, device):
+        """Controller-only validation loss (Functions.py:679-717)."""
+        model.eval()
+        total = 0.0
+        n = 0
+        with torch.no_grad():
+            for X, y, _ in data_loader:
+                X, y = X.to(device), y.to(device)
+                total += loss_function(model(X), y).item()
+                n += 1
+        return total / max(n, 1)
+
+    @staticmethod
+    def train_loop(controller, simulator, train_loader, val_loader, loss_function, optimizer, n_epochs,
+                   device, enable_noise=False, grad_sync=None):
+        """Epoch loop (Functions.py:825-923); returns (controller, train losses, val losses, seconds,
+        stacked loss features)."""
+        NeuralNetwork.validate_model(val_loader, controller, nn.MSELoss(), device)
+        t_losses, v_losses = [], []
+        stacked = {"loss": [], "command": [], "error": [], "prediction": []}
+        t0 = time.time()
+        for epoch in range(n_epochs):
+            tl, f = NeuralNetwork.train_model(train_loader, simulator, controller, loss_function, optimizer,
+                                              device, enable_noise, grad_sync)
+            vl = NeuralNetwork.validate_model(val_loader, controller, nn.MSELoss(), device)
+            if n_epochs >= 10 and epoch % (n_epochs // 10) == 0 or epoch == n_epochs - 1:
+                logger.info("[%.1f%%] Training loss: %.4f,  Validation loss: %.4f",
+                            100.0 * epoch / n_epochs, tl, vl)
+            t_losses.append(tl)
+            v_losses.append(vl)
+            for k in stacked:
+                stacked[k].append(f[k].detach())
+        elapsed = time.time() - t0
+        stacked = {k: torch.stack(v, dim=0) for k, v in stacked.items()}
+        return controller, t_losses, v_losses, elapsed, stacked

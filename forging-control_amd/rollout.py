@@ -1,0 +1,125 @@
+"""torch.autograd.Function over the gfx950 rollout kernels (C ABI in include/fcr.h).
+
+Forward  = MPCLoss.forward  (/root/reference/Unsupervised Learning/Functions.py:1353-1472)
+Backward = what loss.backward() (Functions.py:655) delivers for it: d loss/d u0 (flows on into the
+caller's ``controller(X)`` graph) and the gradients of the controller parameters used inside the
+loss. The frozen LSTM's weight gradients are not produced (the reference computes them but nothing
+consumes them: UL/Main.py:195 optimises the controller only).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _native
+
+WINDOW_ROWS = 10   # Functions.py:1434 hard-codes the 10-row window
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def make_dims(B, N, H, layers, ctrl_hidden, alpha, in_dim=5, out_dim=4, ctrl_in=3, L=WINDOW_ROWS):
+    return _native.FcrDims(B, N, L, H, layers, in_dim, out_dim, ctrl_in, ctrl_hidden, float(alpha))
+
+
+def _dev_f32(t, name):
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name}: expected float32, got {t.dtype}")
+    return t.contiguous()
+
+
+class RolloutFn(torch.autograd.Function):
+    """Inputs: X (B,3), u0 (B,1), states (B,10,5), noise (B,N,4) or None, controller params
+    (W_inp, b_inp, W_out), LSTM weights (w_ih0..2, w_hh0..2, fc_w, fc_b), N, alpha.
+    Outputs: loss (0-d), cost (B,), command (B,), error (B,), prediction (B*N,), xhat (B,N,4)."""
+
+    @staticmethod
+    def forward(ctx, X, u0, states, noise, W_inp, b_inp, W_out, w_ih0, w_ih1, w_ih2, w_hh0, w_hh1,
+                w_hh2, fc_w, fc_b, N, alpha):
+        lib = _native.load()
+        dev = X.device
+        B = X.shape[0]
+        H = w_hh0.shape[1]
+        dims = make_dims(B, N, H, 3, W_inp.shape[0], alpha)
+        need_grad = any(ctx.needs_input_grad[i] for i in (1, 4, 5, 6))
+        ws = torch.empty(_native.workspace_bytes(dims, need_grad), dtype=torch.uint8, device=dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        loss = torch.empty((), **f32)
+        cost = torch.empty(B, **f32)
+        command = torch.empty(B, **f32)
+        error = torch.empty(B, **f32)
+        prediction = torch.empty(B * N, **f32)
+        xhat = torch.empty(B, N, 4, **f32)
+        w = _native.FcrWeights()
+        keep = [t.contiguous() for t in (W_inp, b_inp, W_out, w_ih0, w_ih1, w_ih2, w_hh0, w_hh1, w_hh2,
+                                         fc_w, fc_b)]
+        w.ctrl_w_inp, w.ctrl_b_inp, w.ctrl_w_out = (t.data_ptr() for t in keep[0:3])
+        for l in range(3):
+            w.w_ih[l] = keep[3 + l].data_ptr()
+            w.w_hh[l] = keep[6 + l].data_ptr()
+        w.fc_w, w.fc_b = keep[9].data_ptr(), keep[10].data_ptr()
+        Xc, u0c, stc = X.contiguous(), u0.contiguous(), states.contiguous()
+        nzc = noise.contiguous() if noise is not None else None
+        _native.check(lib.fcr_forward(ctypes.byref(dims), ctypes.byref(w), _ptr(Xc), _ptr(u0c), _ptr(stc),
+                                      _ptr(nzc), _ptr(loss), _ptr(cost), _ptr(command), _ptr(error),
+                                      _ptr(prediction), _ptr(xhat), int(need_grad), _ptr(ws), ws.numel(),
+                                      _stream(dev)), "fcr_forward")
+        ctx.mark_non_differentiable(cost, command, error, prediction, xhat)
+        if need_grad:
+            ctx.ws = ws
+            ctx.dims = dims
+            ctx.save_for_backward(Xc, stc, prediction)
+            ctx.ctrl_shapes = (W_inp.shape, b_inp.shape, W_out.shape)
+        return loss, cost, command, error, prediction, xhat
+
+    @staticmethod
+    def backward(ctx, g_loss, *unused):
+        lib = _native.load()
+        Xc, stc, prediction = ctx.saved_tensors
+        dev = Xc.device
+        B = Xc.shape[0]
+        f32 = dict(dtype=torch.float32, device=dev)
+        g_u0 = torch.empty(B, 1, **f32)
+        s_wi, s_bi, s_wo = ctx.ctrl_shapes
+        g_wi = torch.empty(s_wi, **f32)
+        g_bi = torch.empty(s_bi, **f32)
+        g_wo = torch.empty(s_wo, **f32)
+        dl = g_loss.detach().to(torch.float32).reshape(1).contiguous()
+        _native.check(lib.fcr_backward(ctypes.byref(ctx.dims), _ptr(Xc), _ptr(stc), _ptr(prediction), _ptr(dl),
+                                       _ptr(g_u0), _ptr(g_wi), _ptr(g_bi), _ptr(g_wo), _ptr(ctx.ws),
+                                       ctx.ws.numel(), _stream(dev)), "fcr_backward")
+        ctx.ws = None   # release the activation slab as early as autograd lets us
+        return (None, g_u0, None, None, g_wi, g_bi, g_wo) + (None,) * 10
+
+
+def rollout(X, u0, states, ctrl_params, lstm_params, N, alpha, noise=None):
+    """Functional entry: ctrl_params = (W_inp, b_inp, W_out), lstm_params = (w_ih[3], w_hh[3], fc_w, fc_b)."""
+    w_ih, w_hh, fc_w, fc_b = lstm_params
+    dev = X.device
+    if dev.type != "cuda":
+        raise RuntimeError("forging-control_amd rollout runs on a ROCm device only (got %s); the CPU "
+                           "restatement in oracle/ is test infrastructure, not a fallback" % dev)
+    tensors = [X, u0, states] + list(ctrl_params) + list(w_ih) + list(w_hh) + [fc_w, fc_b]
+    for t in tensors:
+        if t.device != dev:
+            raise RuntimeError(f"all rollout tensors must be on {dev}, found one on {t.device}")
+    if states.dim() != 3 or states.shape[1] != WINDOW_ROWS or states.shape[2] != 5:
+        raise ValueError(f"states must be (B, 10, 5), got {tuple(states.shape)}")
+    B = X.shape[0]
+    if X.shape != (B, 3) or u0.numel() != B:
+        raise ValueError(f"X must be (B,3) and u0 (B,1); got {tuple(X.shape)}, {tuple(u0.shape)}")
+    if noise is not None and noise.shape != (B, N, 4):
+        raise ValueError(f"noise must be (B, N, 4) = {(B, N, 4)}, got {tuple(noise.shape)}")
+    u0 = u0.reshape(B, 1)
+    return RolloutFn.apply(_dev_f32(X, "X"), _dev_f32(u0, "u0"), _dev_f32(states, "states"),
+                           None if noise is None else _dev_f32(noise, "noise"),
+                           *[_dev_f32(t, "controller param") for t in ctrl_params],
+                           *[_dev_f32(t, "lstm weight") for t in list(w_ih) + list(w_hh) + [fc_w, fc_b]],
+                           int(N), float(alpha))

@@ -1,0 +1,115 @@
+/*
+ * fcr.h — C ABI of the MI355X-native (gfx950) unsupervised-MPC rollout engine.
+ *
+ * This library replaces the work torch dispatches inside ONE Python call of the reference,
+ *
+ *     loss, loss_features = loss_function(simulator, model, X, output, z, device, enable_noise)
+ *     ...
+ *     loss.backward()
+ *
+ * at /root/reference/Unsupervised Learning/Functions.py:646 and :655 (MPCLoss.forward,
+ * Functions.py:1353-1472, plus its autograd backward). The reference has no FFI of its own (it is
+ * pure Python/PyTorch); the binding a maintainer adds is the ctypes stub in INTEGRATION.md, and the
+ * Python drop-in `MPCLoss` in forging-control_amd/functions.py is that stub.
+ *
+ * Conventions (all entry points):
+ *   - every pointer is caller-owned DEVICE memory (fp32, contiguous, batch-first exactly as the
+ *     reference lays it out), except `dims`/`w` (host structs);
+ *   - `stream` is a hipStream_t (passed as void* so this header needs no HIP headers); all work is
+ *     stream-ordered on it, nothing synchronises the host;
+ *   - no allocation inside a call: scratch comes from `ws` (size from fcr_workspace_size);
+ *   - return FCR_OK (0) or a negative FCR_E* code; fcr_last_error() (thread-local) explains it.
+ */
+#ifndef FCR_H
+#define FCR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FCR_ABI_VERSION 1
+
+enum {
+    FCR_OK = 0,
+    FCR_EINVAL = -1,      /* bad dims, null pointer, misalignment            */
+    FCR_EWORKSPACE = -2,  /* ws too small                                      */
+    FCR_EHIP = -3,        /* a HIP runtime call failed                         */
+    FCR_EUNSUPPORTED = -4 /* dims valid for the reference but not built here   */
+};
+
+/* Problem shape. Reference values: L=10 (Functions.py:1434 hard-codes the 10-row window),
+ * layers=3 / H=50 / in_dim=5 / out_dim=4 (UL/Main.py:144-154), ctrl 3->50->1 (UL/Main.py:183-188),
+ * N = n_horizon = 10 (UL/template_mpc.py:20), alpha = 20.0 (UL/Main.py:192). */
+typedef struct fcr_dims {
+    int32_t B;           /* trajectories in the batch                         */
+    int32_t N;           /* prediction horizon (MPCLoss.N)                    */
+    int32_t L;           /* lookback rows of the LSTM window (must be 10)     */
+    int32_t H;           /* LSTM hidden size (built: 16, 32, 50, 64)          */
+    int32_t layers;      /* LSTM layers (must be 3)                           */
+    int32_t in_dim;      /* LSTM input features (must be 5)                   */
+    int32_t out_dim;     /* LSTM outputs (must be 4)                          */
+    int32_t ctrl_in;     /* controller inputs (must be 3)                     */
+    int32_t ctrl_hidden; /* controller hidden units (<= 52)                   */
+    float alpha;         /* MPCLoss.alpha, command-variation weight            */
+} fcr_dims;
+
+/* Weights, torch layouts (row-major, as state_dict holds them). */
+typedef struct fcr_weights {
+    const float *ctrl_w_inp; /* FNNModel.fc_inp.weight (ctrl_hidden, ctrl_in)  Functions.py:249 */
+    const float *ctrl_b_inp; /* FNNModel.fc_inp.bias   (ctrl_hidden)                            */
+    const float *ctrl_w_out; /* FNNModel.fc_out.weight (1, ctrl_hidden), no bias Functions.py:251 */
+    const float *w_ih[3];    /* LSTMModel.lstm.weight_ih_l{0,1,2} (4H, in_dim | H)  :325        */
+    const float *w_hh[3];    /* LSTMModel.lstm.weight_hh_l{0,1,2} (4H, H)                       */
+    const float *fc_w;       /* LSTMModel.fc.weight (out_dim, H)                     :329        */
+    const float *fc_b;       /* LSTMModel.fc.bias   (out_dim)                                    */
+} fcr_weights;
+
+/* Bytes of scratch a forward (+ backward when with_backward != 0) needs for `dims`. */
+int fcr_workspace_size(const fcr_dims *dims, int with_backward, size_t *bytes);
+
+/*
+ * Forward rollout = MPCLoss.forward (Functions.py:1353-1472).
+ *   X        (B,3)   input_controller [y_dot, z, ref]          (Functions.py:1353, ref = X[:,-1] :1392)
+ *   u0       (B,1)   output_controller = controller(X)          (Functions.py:643)
+ *   states   (B,L,5) LSTM window [y_dot,p1,p2,z,u]              (Functions.py:1395)
+ *   noise    (B,N,4) additive LSTM-output noise, or NULL        (Functions.py:1400-1402,1438-1440)
+ * Outputs:
+ *   loss (1) mean cost; cost/command/error (B) = loss_features['loss'|'command'|'error'];
+ *   prediction (B*N) sample-major = loss_features['prediction']  (Functions.py:1466);
+ *   xhat (B,N,4) per-step LSTM predictions (closed-loop state trajectory), or NULL.
+ * with_backward != 0 keeps the activations fcr_backward needs in `ws` (which must then not be
+ * reused until fcr_backward has run).
+ */
+int fcr_forward(const fcr_dims *dims, const fcr_weights *w,
+                const float *X, const float *u0, const float *states, const float *noise,
+                float *loss, float *cost, float *command, float *error,
+                float *prediction, float *xhat,
+                int with_backward, void *ws, size_t ws_bytes, void *stream);
+
+/*
+ * Backward of the last fcr_forward(with_backward=1) on the same `ws` = what loss.backward()
+ * (Functions.py:655) delivers: d loss/d u0 (B,1) — handed back to the caller's controller(X) graph —
+ * and the gradients of the controller parameters used inside the loss. `dloss` is a DEVICE pointer
+ * to the incoming scalar gradient (no host sync). LSTM weight gradients are not computed (the
+ * reference computes them but nothing reads them: UL/Main.py:195 optimises only the controller).
+ * Parameter gradients are OVERWRITTEN (not accumulated); reduction order is fixed (deterministic).
+ */
+int fcr_backward(const fcr_dims *dims,
+                 const float *X, const float *states, const float *prediction,
+                 const float *dloss,
+                 float *g_u0, float *g_w_inp, float *g_b_inp, float *g_w_out,
+                 void *ws, size_t ws_bytes, void *stream);
+
+/* Thread-local description of the last error (never NULL). */
+const char *fcr_last_error(void);
+
+/* FCR_ABI_VERSION of the loaded library. */
+int fcr_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FCR_H */

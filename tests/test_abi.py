@@ -1,0 +1,78 @@
+"""CPU: the C-ABI library loads, exports exactly what include/fcr.h declares, and validates dims
+(no compute calls: there is no GPU here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import forging_control_amd as fca
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "fcr.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(fcr_\w+)\s*\(", text, re.M)))
+
+
+def test_header_declares_the_five_entry_points():
+    assert declared_symbols() == sorted(fca._native.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = fca._native.load()
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", fca._native.LIB_PATH], capture_output=True, text=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l and l.split()[-1].startswith("fcr_")}
+    assert exported == set(declared_symbols())
+
+
+def test_library_targets_gfx950():
+    blob = open(fca._native.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_abi_version():
+    assert fca._native.load().fcr_abi_version() == fca._native.ABI_VERSION
+
+
+def dims(**kw):
+    base = dict(B=65536, N=10, H=50, layers=3, ctrl_hidden=50, alpha=20.0)
+    base.update(kw)
+    return fca.rollout.make_dims(base["B"], base["N"], base["H"], base["layers"], base["ctrl_hidden"], base["alpha"])
+
+
+def test_workspace_size_scales_with_batch_and_backward():
+    small = fca._native.workspace_bytes(dims(B=64), True)     # 4 waves of 16 trajectories
+    big = fca._native.workspace_bytes(dims(B=65536), True)    # 4096 waves
+    fwd_only = fca._native.workspace_bytes(dims(B=65536), False)
+    assert 0.97 * 1024 * small < big < 1.01 * 1024 * small   # fixed fragment blocks are the slack
+    # activations of 10 windows x 30 cells x 52 slots x (i,f,g,o,c) fp32 per trajectory
+    assert big > 65536 * 10 * 30 * 52 * 5 * 4
+    assert fwd_only < big / 100
+
+
+@pytest.mark.parametrize("kw,code", [
+    (dict(B=0), -1), (dict(N=0), -1), (dict(H=48), -4), (dict(layers=2), -4), (dict(ctrl_hidden=80), -4),
+])
+def test_invalid_dims_rejected_with_message(kw, code):
+    lib = fca._native.load()
+    out = ctypes.c_size_t(0)
+    d = dims(**kw)
+    rc = lib.fcr_workspace_size(ctypes.byref(d), 1, ctypes.byref(out))
+    assert rc == code
+    assert lib.fcr_last_error().decode()
+
+
+def test_null_pointers_rejected_before_any_device_call():
+    lib = fca._native.load()
+    d = dims(B=16)
+    w = fca._native.FcrWeights()
+    rc = lib.fcr_forward(ctypes.byref(d), ctypes.byref(w), *([None] * 10), 1, None, 0, None)
+    assert rc == -1 and "NULL" in lib.fcr_last_error().decode()
+    rc = lib.fcr_backward(ctypes.byref(d), *([None] * 8), None, 0, None)
+    assert rc == -1

@@ -1,0 +1,95 @@
+"""CPU: host-side mirror of the reference interface and the data-parallel plumbing."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import forging_control_amd as fca
+from conftest import GOLDEN
+
+
+def test_reference_state_dicts_load_into_mirror_modules():
+    w = np.load(os.path.join(GOLDEN, "weights_ref.npz"))
+    sim = fca.LSTMModel(5, 50, 4, 3)
+    sd = {f"lstm.weight_ih_l{k}": torch.tensor(w[f"Wih{k}"]) for k in range(3)}
+    sd.update({f"lstm.weight_hh_l{k}": torch.tensor(w[f"Whh{k}"]) for k in range(3)})
+    sd.update({"fc.weight": torch.tensor(w["fcW"]), "fc.bias": torch.tensor(w["fcb"])})
+    sim.load_state_dict(sd)          # strict: same keys as UL/Model_NN/results/model_NN.pt
+    ctrl = fca.FNNModel(3, 50, 1, 1, torch.nn.ReLU, bias=True)
+    keys = set(ctrl.state_dict())
+    assert keys == {"fc_inp.weight", "fc_inp.bias", "fc_int.weight", "fc_int.bias", "fc_out.weight"}
+
+
+def test_fnn_forward_matches_oracle():
+    from oracle import rollout_np as R
+    torch.manual_seed(0)
+    ctrl = fca.FNNModel(3, 50, 1, 1)
+    x = torch.randn(64, 3, dtype=torch.float64) * 3
+    ctrl = ctrl.double()
+    u_np, _ = R.fnn_forward(x.numpy(), ctrl.fc_inp.weight.detach().numpy(), ctrl.fc_inp.bias.detach().numpy(),
+                            ctrl.fc_out.weight.detach().numpy())
+    assert np.allclose(ctrl(x).detach().numpy()[:, 0], u_np, atol=1e-14)
+
+
+def test_mpcloss_refuses_cpu_tensors():
+    """No CPU fallback: the product path runs on the ROCm device or raises."""
+    sim = fca.LSTMModel(5, 50, 4, 3)
+    ctrl = fca.FNNModel(3, 50, 1, 1)
+    X = torch.zeros(4, 3)
+    with pytest.raises(RuntimeError, match="ROCm device only"):
+        fca.MPCLoss(10, 20.0)(sim, ctrl, X, ctrl(X), torch.zeros(4, 10, 5), "cpu")
+
+
+def test_mpcloss_rejects_unsupported_models():
+    sim = fca.LSTMModel(5, 50, 4, 3, bias=True)
+    ctrl = fca.FNNModel(3, 50, 1, 1)
+    with pytest.raises(NotImplementedError):
+        fca.functions._simulator_params(sim)
+    with pytest.raises(NotImplementedError):
+        fca.functions._controller_params(fca.FNNModel(3, 50, 1, 2))
+
+
+def test_shard_range_partitions_batch():
+    for B, W in [(65536, 8), (15, 4), (7, 8)]:
+        spans = [fca.distributed.shard_range(B, r, W) for r in range(W)]
+        assert spans[0][0] == 0 and spans[-1][1] == B
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+        assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+def _dp_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    model = fca.FNNModel(3, 50, 1, 1)
+    B_global = 12
+    lo, hi = fca.distributed.shard_range(B_global, rank, world)
+    g = torch.Generator().manual_seed(1)
+    X = torch.randn(B_global, 3, generator=g)
+    # local mean loss over the shard; the all-reduced grad must equal the global-mean grad
+    loss = model(X[lo:hi]).pow(2).mean()
+    loss.backward()
+    red_loss = fca.distributed.GradAllReduce()(model, hi - lo, B_global, loss)
+    out[rank] = (torch.cat([p.grad.reshape(-1) for p in model.parameters() if p.grad is not None]).numpy(),
+                 float(red_loss))
+    dist.destroy_process_group()
+
+
+def test_grad_allreduce_equals_global_mean_gloo_world2():
+    port = 29500 + os.getpid() % 1000
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_dp_worker, args=(2, port, out), nprocs=2, join=True)
+        res = dict(out)
+    torch.manual_seed(0)
+    model = fca.FNNModel(3, 50, 1, 1)
+    X = torch.randn(12, 3, generator=torch.Generator().manual_seed(1))
+    loss = model(X).pow(2).mean()
+    loss.backward()
+    ref = torch.cat([p.grad.reshape(-1) for p in model.parameters() if p.grad is not None]).numpy()
+    for r in (0, 1):
+        assert np.allclose(res[r][0], ref, atol=1e-6)
+        assert abs(res[r][1] - loss.item()) < 1e-6
