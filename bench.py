@@ -46,6 +46,19 @@ def hbm_bytes_per_rollout_step(N=10):
     return (12 + 200 + 3 * 4 + 4 * N) / N
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/r*_pmc.json, collected by scripts/profile.sh on this workload), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    if kernel not in d:
+        return None, None
+    return d[kernel]["hbm_bytes_corrected"], os.path.basename(files[-1])
+
+
 def load_weights(dev, H):
     if H == 50:
         w = np.load(os.path.join(ROOT, "tests", "golden", "weights_ref.npz"))
@@ -199,6 +212,7 @@ def main():
         dom = ("bwd", b_ms) if b_ms >= f_ms else ("fwd", f_ms)
         achieved = B * N * fl[dom[0]] / (dom[1] * 1e-3) / 1e12
         hbm_roof = HBM_PEAK_GBS * 1e9 / hbm_bytes_per_rollout_step(N)
+        traffic, traffic_src = pmc_traffic(f"fcr_{dom[0]}_kernel") if (B, N, H) == (65536, 10, 50) else (None, None)
         line = {
             "metric": "rollout-steps/s (batch x horizon), fwd+bwd+AdamW step",
             "value": value, "unit": "rollout-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -209,7 +223,7 @@ def main():
                        "hidden": H, "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "kernel": f"fcr_{dom[0]}_kernel", "achieved": achieved,
                          "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
-                         "traffic": None},
+                         "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src},
             "kernels_ms": {"fwd": f_ms, "bwd": b_ms},
             "hbm_roofline_frac": value / world / hbm_roof,
             "loss": float(loss.item()),
