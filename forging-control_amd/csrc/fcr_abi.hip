@@ -30,7 +30,8 @@ int fail(int code, const char *fmt, ...) {
 
 struct Layout {
     int HS, nw, nw_pad, NB0, NB1;
-    size_t fa[3], ba[3], fcp, fcb, fnp, xhat, loss_part, fnn_part, gates, cstore, dseq, total;
+    size_t fa[3], ba[3], fcp, fcb, fnp, xhat, dv, loss_part, fnn_part, gates, cstore, dseq, dxrow, total;
+    int ctrl_blocks;
 };
 
 size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -46,8 +47,8 @@ int check_dims(const fcr_dims *d) {
                     d->out_dim, d->ctrl_in);
     if (d->ctrl_hidden < 1 || d->ctrl_hidden > 4 * kMS)
         return fail(FCR_EUNSUPPORTED, "ctrl_hidden=%d: built for 1..52", d->ctrl_hidden);
-    if (!(d->H == 16 || d->H == 32 || d->H == 50 || d->H == 64))
-        return fail(FCR_EUNSUPPORTED, "H=%d: built for 16, 32, 50, 64", d->H);
+    if (!(d->H == 16 || d->H == 32 || d->H == 50))
+        return fail(FCR_EUNSUPPORTED, "H=%d: built for 16, 32, 50 (LDS-resident fragments)", d->H);
     if ((long long)d->B * d->N > (1LL << 31)) return fail(FCR_EINVAL, "B*N too large");
     return FCR_OK;
 }
@@ -79,12 +80,16 @@ Layout make_layout(const fcr_dims *d, int with_backward) {
     L.fnp = take(sizeof(float) * kMS * 4 * kFnpStride);
     L.xhat = take(sizeof(float) * (size_t)d->B * d->N * kOut);
     L.loss_part = take(sizeof(float) * L.nw_pad);
-    L.fnn_part = take(sizeof(float) * (size_t)L.nw_pad * d->ctrl_hidden * 5);
+    L.dv = take(sizeof(float) * (size_t)d->B * d->N);
+    L.ctrl_blocks = (int)(((long long)d->B * d->N + kCtrlItems - 1) / kCtrlItems);
+    L.fnn_part = take(sizeof(float) * (size_t)L.ctrl_blocks * d->ctrl_hidden * 5);
+    // sequence hand-off slab: forward h of layers 0/1, then (same addresses) backward dx of layers 2/1
+    L.dseq = take(sizeof(f32x4) * (size_t)L.nw_pad * d->N * 2 * kL * ((HS + 3) / 4) * kWave);
     if (with_backward) {
         const size_t cells = (size_t)L.nw_pad * d->N * kLayers * kL * HS * kWave;
         L.gates = take(sizeof(f32x4) * cells);
-        L.cstore = take(sizeof(float) * cells);
-        L.dseq = take(sizeof(float) * (size_t)L.nw_pad * d->N * 2 * kL * HS * kWave);
+        L.cstore = take(sizeof(f32x2) * cells);
+        L.dxrow = take(sizeof(f32x2) * (size_t)L.nw_pad * d->N * kL * kWave);
     }
     L.total = off;
     return L;
@@ -227,14 +232,14 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
     fa.xhat_user = xhat;
     fa.xhat_ws = (float *)(base + L.xhat);
     fa.loss_part = (float *)(base + L.loss_part);
+    fa.hseq = (f32x4 *)(base + L.dseq);
     fa.gates = with_backward ? (f32x4 *)(base + L.gates) : nullptr;
-    fa.cstore = with_backward ? (float *)(base + L.cstore) : nullptr;
+    fa.cstore = with_backward ? (f32x2 *)(base + L.cstore) : nullptr;
     fa.p = packed_ptrs(L, base);
     switch (d->H) {
         case 16: rc = launch_fwd<4>(fa, L, s); break;
         case 32: rc = launch_fwd<8>(fa, L, s); break;
         case 50: rc = launch_fwd<13>(fa, L, s); break;
-        case 64: rc = launch_fwd<16>(fa, L, s); break;
         default: rc = fail(FCR_EUNSUPPORTED, "H=%d", d->H);
     }
     if (rc) return rc;
@@ -267,21 +272,25 @@ int fcr_backward(const fcr_dims *d, const float *X, const float *states, const f
     ba.xhat = (const float *)(base + L.xhat);
     ba.dloss = dloss;
     ba.gates = (const f32x4 *)(base + L.gates);
-    ba.cstore = (const float *)(base + L.cstore);
-    ba.dseq = (float *)(base + L.dseq);
+    ba.cstore = (const f32x2 *)(base + L.cstore);
+    ba.dseq = (f32x4 *)(base + L.dseq);
+    ba.dxrow = (f32x2 *)(base + L.dxrow);
     ba.g_u0 = g_u0;
-    ba.fnn_part = (float *)(base + L.fnn_part);
+    ba.dv = (float *)(base + L.dv);
     ba.p = packed_ptrs(L, base);
     switch (d->H) {
         case 16: rc = launch_bwd<4>(ba, L, s); break;
         case 32: rc = launch_bwd<8>(ba, L, s); break;
         case 50: rc = launch_bwd<13>(ba, L, s); break;
-        case 64: rc = launch_bwd<16>(ba, L, s); break;
         default: rc = fail(FCR_EUNSUPPORTED, "H=%d", d->H);
     }
     if (rc) return rc;
-    hipLaunchKernelGGL(grad_reduce_kernel, dim3(d->ctrl_hidden * 5), dim3(256), 0, s,
-                       (const float *)ba.fnn_part, L.nw_pad, d->ctrl_hidden, g_w_inp, g_b_inp, g_w_out);
+    float *part = (float *)(base + L.fnn_part);
+    hipLaunchKernelGGL(ctrl_grad_kernel, dim3(L.ctrl_blocks), dim3(kCtrlBlock), 0, s, X, ba.xhat,
+                       (const float *)ba.dv, ba.p.fnp, d->B, d->N, d->ctrl_hidden, part);
+    if ((rc = launch_check("ctrl_grad_kernel"))) return rc;
+    hipLaunchKernelGGL(grad_reduce_kernel, dim3(d->ctrl_hidden * 5), dim3(256), 0, s, (const float *)part,
+                       L.ctrl_blocks, d->ctrl_hidden, g_w_inp, g_b_inp, g_w_out);
     return launch_check("grad_reduce_kernel");
 }
 

@@ -18,6 +18,7 @@
 namespace fcr {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kWave = 64;
 constexpr int kTile = 16;        // trajectories per wave (MFMA 16x16x4 column count)
@@ -28,8 +29,20 @@ constexpr int kOut = 4;          // [y_dot, p1, p2, z]
 constexpr int kCtrlIn = 3;       // [y_dot, z, ref]
 constexpr int kMS = 13;          // controller hidden slots (units 4m+q), hidden <= 52
 constexpr int kFnpStride = 8;    // floats per (m, q) controller record: W0 W1 W2 b wout 0 0 0
-constexpr int kFwdWaves = 4;     // waves per forward workgroup (1 per SIMD, 512 VGPRs)
-constexpr int kBwdWaves = 4;     // waves per backward workgroup (1 per SIMD, 512 VGPRs)
+#ifndef FCR_FWD_TILE_REGION
+#define FCR_FWD_TILE_REGION 0   // 1: one scheduling region per gate tile (next tile's reads prefetched)
+#endif
+#ifndef FCR_FWD_WAVES
+#define FCR_FWD_WAVES 8
+#endif
+constexpr int kFwdWaves = FCR_FWD_WAVES;  // waves per forward workgroup (8 = 2 per SIMD)
+#ifndef FCR_BWD_PIPE
+#define FCR_BWD_PIPE 1     // software-pipelined backward cell (see fcr_bwd.h)
+#endif
+#ifndef FCR_BWD_WAVES
+#define FCR_BWD_WAVES 8
+#endif
+constexpr int kBwdWaves = FCR_BWD_WAVES;   // waves per backward workgroup (8 = 2 per SIMD)     // waves per backward workgroup (1 per SIMD, 512 VGPRs)
 constexpr float kP1Max = 2.122366f;  // Functions.py:1411 (32e6 / p1 max_abs_)
 constexpr float kP2Max = 1.036233f;  // Functions.py:1411 (32e6 / p2 max_abs_)
 
@@ -38,6 +51,7 @@ struct Geo {
     static constexpr int KS0 = 2 + HS;
     static constexpr int KS1 = 2 * HS;
     static constexpr int KB = 4 * HS;
+    static constexpr int HQ = (HS + 3) / 4;   // 16-B quads per unit-slot vector (sequence slabs)
     static constexpr int NB0 = (HS + 2 + 3) / 4;
     static constexpr int NB1 = (2 * HS + 3) / 4;
     static constexpr int KQ0 = (KS0 + 3) / 4 * 4;  // k-steps padded to whole k-quads
@@ -46,8 +60,14 @@ struct Geo {
     static constexpr int FA1 = HS * KQ1 * kWave;
     static constexpr int BA0 = NB0 * KB * kWave;
     static constexpr int BA1 = NB1 * KB * kWave;
-    static constexpr int LDS_FWD = (FA0 > FA1 ? FA0 : FA1) * 4;  // bytes
-    static constexpr int LDS_BWD = (BA0 > BA1 ? BA0 : BA1) * 4;
+    // LDS map (floats): [0, A) the layer-1/2 fragments of the current phase (refilled per phase),
+    // [A, A+B) the layer-0 fragments (resident for the whole kernel), then the controller records,
+    // fc.weight in lane layout and fc.bias (resident).
+    static constexpr int FNP = kMS * 4 * kFnpStride;
+    static constexpr int FCP = kOut * HS * 4;
+    static constexpr int MISC = FNP + FCP + 4;
+    static constexpr int LDS_FWD = (FA1 + FA0 + MISC) * 4;  // bytes
+    static constexpr int LDS_BWD = (BA1 + BA0 + MISC) * 4;
 };
 
 struct Packed {                    // device pointers into the workspace
@@ -63,8 +83,9 @@ struct FwdArgs {
     float alpha;
     const float *X, *u0, *states, *noise;
     float *cost, *command, *error, *prediction, *xhat_user, *xhat_ws, *loss_part;
-    f32x4 *gates;    // [wave][j][l][t][slot][64] post-activation (i,f,g,o), or null
-    float *cstore;   // [wave][j][l][t][slot][64] c_t, or null
+    f32x4 *hseq;     // [wave][j][2][t][quad][64] layer-0/1 outputs handed to the next layer phase
+    f32x4 *gates;    // [wave][j][l][t][slot][64] (dh/dc, dh/do, dc/di, dc/df) per cell, or null
+    f32x2 *cstore;   // [wave][j][l][t][slot][64] (dc/dg, f) per cell, or null
     Packed p;
 };
 
@@ -73,9 +94,11 @@ struct BwdArgs {
     float alpha;
     const float *X, *states, *prediction, *xhat, *dloss;
     const f32x4 *gates;
-    const float *cstore;
-    float *dseq;     // [wave][j][2][t][slot][64] dx of layers 2 and 1 (inputs of layers 1 and 0)
-    float *g_u0, *fnn_part;
+    const f32x2 *cstore;
+    f32x4 *dseq;     // [wave][j][2][t][quad][64] dx of layers 2 and 1 (inputs of layers 1 and 0)
+    f32x2 *dxrow;    // [wave][j][t][64] window-row gradients (col q in lane group q, col 4 in group 0)
+    float *g_u0;
+    float *dv;       // [B][N] d loss / d (controller pre-Hardtanh output) of the call fed by step j
     Packed p;
 };
 
@@ -106,6 +129,15 @@ __device__ __forceinline__ float xor_sum_q(float v) {
 }
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
 
+// An LDS pointer the compiler cannot see through: stops it from hoisting loop-invariant LDS reads
+// (e.g. the 65 controller parameters) out of the window loop into registers it does not have.
+template <typename T>
+__device__ __forceinline__ T *opaque(T *p) {
+    int z = 0;
+    asm volatile("" : "+s"(z));
+    return p + z;
+}
+
 // ds_read_b128 of fragment quad `idx` (units of 16 B per lane-slot, i.e. element idx*64+lane of an
 // f32x4 array). ds_* immediate offsets are 16-bit, so fragment blocks beyond 64 KB would each need a
 // materialised address VGPR (which the compiler then hoists out of every loop and spills). Two
@@ -119,14 +151,40 @@ __device__ __forceinline__ f32x4 lds_quad(const float *lw, int idx, int lane) {
     return *reinterpret_cast<const f32x4 *>(hi + (byte - kSplit));
 }
 
-// Copy the current phase's fragment block (global, L2-resident) into LDS. Every wave of the
-// workgroup calls this at the same program point.
-__device__ __forceinline__ void lds_fill(float *lw, const float *__restrict__ src, int nfloats) {
-    __syncthreads();
+// Copy a fragment block (global, L2-resident) into LDS; the caller brackets it with barriers.
+__device__ __forceinline__ void lds_copy(float *lw, const float *__restrict__ src, int nfloats) {
     const float4 *s4 = reinterpret_cast<const float4 *>(src);
     float4 *d4 = reinterpret_cast<float4 *>(lw);
     for (int i = threadIdx.x; i < nfloats / 4; i += blockDim.x) d4[i] = s4[i];
+}
+// Refill the per-phase region. Every wave of the workgroup calls this at the same program point.
+__device__ __forceinline__ void lds_fill(float *lw, const float *__restrict__ src, int nfloats) {
     __syncthreads();
+    lds_copy(lw, src, nfloats);
+    __syncthreads();
+}
+
+// Unit-slot vectors <-> 16-B quads (slots 4k..4k+3 of one lane in one record): sequence hand-offs
+// cost ceil(HS/4) memory instructions per cell instead of HS (vmcnt holds at most 63 per wave).
+template <int HS>
+__device__ __forceinline__ void store_quads(f32x4 *dst, const float (&v)[HS], int lane) {
+#pragma unroll
+    for (int k = 0; k < (HS + 3) / 4; ++k) {
+        f32x4 q;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) q[e] = (4 * k + e < HS) ? v[4 * k + e < HS ? 4 * k + e : 0] : 0.0f;
+        dst[k * kWave + lane] = q;
+    }
+}
+template <int HS>
+__device__ __forceinline__ void load_quads(float (&v)[HS], const f32x4 *src, int lane) {
+#pragma unroll
+    for (int k = 0; k < (HS + 3) / 4; ++k) {
+        const f32x4 q = src[k * kWave + lane];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (4 * k + e < HS) v[4 * k + e] = q[e];
+    }
 }
 
 // Controller pre-activation (FNNModel.forward, Functions.py:261-289): lane group q evaluates hidden

@@ -2,8 +2,9 @@
 //
 // One wave = 16 trajectories; one workgroup = kFwdWaves waves sharing one LDS-resident layer of
 // MFMA fragments. Each window (horizon step) runs three layer PHASES (layer-major): the current
-// layer's fragments are copied into LDS, then the wave steps t = 0..9 through that layer, keeping
-// the layer's 10 outputs in a register ring that becomes the next phase's input.
+// layer's fragments are copied into LDS, then the wave steps t = 0..9 through that layer. The layer's
+// 10 outputs go to a per-wave global slab (written once, read once, prefetched one cell ahead by the
+// next phase), which keeps the live state small enough for 2 waves per SIMD.
 #pragma once
 #include "fcr_common.h"
 
@@ -11,18 +12,20 @@ namespace fcr {
 
 // Cell update for one unit slot: a = D fragment (i,f,g,o pre-activations of unit 4r+q).
 template <bool FIRST, bool STORE>
-__device__ __forceinline__ void fwd_pointwise(f32x4 a, float &c, float &h, f32x4 *gs, float *cs,
+__device__ __forceinline__ void fwd_pointwise(f32x4 a, float &c, float &h, f32x4 *gs, f32x2 *cs,
                                               int lane) {
     const float i = sigm(a[0]);
     const float f = sigm(a[1]);
     const float g = tanh_f(a[2]);
     const float o = sigm(a[3]);
-    const float cn = FIRST ? i * g : f * c + i * g;   // c_{-1} = 0 (Functions.py:349-350)
+    const float cold = FIRST ? 0.0f : c;              // c_{-1} = 0 (Functions.py:349-350)
+    const float cn = FIRST ? i * g : f * c + i * g;
     c = cn;
-    h = o * tanh_f(cn);
-    if (STORE) {
-        gs[lane] = f32x4{i, f, g, o};
-        cs[lane] = cn;
+    const float tc = tanh_f(cn);
+    h = o * tc;
+    if (STORE) {   // the local derivatives the backward needs (fcr_bwd.h cell_grad), 24 B per slot
+        gs[lane] = f32x4{o * (1.0f - tc * tc), tc * o * (1.0f - o), g * i * (1.0f - i), cold * f * (1.0f - f)};
+        cs[lane] = f32x2{i * (1.0f - g * g), f};
     }
 }
 
@@ -34,11 +37,39 @@ __device__ __forceinline__ void fwd_pointwise(f32x4 a, float &c, float &h, f32x4
 template <int HS, bool L0, bool FIRST, bool STORE>
 __device__ __forceinline__ void fwd_cell(const float *__restrict__ lw, int lane, float x0, float x1,
                                          const float (&x)[HS], const float (&hp)[HS], float (&c)[HS],
-                                         float (&hout)[HS], f32x4 *gs, float *cs) {
+                                         float (&hout)[HS], f32x4 *gs, f32x2 *cs) {
     constexpr int NX = L0 ? 2 : HS;                 // k-steps over the input
     constexpr int NK = FIRST ? NX : NX + HS;        // k-steps used (h_{t-1} part skipped at t = 0)
     constexpr int QR = (NX + HS + 3) / 4;           // k-quads per fragment row
     constexpr int QN = (NK + 3) / 4;                // k-quads used
+#if FCR_FWD_TILE_REGION
+    f32x4 qb[2][QN];
+#pragma unroll
+    for (int qd = 0; qd < QN; ++qd) qb[0][qd] = lds_quad(lw, qd, lane);
+    f32x4 prev = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int r = 0; r < HS; ++r) {
+        sched_fence();
+        if (r + 1 < HS) {
+#pragma unroll
+            for (int qd = 0; qd < QN; ++qd) qb[(r + 1) & 1][qd] = lds_quad(lw, (r + 1) * QR + qd, lane);
+        }
+        f32x4 va[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) va[u] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int s = 0; s < NK; ++s) {
+            float bop;
+            if (s < NX) bop = L0 ? (s == 0 ? x0 : x1) : x[s < NX ? s : 0];
+            else bop = hp[s - NX < HS ? s - NX : 0];
+            va[s & 3] = mfma(qb[r & 1][s >> 2][s & 3], bop, va[s & 3]);
+        }
+        if (r > 0)
+            fwd_pointwise<FIRST, STORE>(prev, c[r - 1], hout[r - 1], gs + (r - 1) * kWave,
+                                        cs + (r - 1) * kWave, lane);
+        prev = (va[0] + va[1]) + (va[2] + va[3]);
+    }
+#else
     f32x4 cur = lds_quad(lw, 0, lane);
     f32x4 prev = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -69,19 +100,10 @@ __device__ __forceinline__ void fwd_cell(const float *__restrict__ lw, int lane,
         }
         prev = (va[0] + va[1]) + (va[2] + va[3]);
     }
+#endif
     sched_fence();
     fwd_pointwise<FIRST, STORE>(prev, c[HS - 1], hout[HS - 1], gs + (HS - 1) * kWave,
                                 cs + (HS - 1) * kWave, lane);
-}
-
-template <int HS>
-__device__ __forceinline__ void ring_push(float (&ring)[kL][HS], const float (&v)[HS]) {
-#pragma unroll
-    for (int k = 0; k < kL - 1; ++k)
-#pragma unroll
-        for (int r = 0; r < HS; ++r) ring[k][r] = ring[k + 1][r];
-#pragma unroll
-    for (int r = 0; r < HS; ++r) ring[kL - 1][r] = v[r];
 }
 
 __device__ __forceinline__ void rot_left(float (&w)[kL]) {
@@ -92,9 +114,17 @@ __device__ __forceinline__ void rot_left(float (&w)[kL]) {
 }
 
 template <int HS, bool STORE>
-__global__ __launch_bounds__(kFwdWaves * kWave, 1) void fcr_fwd_kernel(FwdArgs a) {
+__global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kernel(FwdArgs a) {
     using G = Geo<HS>;
     extern __shared__ __attribute__((aligned(16))) float lw[];
+    float *lw0 = lw + G::FA1;                   // resident layer-0 fragments
+    float *lfnp = lw0 + G::FA0;                 // resident controller records
+    float *lfcp = lfnp + G::FNP;                // resident fc.weight (lane layout) and fc.bias
+    float *lfcb = lfcp + G::FCP;
+    lds_copy(lw0, a.p.fa[0], G::FA0);
+    lds_copy(lfnp, a.p.fnp, G::FNP);
+    lds_copy(lfcp, a.p.fcp, G::FCP);
+    lds_copy(lfcb, a.p.fcb, 4);
     const int lane = threadIdx.x & 63;
     const int q = lane >> 4, sl = lane & 15;
     // wave-uniform by construction; readfirstlane lets the compiler keep every address base in SGPRs
@@ -120,20 +150,19 @@ __global__ __launch_bounds__(kFwdWaves * kWave, 1) void fcr_fwd_kernel(FwdArgs a
     float cmd_sum = 0.0f, err_sum = 0.0f, tot_sum = 0.0f;
     float xh0 = 0.0f, xh1 = 0.0f, xh2 = 0.0f, xh3 = 0.0f;
 
-    float ring[kL][HS];   // outputs of the current layer for t = 0..9 (next phase's inputs)
-    float c[HS], hout[HS];
-#pragma unroll
-    for (int k = 0; k < kL; ++k)
-#pragma unroll
-        for (int r = 0; r < HS; ++r) ring[k][r] = 0.0f;
+    float c[HS], hout[HS], hp[HS], xc[HS], xn[HS];
     const size_t cell = (size_t)HS * kWave;
     const size_t cells_per_wave = (size_t)N * kLayers * kL;
+    // h-sequence hand-off slab [wave][j][layer 0|1][t][slot][64]: each address written once, read once
+    const size_t qcell = (size_t)Geo<HS>::HQ * kWave;    // one cell of a sequence slab, in quads
+    f32x4 *hs_wave = a.hseq + (size_t)wave * N * 2 * kL * qcell;
 
     for (int j = 0; j < N; ++j) {
+        const float *lfnp_j = opaque(lfnp), *lfcp_j = opaque(lfcp), *lfcb_j = opaque(lfcb);
         float pred = u0;
         if (j > 0) {                                                   // Functions.py:1421-1434
             float z[kMS];
-            const float un = hardtanh(fnn_pre(a.p.fnp, q, xh0, xh3, ref, z));
+            const float un = hardtanh(fnn_pre(lfnp_j, q, xh0, xh3, ref, z));
             cmd_j = alpha * sq(u_prev - un);                           // Functions.py:1446
 #pragma unroll
             for (int k = 0; k < kL - 1; ++k) {
@@ -148,7 +177,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, 1) void fcr_fwd_kernel(FwdArgs a
         if (valid && q == 0) a.prediction[(size_t)b * N + j] = pred;   // Functions.py:1455,1466
 
         f32x4 *gs = a.gates;
-        float *cs = a.cstore;
+        f32x2 *cs = a.cstore;
         if (STORE) {
             const size_t base = ((size_t)wave * cells_per_wave + (size_t)j * kLayers * kL) * cell;
             gs += base;
@@ -156,34 +185,52 @@ __global__ __launch_bounds__(kFwdWaves * kWave, 1) void fcr_fwd_kernel(FwdArgs a
         }
 #define FCR_G(l, t) (gs + (STORE ? (size_t)((l) * kL + (t)) * cell : 0))
 #define FCR_C(l, t) (cs + (STORE ? (size_t)((l) * kL + (t)) * cell : 0))
+        f32x4 *hs0 = hs_wave + (size_t)j * 2 * kL * qcell;  // layer-0 outputs, t-major
+        f32x4 *hs1 = hs0 + (size_t)kL * qcell;              // layer-1 outputs
         // ---- layer 0 over the window (Functions.py:374) ----
-        lds_fill(lw, a.p.fa[0], G::FA0);
+        __syncthreads();   // resident blocks are in place (first window) — no refill for layer 0
         {
             const float x0 = w0[0], x1 = w1[0];
             rot_left(w0);
             rot_left(w1);
-            fwd_cell<HS, true, true, STORE>(lw, lane, x0, x1, hout, hout, c, hout, FCR_G(0, 0), FCR_C(0, 0));
-            ring_push<HS>(ring, hout);
+            fwd_cell<HS, true, true, STORE>(lw0, lane, x0, x1, hp, hp, c, hout, FCR_G(0, 0), FCR_C(0, 0));
+            store_quads<HS>(hs0, hout, lane);
+#pragma unroll
+            for (int r = 0; r < HS; ++r) hp[r] = hout[r];
         }
         for (int t = 1; t < kL; ++t) {
             const float x0 = w0[0], x1 = w1[0];
             rot_left(w0);
             rot_left(w1);
-            fwd_cell<HS, true, false, STORE>(lw, lane, x0, x1, hout, ring[kL - 1], c, hout, FCR_G(0, t),
-                                      FCR_C(0, t));
-            ring_push<HS>(ring, hout);
+            fwd_cell<HS, true, false, STORE>(lw0, lane, x0, x1, hp, hp, c, hout, FCR_G(0, t), FCR_C(0, t));
+            store_quads<HS>(hs0 + (size_t)t * qcell, hout, lane);
+#pragma unroll
+            for (int r = 0; r < HS; ++r) hp[r] = hout[r];
         }
-        // ---- layers 1, 2 ----
+        // ---- layers 1, 2: input sequence streamed back from the slab, one cell ahead ----
 #pragma unroll
         for (int l = 1; l < kLayers; ++l) {
+            const f32x4 *src = (l == 1) ? hs0 : hs1;
             lds_fill(lw, a.p.fa[l], G::FA1);
-            fwd_cell<HS, false, true, STORE>(lw, lane, 0.0f, 0.0f, ring[0], ring[0], c, hout, FCR_G(l, 0),
-                                      FCR_C(l, 0));
-            ring_push<HS>(ring, hout);
+            load_quads<HS>(xc, src, lane);
+            load_quads<HS>(xn, src + qcell, lane);
+            fwd_cell<HS, false, true, STORE>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, FCR_G(l, 0), FCR_C(l, 0));
+            if (l == 1) store_quads<HS>(hs1, hout, lane);
+#pragma unroll
+            for (int r = 0; r < HS; ++r) {
+                hp[r] = hout[r];
+                xc[r] = xn[r];
+            }
             for (int t = 1; t < kL; ++t) {
-                fwd_cell<HS, false, false, STORE>(lw, lane, 0.0f, 0.0f, ring[0], ring[kL - 1], c, hout,
-                                           FCR_G(l, t), FCR_C(l, t));
-                ring_push<HS>(ring, hout);
+                load_quads<HS>(xn, src + (size_t)(t + 1 < kL ? t + 1 : t) * qcell, lane);
+                fwd_cell<HS, false, false, STORE>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, FCR_G(l, t),
+                                                  FCR_C(l, t));
+                if (l == 1) store_quads<HS>(hs1 + (size_t)t * qcell, hout, lane);
+#pragma unroll
+                for (int r = 0; r < HS; ++r) {
+                    hp[r] = hout[r];
+                    xc[r] = xn[r];
+                }
             }
         }
 #undef FCR_G
@@ -194,8 +241,8 @@ __global__ __launch_bounds__(kFwdWaves * kWave, 1) void fcr_fwd_kernel(FwdArgs a
         for (int o = 0; o < kOut; ++o) {
             float p = 0.0f;
 #pragma unroll
-            for (int r = 0; r < HS; ++r) p += a.p.fcp[(o * HS + r) * 4 + q] * ring[kL - 1][r];
-            xo[o] = xor_sum_q(p) + a.p.fcb[o];
+            for (int r = 0; r < HS; ++r) p += lfcp_j[(o * HS + r) * 4 + q] * hp[r];
+            xo[o] = xor_sum_q(p) + lfcb_j[o];
         }
         if (a.noise) {                                                 // Functions.py:1400-1402
             const float *nz = a.noise + ((size_t)bc * N + j) * kOut;

@@ -1,0 +1,106 @@
+"""A/B timing of libfcr.so build variants in ONE process (interleaved rounds, same device, same data).
+
+    python scripts/kbench.py lib/a.so lib/b.so ... [--batch 65536] [--rounds 5]
+
+For each variant: fcr_forward(with_backward=1) and fcr_backward timed with HIP events on the launch
+stream; outputs are checked against the first variant (loss, g_u0, controller grads within 1e-5 rel).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import forging_control_amd as fca  # noqa: E402
+from bench import load_weights, synth_batch  # noqa: E402
+
+_n = fca._native
+
+
+def bind(path):
+    lib = ctypes.CDLL(os.path.abspath(path))
+    vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    lib.fcr_workspace_size.argtypes = [ctypes.POINTER(_n.FcrDims), i32, ctypes.POINTER(sz)]
+    lib.fcr_forward.argtypes = [ctypes.POINTER(_n.FcrDims), ctypes.POINTER(_n.FcrWeights)] + [vp] * 10 + [i32, vp, sz, vp]
+    lib.fcr_backward.argtypes = [ctypes.POINTER(_n.FcrDims)] + [vp] * 8 + [vp, sz, vp]
+    lib.fcr_last_error.restype = ctypes.c_char_p
+    return lib
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--horizon", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=5)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    B, N = a.batch, a.horizon
+    sim, ctrl = load_weights(dev, 50)
+    X, S = synth_batch(B, dev, 7)
+    with torch.no_grad():
+        u0 = ctrl(X).contiguous()
+    dims = fca.rollout.make_dims(B, N, 50, 3, 50, 20.0)
+    w = _n.FcrWeights()
+    params = [ctrl.fc_inp.weight, ctrl.fc_inp.bias, ctrl.fc_out.weight]
+    w.ctrl_w_inp, w.ctrl_b_inp, w.ctrl_w_out = (p.data_ptr() for p in params)
+    for k in range(3):
+        w.w_ih[k] = getattr(sim.lstm, f"weight_ih_l{k}").data_ptr()
+        w.w_hh[k] = getattr(sim.lstm, f"weight_hh_l{k}").data_ptr()
+    w.fc_w, w.fc_b = sim.fc.weight.data_ptr(), sim.fc.bias.data_ptr()
+    libs = [bind(p) for p in a.libs]
+    need = []
+    for lib in libs:
+        nb = ctypes.c_size_t()
+        lib.fcr_workspace_size(ctypes.byref(dims), 1, ctypes.byref(nb))
+        need.append(nb.value)
+    nbytes = ctypes.c_size_t(max(need))
+    ws = torch.empty(nbytes.value, dtype=torch.uint8, device=dev)
+    f32 = dict(dtype=torch.float32, device=dev)
+    outs = {k: torch.empty(s, **f32) for k, s in
+            dict(loss=(), cost=B, command=B, error=B, pred=B * N, xhat=(B, N, 4), gu0=(B, 1), gwi=(50, 3),
+                 gbi=(50,), gwo=(1, 50)).items()}
+    dl = torch.ones(1, **f32)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    times = {i: {"fwd": [], "bwd": []} for i in range(len(libs))}
+    ref = None
+    results = {}
+    for rnd in range(a.rounds + 1):
+        for i, lib in enumerate(libs):
+            ev[0].record()
+            rc = lib.fcr_forward(ctypes.byref(dims), ctypes.byref(w), p(X), p(u0), p(S), None, p(outs["loss"]),
+                                 p(outs["cost"]), p(outs["command"]), p(outs["error"]), p(outs["pred"]),
+                                 p(outs["xhat"]), 1, p(ws), nbytes, st)
+            ev[1].record()
+            rc |= lib.fcr_backward(ctypes.byref(dims), p(X), p(S), p(outs["pred"]), p(dl), p(outs["gu0"]),
+                                   p(outs["gwi"]), p(outs["gbi"]), p(outs["gwo"]), p(ws), nbytes, st)
+            ev[2].record()
+            torch.cuda.synchronize()
+            if rc:
+                raise RuntimeError(lib.fcr_last_error())
+            if rnd > 0:
+                times[i]["fwd"].append(ev[0].elapsed_time(ev[1]))
+                times[i]["bwd"].append(ev[1].elapsed_time(ev[2]))
+            snap = {k: outs[k].detach().cpu().numpy().copy() for k in ("loss", "gu0", "gwi", "gbi", "gwo", "xhat")}
+            if ref is None:
+                ref = snap
+            err = max(float(np.abs(snap[k] - ref[k]).max() / max(np.abs(ref[k]).max(), 1e-30)) for k in snap)
+            results[i] = err
+    for i, path in enumerate(a.libs):
+        f, b = np.median(times[i]["fwd"]), np.median(times[i]["bwd"])
+        print(json.dumps({"lib": os.path.basename(path), "fwd_ms": round(f, 3), "bwd_ms": round(b, 3),
+                          "fwd_min": round(min(times[i]["fwd"]), 3), "bwd_min": round(min(times[i]["bwd"]), 3),
+                          "step_ms": round(f + b, 3), "maxrel_vs_first": results[i]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -47,13 +47,13 @@ def dims(**kw):
 
 
 def test_workspace_size_scales_with_batch_and_backward():
-    small = fca._native.workspace_bytes(dims(B=64), True)     # 4 waves of 16 trajectories
+    small = fca._native.workspace_bytes(dims(B=128), True)    # 8 waves of 16 trajectories (one forward workgroup)
     big = fca._native.workspace_bytes(dims(B=65536), True)    # 4096 waves
     fwd_only = fca._native.workspace_bytes(dims(B=65536), False)
-    assert 0.97 * 1024 * small < big < 1.01 * 1024 * small   # fixed fragment blocks are the slack
+    assert 0.97 * 512 * small < big < 1.01 * 512 * small   # fixed fragment blocks are the slack
     # activations of 10 windows x 30 cells x 52 slots x (i,f,g,o,c) fp32 per trajectory
     assert big > 65536 * 10 * 30 * 52 * 5 * 4
-    assert fwd_only < big / 100
+    assert fwd_only < big / 5          # forward-only keeps just the inter-layer sequence slab
 
 
 @pytest.mark.parametrize("kw,code", [
