@@ -62,7 +62,7 @@ __device__ __forceinline__ void bwd_cell(const float *__restrict__ lw, int lane,
     f32x4 acc[NB];
 #pragma unroll
     for (int k = 0; k < NB; ++k) acc[k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#if FCR_BWD_PIPE
+#if FCR_BWD_PIPE == 1
     // software pipeline: region r issues slot r's MFMAs while the VALU computes slot r+1's gradients
     // (and its fragment reads land), so the in-order issue never waits on a VALU chain.
     f32x4 w[2][NB];
@@ -263,6 +263,7 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         }
         float unused0, unused1;
         lds_fill(lw, a.p.ba[2], G::BA1);
+        stagger();
 #pragma unroll
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
         for (int t = kL - 1; t >= 0; --t) {
@@ -273,6 +274,7 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         }
         // ---- layer 1 ----
         lds_fill(lw, a.p.ba[1], G::BA1);
+        stagger();
 #pragma unroll
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
         for (int t = kL - 1; t >= 0; --t) {

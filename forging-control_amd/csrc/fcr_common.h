@@ -32,6 +32,9 @@ constexpr int kFnpStride = 8;    // floats per (m, q) controller record: W0 W1 W
 #ifndef FCR_FWD_TILE_REGION
 #define FCR_FWD_TILE_REGION 0   // 1: one scheduling region per gate tile (next tile's reads prefetched)
 #endif
+#ifndef FCR_FWD_CHAINS
+#define FCR_FWD_CHAINS 2        // accumulator chains per gate tile in the forward (2 or 4)
+#endif
 #ifndef FCR_FWD_WAVES
 #define FCR_FWD_WAVES 8
 #endif
@@ -115,6 +118,13 @@ __device__ __forceinline__ float sigm(float x) {
 __device__ __forceinline__ float tanh_f(float x) {
     return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * 2.8853900817779268f));
 }
+// the same on an argument that is already scaled: sigm_pre(-x log2e) = sigm(x), tanh_pre(2x log2e) = tanh(x)
+__device__ __forceinline__ float sigm_pre(float a) { return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(a)); }
+__device__ __forceinline__ float tanh_pre(float a) {
+    return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(a));
+}
+constexpr float kNegLog2e = -1.4426950408889634f;   // gate-row scales folded into the forward fragments
+constexpr float kTwoLog2e = 2.8853900817779268f;
 __device__ __forceinline__ float relu(float x) { return x > 0.0f ? x : 0.0f; }
 __device__ __forceinline__ float sq(float x) { return x * x; }
 __device__ __forceinline__ float hardtanh(float v) { return fminf(fmaxf(v, -1.0f), 1.0f); }
@@ -128,6 +138,18 @@ __device__ __forceinline__ float xor_sum_q(float v) {
     return v;
 }
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
+
+// After a workgroup barrier every wave runs the same instruction stream in lockstep, so the two
+// waves sharing a SIMD stall at the same points. Delaying the second half of the workgroup by
+// FCR_STAGGER x 64 cycles offsets them (MI355X_MICROARCH.md, "try a stagger").
+#ifndef FCR_STAGGER
+#define FCR_STAGGER 0
+#endif
+__device__ __forceinline__ void stagger() {
+#if FCR_STAGGER > 0
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= (int)(blockDim.x >> 7)) __builtin_amdgcn_s_sleep(FCR_STAGGER);
+#endif
+}
 
 // An LDS pointer the compiler cannot see through: stops it from hoisting loop-invariant LDS reads
 // (e.g. the 65 controller parameters) out of the window loop into registers it does not have.

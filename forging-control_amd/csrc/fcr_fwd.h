@@ -14,18 +14,23 @@ namespace fcr {
 template <bool FIRST, bool STORE>
 __device__ __forceinline__ void fwd_pointwise(f32x4 a, float &c, float &h, f32x4 *gs, f32x2 *cs,
                                               int lane) {
-    const float i = sigm(a[0]);
-    const float f = sigm(a[1]);
-    const float g = tanh_f(a[2]);
-    const float o = sigm(a[3]);
-    const float cold = FIRST ? 0.0f : c;              // c_{-1} = 0 (Functions.py:349-350)
-    const float cn = FIRST ? i * g : f * c + i * g;
+    // The packed weights carry the exp2 scaling (pack_fwd_kernel): a = (-x log2e) for i, f, o and
+    // (2 x log2e) for g, so each activation is exp2 + add + rcp (+ one fma for tanh).
+    const float i = sigm_pre(a[0]);
+    const float f = sigm_pre(a[1]);
+    const float g = tanh_pre(a[2]);
+    const float o = sigm_pre(a[3]);
+    const float gi = g * i;
+    const float cf = FIRST ? 0.0f : f * c;            // c_{-1} = 0 (Functions.py:349-350)
+    const float cn = cf + gi;
     c = cn;
     const float tc = tanh_f(cn);
     h = o * tc;
-    if (STORE) {   // the local derivatives the backward needs (fcr_bwd.h cell_grad), 24 B per slot
-        gs[lane] = f32x4{o * (1.0f - tc * tc), tc * o * (1.0f - o), g * i * (1.0f - i), cold * f * (1.0f - f)};
-        cs[lane] = f32x2{i * (1.0f - g * g), f};
+    if (STORE) {   // local derivatives for the backward (fcr_bwd.h cell_grad), 24 B per slot:
+        // dh/dc = o(1-tc^2), dh/do_pre = tc o(1-o), dc/di_pre = g i(1-i), dc/df_pre = c_{t-1} f(1-f),
+        // dc/dg_pre = i(1-g^2), and f — each one fma from products already formed
+        gs[lane] = f32x4{fmaf(-h, tc, o), fmaf(-h, o, h), fmaf(-gi, i, gi), fmaf(-cf, f, cf)};
+        cs[lane] = f32x2{fmaf(-gi, g, i), f};
     }
 }
 
@@ -71,10 +76,12 @@ __device__ __forceinline__ void fwd_cell(const float *__restrict__ lw, int lane,
     }
 #else
     f32x4 cur = lds_quad(lw, 0, lane);
-    f32x4 prev = {0.0f, 0.0f, 0.0f, 0.0f};
+    f32x4 pv[4];   // the previous tile's chains: summed one region later, once their MFMAs have landed
+#pragma unroll
+    for (int u = 0; u < 4; ++u) pv[u] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int r = 0; r < HS; ++r) {
-        f32x4 va[4];   // four accumulation chains over the k-steps (MFMA dependent latency)
+        f32x4 va[4];   // FCR_FWD_CHAINS accumulation chains over the k-steps (MFMA dependent latency)
 #pragma unroll
         for (int u = 0; u < 4; ++u) va[u] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -90,16 +97,20 @@ __device__ __forceinline__ void fwd_cell(const float *__restrict__ lw, int lane,
                     float bop;
                     if (s < NX) bop = L0 ? (s == 0 ? x0 : x1) : x[s < NX ? s : 0];
                     else bop = hp[s - NX < HS ? s - NX : 0];
-                    va[e] = mfma(cur[e], bop, va[e]);
+                    va[e % FCR_FWD_CHAINS] = mfma(cur[e], bop, va[e % FCR_FWD_CHAINS]);
                 }
             }
-            if (qd == 0 && r > 0)
+            if (qd == 0 && r > 0) {
+                const f32x4 prev = FCR_FWD_CHAINS == 4 ? (pv[0] + pv[1]) + (pv[2] + pv[3]) : pv[0] + pv[1];
                 fwd_pointwise<FIRST, STORE>(prev, c[r - 1], hout[r - 1], gs + (r - 1) * kWave,
                                             cs + (r - 1) * kWave, lane);
+            }
             cur = nxt;
         }
-        prev = (va[0] + va[1]) + (va[2] + va[3]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) pv[u] = va[u];
     }
+    const f32x4 prev = FCR_FWD_CHAINS == 4 ? (pv[0] + pv[1]) + (pv[2] + pv[3]) : pv[0] + pv[1];
 #endif
     sched_fence();
     fwd_pointwise<FIRST, STORE>(prev, c[HS - 1], hout[HS - 1], gs + (HS - 1) * kWave,
@@ -189,6 +200,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
         f32x4 *hs1 = hs0 + (size_t)kL * qcell;              // layer-1 outputs
         // ---- layer 0 over the window (Functions.py:374) ----
         __syncthreads();   // resident blocks are in place (first window) — no refill for layer 0
+        stagger();
         {
             const float x0 = w0[0], x1 = w1[0];
             rot_left(w0);
@@ -212,6 +224,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
         for (int l = 1; l < kLayers; ++l) {
             const f32x4 *src = (l == 1) ? hs0 : hs1;
             lds_fill(lw, a.p.fa[l], G::FA1);
+            stagger();
             load_quads<HS>(xc, src, lane);
             load_quads<HS>(xn, src + qcell, lane);
             fwd_cell<HS, false, true, STORE>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, FCR_G(l, 0), FCR_C(l, 0));

@@ -47,7 +47,7 @@ __global__ void pack_fwd_kernel(PackArgs a, int l) {
             }
         }
     }
-    a.fa[l][idx] = v;
+    a.fa[l][idx] = v * (gate == 2 ? kTwoLog2e : kNegLog2e);   // exp2 argument scaling, see fwd_pointwise
 }
 
 // Backward fragment, layout [tau][r][lane][gamma]: element is A'[rho][k] of k-step s' = 4r+gamma
