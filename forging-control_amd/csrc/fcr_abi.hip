@@ -68,6 +68,10 @@ Layout make_layout(const fcr_dims *d, int with_backward) {
         return o;
     };
     const int HS = L.HS;
+#if FCR_F16
+    for (int l = 0; l < kLayers; ++l) L.fa[l] = take(f16_fwd_bytes(HS, l));
+    for (int l = 0; l < kLayers; ++l) L.ba[l] = take(f16_bwd_bytes(HS, l));
+#else
     const int KQ0 = (2 + HS + 3) / 4 * 4, KQ1 = (2 * HS + 3) / 4 * 4;
     L.fa[0] = take(sizeof(float) * HS * KQ0 * kWave);
     L.fa[1] = take(sizeof(float) * HS * KQ1 * kWave);
@@ -75,6 +79,7 @@ Layout make_layout(const fcr_dims *d, int with_backward) {
     L.ba[0] = take(sizeof(float) * L.NB0 * 4 * HS * kWave);
     L.ba[1] = take(sizeof(float) * L.NB1 * 4 * HS * kWave);
     L.ba[2] = take(sizeof(float) * L.NB1 * 4 * HS * kWave);
+#endif
     L.fcp = take(sizeof(float) * kOut * HS * 4);
     L.fcb = take(sizeof(float) * kOut);
     L.fnp = take(sizeof(float) * kMS * 4 * kFnpStride);
@@ -115,7 +120,7 @@ int launch_check(const char *what) {
 
 template <int HS, bool STORE>
 int launch_fwd_t(const FwdArgs &fa, const Layout &L, hipStream_t s) {
-    const int lds = Geo<HS>::LDS_FWD;
+    const int lds = FCR_FGEO<HS>::LDS_FWD;
     static bool attr_set = false;
     if (!attr_set) {
         const hipError_t e = hipFuncSetAttribute((const void *)fcr_fwd_kernel<HS, STORE>,
@@ -135,7 +140,7 @@ int launch_fwd(const FwdArgs &fa, const Layout &L, hipStream_t s) {
 
 template <int HS>
 int launch_bwd(const BwdArgs &ba, const Layout &L, hipStream_t s) {
-    const int lds = Geo<HS>::LDS_BWD;
+    const int lds = FCR_BGEO<HS>::LDS_BWD;
     static bool attr_set = false;
     if (!attr_set) {
         const hipError_t e = hipFuncSetAttribute((const void *)fcr_bwd_kernel<HS>,
@@ -205,6 +210,18 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
     pa.fcbo = (float *)(base + L.fcb);
     pa.fnp = (float *)(base + L.fnp);
     for (int l = 0; l < kLayers; ++l) {
+#if FCR_F16
+        const int nf = (int)(f16_fwd_bytes(L.HS, l) / 4);   // one thread per (hi, lo) pair
+        hipLaunchKernelGGL(pack_fwd16_kernel, dim3((nf + 255) / 256), dim3(256), 0, s, pa, l,
+                           (_Float16 *)(base + L.fa[l]));
+        if ((rc = launch_check("pack_fwd16_kernel"))) return rc;
+        if (with_backward) {
+            const int nb = (int)(f16_bwd_bytes(L.HS, l) / 4);
+            hipLaunchKernelGGL(pack_bwd16_kernel, dim3((nb + 255) / 256), dim3(256), 0, s, pa, l,
+                               (_Float16 *)(base + L.ba[l]));
+            if ((rc = launch_check("pack_bwd16_kernel"))) return rc;
+        }
+#else
         const int nf = L.HS * (l == 0 ? (2 + L.HS + 3) / 4 * 4 : (2 * L.HS + 3) / 4 * 4) * kWave;
         hipLaunchKernelGGL(pack_fwd_kernel, dim3((nf + 255) / 256), dim3(256), 0, s, pa, l);
         if ((rc = launch_check("pack_fwd_kernel"))) return rc;
@@ -213,6 +230,7 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
             hipLaunchKernelGGL(pack_bwd_kernel, dim3((nb + 255) / 256), dim3(256), 0, s, pa, l);
             if ((rc = launch_check("pack_bwd_kernel"))) return rc;
         }
+#endif
     }
     hipLaunchKernelGGL(pack_misc_kernel, dim3(2), dim3(256), 0, s, pa);
     if ((rc = launch_check("pack_misc_kernel"))) return rc;

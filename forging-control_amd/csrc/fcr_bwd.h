@@ -7,6 +7,7 @@
 // in-order vmcnt of these HBM loads).
 #pragma once
 #include "fcr_common.h"
+#include "fcr_f16.h"
 
 namespace fcr {
 
@@ -35,18 +36,28 @@ struct CellBuf {
     __device__ __forceinline__ float din(int r) const { return dq[r >> 2][r & 3]; }
 };
 
-struct NextCell {              // where the next cell's data lives
-    const f32x4 *g;
-    const f32x2 *c;
-    const f32x4 *din;          // always a valid address; unused by layer-2 cells
+// Where the next cell's data lives: buffer descriptors over this wave's own regions (wave-uniform,
+// SGPRs) and the cell's byte offsets in them (SGPRs), so every load's address is one shared lane
+// offset VGPR — no 64-bit address pairs per slot for the compiler to keep live.
+struct NextCell {
+    __amdgpu_buffer_rsrc_t rg, rc, rd;   // gates (P), cstore (Q), dseq (din) regions of this wave
+    uint32_t g, c, din;                  // byte offsets of the cell; din always valid (layer 2 ignores it)
+    bool ld_din;                         // the cell reads a din (layers 0, 1): only then fetch it — a
+                                         // fetched-but-unused register is reused at once, i.e. waited for
 };
 
 // Nothing here may touch the loaded values (a use at load time would make the wave wait for them).
-template <int HS>
+template <int HS, bool DQ = true>
 __device__ __forceinline__ void load_slot(CellBuf<HS> &cb, const NextCell &n, int r, int lane) {
-    cb.g[r] = n.g[r * kWave + lane];
-    cb.cc[r] = n.c[r * kWave + lane];
-    if ((r & 3) == 3 || r == HS - 1) cb.dq[r >> 2] = n.din[(r >> 2) * kWave + lane];   // quad consumed
+    cb.g[r] = buf_ld4(n.rg, lane * 16, n.g + r * kWave * 16);
+    cb.cc[r] = buf_ld2(n.rc, lane * 8, n.c + r * kWave * 8);
+    if (DQ && ((r & 3) == 3 || r == HS - 1))   // quad consumed
+        cb.dq[r >> 2] = buf_ld4(n.rd, lane * 16, n.din + (r >> 2) * kWave * 16);
+}
+template <int HS>
+__device__ __forceinline__ void load_din(CellBuf<HS> &cb, const NextCell &n, int lane) {
+#pragma unroll
+    for (int k = 0; k < Geo<HS>::HQ; ++k) cb.dq[k] = buf_ld4(n.rd, lane * 16, n.din + k * kWave * 16);
 }
 
 // One backward cell: [dx ; dh_prev] = W^T . dgates over NB output tiles. dh (in: carried dh from
@@ -147,9 +158,118 @@ __device__ __forceinline__ void bwd_cell(const float *__restrict__ lw, int lane,
     }
 }
 
+// The same cell on the f16 matrix cores (fcr_f16.h). k-block kb = unit slots 2kb, 2kb+1 x gates; the
+// lane's own dgates of those slots are its B operand, so no data moves between lanes. The dgates of a
+// trajectory are scaled by 2^(13-e) (e = exponent of the largest |dh|+|dc| over its slots, which bounds
+// every dgate) before the hi/lo split, and the products scaled back: both exact powers of two.
+// Region kb issues block kb's MFMAs beside the VALU work of block kb+1 (gradients, scale, split).
+#ifndef FCR_B16_AT
+#define FCR_B16_AT 0      // tile step of region kb that builds block kb+1's operands
+#endif
+#ifndef FCR_B16_FINE
+#define FCR_B16_FINE 1    // one scheduling region per (kb, tile) instead of per kb
+#endif
+template <int HS, bool L0, bool DIN>
+__device__ __forceinline__ void bwd16_cell(const float *__restrict__ lw, int lane, const float (&ext)[HS],
+                                           float (&dh)[HS], float (&dc)[HS], float (&dxo)[HS], float &dxq,
+                                           float &dx4, CellBuf<HS> &cb, const NextCell &nx) {
+    using G = Geo16<HS>;
+    constexpr int NB = L0 ? G::NB0 : G::NB1;
+    constexpr int KBB = G::KBB;
+    float m = 0.0f;
+#pragma unroll
+    for (int r = 0; r < HS; ++r) {
+        dh[r] += DIN ? cb.din(r) : ext[r];
+        m = fmaxf(m, fabsf(dh[r]) + fabsf(dc[r]));
+    }
+    // every din is consumed: the next cell's come in now, a whole cell ahead of the wait for them
+    if (nx.ld_din) load_din<HS>(cb, nx, lane);
+    m = fmaxf(m, __shfl_xor(m, 16));
+    m = fmaxf(m, __shfl_xor(m, 32));
+    const int e = max(__builtin_amdgcn_frexp_expf(m), -100);   // m < 2^e; all-zero -> e = 0
+    const float up = __builtin_amdgcn_ldexpf(1.0f, 13 - e), down = __builtin_amdgcn_ldexpf(1.0f, e - 13);
+    // B operand of block kb: scaled dgates of slots 2kb, 2kb+1 (j = 4*(slot&1) + gate)
+    auto block = [&](int kb, f16x8 &bh, f16x8 &bl) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int r = 2 * kb + u;
+            if (r < HS) {
+                float dcs = dc[r] * up;
+                cell_grad(cb.g[r], cb.cc[r], dh[r] * up, dcs, v[4 * u], v[4 * u + 1], v[4 * u + 2], v[4 * u + 3]);
+                dc[r] = dcs * down;
+            } else {
+                v[4 * u] = v[4 * u + 1] = v[4 * u + 2] = v[4 * u + 3] = 0.0f;
+            }
+        }
+        split8(v, bh, bl);
+    };
+    f32x4 acc[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) acc[k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    f16x8 bh[2], bl[2];
+    block(0, bh[0], bl[0]);
+    f16x8 ah = lds_frag16(lw, 0, lane), al = lds_frag16(lw, 1, lane);
+#pragma unroll
+    for (int kb = 0; kb < KBB; ++kb) {
+        const int cu = kb & 1, nu = cu ^ 1;
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+            // one scheduling region per (kb, tile): fragment (t, kb) is in (ah, al); the next one in
+            // (tau, kb) order is fetched beside its MFMAs, and block kb+1 is built in the first region
+            if (FCR_B16_FINE || t == 0) sched_fence();
+            f16x8 nh = ah, nl = al;
+            const int nt = t + 1 < NB ? t + 1 : 0, nk = t + 1 < NB ? kb : kb + 1;
+            if (nk < KBB) {
+                nh = lds_frag16(lw, (nt * KBB + nk) * 2, lane);
+                nl = lds_frag16(lw, (nt * KBB + nk) * 2 + 1, lane);
+            }
+            if (t == (FCR_B16_AT < NB ? FCR_B16_AT : NB - 1) && kb + 1 < KBB) block(kb + 1, bh[nu], bl[nu]);
+            // the products only feed the cell's outputs, so IR passes would sink every MFMA to the
+            // end of the cell (all fragments live at once); naming the accumulator here keeps block
+            // kb-1's MFMAs ahead of this point (issued ~NB*3 MFMAs ago: no hazard wait)
+            if (kb > 0) asm volatile("" : "+v"(acc[t]));
+            acc[t] = mma3(ah, al, bh[cu], bl[cu], acc[t]);
+            ah = nh;
+            al = nl;
+        }
+        // slots 2kb+2, 2kb+3 were consumed by block(kb+1): their next-cell records may load now
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int r = 2 * (kb + 1) + u;
+            if (kb == 0 && u == 0) {
+                load_slot<HS, false>(cb, nx, 0, lane);
+                load_slot<HS, false>(cb, nx, 1, lane);
+            }
+            if (r < HS) load_slot<HS, false>(cb, nx, r, lane);
+        }
+    }
+    sched_fence();
+    if (L0) {
+#pragma unroll
+        for (int s = 0; s < HS; ++s) dh[s] = acc[s >> 2][s & 3] * down;
+        dxq = acc[HS >> 2][HS & 3] * down;
+        dx4 = acc[(HS + 1) >> 2][(HS + 1) & 3] * down;
+    } else {
+#pragma unroll
+        for (int s = 0; s < HS; ++s) {
+            dxo[s] = acc[s >> 2][s & 3] * down;
+            dh[s] = acc[(HS + s) >> 2][(HS + s) & 3] * down;
+        }
+    }
+}
+
+#if FCR_F16
+#define FCR_BWD_CELL bwd16_cell
+#define FCR_BGEO Geo16
+#else
+#define FCR_BWD_CELL bwd_cell
+#define FCR_BGEO Geo
+#endif
+
 template <int HS>
 __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kernel(BwdArgs a) {
-    using G = Geo<HS>;
+    using G = FCR_BGEO<HS>;
     extern __shared__ __attribute__((aligned(16))) float lw[];
     float *lw0 = lw + G::BA1;                   // resident layer-0 fragments
     float *lfnp = lw0 + G::BA0;                 // resident controller records
@@ -175,12 +295,12 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
 
     // window-row gradients dx(w, t) (lane group q: column q; lane group 0 also column 4) go to a
     // per-wave slab; row rho = w + t of the extended sequence sums the windows that contained it.
-    f32x2 *dxr = a.dxrow + (size_t)wave * N * kL * kWave;
+    const __amdgpu_buffer_rsrc_t rx = wave_rsrc(a.dxrow + (size_t)wave * N * kL * kWave, (size_t)N * kL * kWave * 8);
     auto row_grad = [&](int rho) {   // sum over windows w = max(0, rho-9) .. min(N-1, rho) of dx(w, rho-w)
         f32x2 acc2 = {0.0f, 0.0f};
         const int w_hi = rho < N - 1 ? rho : N - 1;
         const int w_lo = rho - (kL - 1) > 0 ? rho - (kL - 1) : 0;
-        for (int w = w_hi; w >= w_lo; --w) acc2 += dxr[((size_t)w * kL + (rho - w)) * kWave + lane];
+        for (int w = w_hi; w >= w_lo; --w) acc2 += buf_ld2(rx, lane * 8, (uint32_t)((w * kL + (rho - w)) * kWave * 8));
         return acc2;
     };
     float dh[HS], dc[HS], dxo[HS], dab[HS];
@@ -190,10 +310,18 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
     const size_t qcell = (size_t)Geo<HS>::HQ * kWave;   // one cell of the dx slab, in quads
     const size_t seq_base = (size_t)wave * N * 2 * kL * qcell;
     // stored activations of cell (j, l, t); dx handed from layer src+... : slab (j, l_from, t), l_from = 2 or 1
-    auto gcell = [&](int j, int l, int t) { return wave_base + ((size_t)(j * kLayers + l) * kL + t) * cell; };
-    auto scell = [&](int j, int lfrom, int t) { return seq_base + ((size_t)(j * 2 + (2 - lfrom)) * kL + t) * qcell; };
+    // cell offsets inside this wave's regions (elements), and the absolute slab cell for stores
+    auto gcell = [&](int j, int l, int t) { return ((size_t)(j * kLayers + l) * kL + t) * cell; };
+    auto srel = [&](int j, int lfrom, int t) { return ((size_t)(j * 2 + (2 - lfrom)) * kL + t) * qcell; };
+    const size_t wave_cells = (size_t)N * kLayers * kL * cell;
+    const __amdgpu_buffer_rsrc_t rg = wave_rsrc(a.gates + wave_base, wave_cells * 16);
+    const __amdgpu_buffer_rsrc_t rc = wave_rsrc(a.cstore + wave_base, wave_cells * 8);
+    const __amdgpu_buffer_rsrc_t rd = wave_rsrc(a.dseq + seq_base, (size_t)N * 2 * kL * qcell * 16);
     auto next_of = [&](int j, int l, int t) {   // the cell processed after (j, l, t)
         NextCell n;
+        n.rg = rg;
+        n.rc = rc;
+        n.rd = rd;
         int nj = j, nl = l, nt = t - 1;
         if (t == 0) {
             nt = kL - 1;
@@ -202,9 +330,10 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         }
         if (nj < 0) { nj = 0; nl = 0; nt = 0; }   // past the last cell: reload it (harmless)
         const size_t gb = gcell(nj, nl, nt);
-        n.g = a.gates + gb;
-        n.c = a.cstore + gb;
-        n.din = a.dseq + (nl < 2 ? scell(nj, nl + 1, nt) : seq_base);
+        n.g = (uint32_t)(gb * 16);
+        n.c = (uint32_t)(gb * 8);
+        n.din = (uint32_t)((nl < 2 ? srel(nj, nl + 1, nt) : 0) * 16);
+        n.ld_din = nl < 2;
         return n;
     };
     CellBuf<HS> cb;
@@ -269,8 +398,8 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         for (int t = kL - 1; t >= 0; --t) {
 #pragma unroll
             for (int r = 0; r < HS; ++r) dab[r] = (t == kL - 1) ? dh_out[r] : 0.0f;
-            bwd_cell<HS, false, false>(lw, lane, dab, dh, dc, dxo, unused0, unused1, cb, next_of(j, 2, t));
-            store_quads<HS>(a.dseq + scell(j, 2, t), dxo, lane);
+            FCR_BWD_CELL<HS, false, false>(lw, lane, dab, dh, dc, dxo, unused0, unused1, cb, next_of(j, 2, t));
+            store_quads<HS>(a.dseq + seq_base + srel(j, 2, t), dxo, lane);
         }
         // ---- layer 1 ----
         lds_fill(lw, a.p.ba[1], G::BA1);
@@ -278,16 +407,16 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
 #pragma unroll
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
         for (int t = kL - 1; t >= 0; --t) {
-            bwd_cell<HS, false, true>(lw, lane, dab, dh, dc, dxo, unused0, unused1, cb, next_of(j, 1, t));
-            store_quads<HS>(a.dseq + scell(j, 1, t), dxo, lane);
+            FCR_BWD_CELL<HS, false, true>(lw, lane, dab, dh, dc, dxo, unused0, unused1, cb, next_of(j, 1, t));
+            store_quads<HS>(a.dseq + seq_base + srel(j, 1, t), dxo, lane);
         }
         // ---- layer 0: dx -> window-row gradients ----
 #pragma unroll
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
         for (int t = kL - 1; t >= 0; --t) {
             float dxq, dx4;
-            bwd_cell<HS, true, true>(lw0, lane, dab, dh, dc, dxo, dxq, dx4, cb, next_of(j, 0, t));
-            dxr[((size_t)j * kL + t) * kWave + lane] = f32x2{dxq, dx4};   // row j+t
+            FCR_BWD_CELL<HS, true, true>(lw0, lane, dab, dh, dc, dxo, dxq, dx4, cb, next_of(j, 0, t));
+            buf_st2(rx, lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{dxq, dx4});   // row j+t
         }
     }
     const float g_u0_rows = row_grad(kL - 1)[1];   // row 9, col 4 = u0 (Functions.py:1396)

@@ -29,6 +29,9 @@ constexpr int kOut = 4;          // [y_dot, p1, p2, z]
 constexpr int kCtrlIn = 3;       // [y_dot, z, ref]
 constexpr int kMS = 13;          // controller hidden slots (units 4m+q), hidden <= 52
 constexpr int kFnpStride = 8;    // floats per (m, q) controller record: W0 W1 W2 b wout 0 0 0
+#ifndef FCR_F16
+#define FCR_F16 1               // gate products on the f16 matrix cores with fp32-accurate splitting
+#endif
 #ifndef FCR_FWD_TILE_REGION
 #define FCR_FWD_TILE_REGION 0   // 1: one scheduling region per gate tile (next tile's reads prefetched)
 #endif
@@ -171,6 +174,23 @@ __device__ __forceinline__ f32x4 lds_quad(const float *lw, int idx, int lane) {
     if (byte < kSplit) return *reinterpret_cast<const f32x4 *>(lo + byte);
     const char *hi = lo + kSplit;
     return *reinterpret_cast<const f32x4 *>(hi + (byte - kSplit));
+}
+
+// Raw buffer loads through a wave-uniform descriptor (base and size from SGPR values only, so no
+// waterfall loop): the per-lane part is a 32-bit voffset, the rest an SGPR soffset.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void *base, size_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)(uint32_t)bytes, 0x00020000);
+}
+__device__ __forceinline__ f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
+}
+__device__ __forceinline__ f32x2 buf_ld2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0));
+}
+
+__device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, f32x2 v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int, v), r,
+                                          (int)voff, (int)soff, 0);
 }
 
 // Copy a fragment block (global, L2-resident) into LDS; the caller brackets it with barriers.

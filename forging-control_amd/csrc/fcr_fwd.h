@@ -7,6 +7,7 @@
 // next phase), which keeps the live state small enough for 2 waves per SIMD.
 #pragma once
 #include "fcr_common.h"
+#include "fcr_f16.h"
 
 namespace fcr {
 
@@ -124,9 +125,83 @@ __device__ __forceinline__ void rot_left(float (&w)[kL]) {
     w[kL - 1] = t0;
 }
 
+// The same cell on the f16 matrix cores (fcr_f16.h): fragments [r][kb][hi|lo][lane][8 halves].
+// The B operands (this cell's inputs and h_{t-1}) are split once per cell and shared by all tiles;
+// each k-block is its own scheduling region with the next block's two fragment reads in flight.
+template <int HS, bool L0, bool FIRST, bool STORE>
+__device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lane, float x0, float x1,
+                                           const float (&x)[HS], const float (&hp)[HS], float (&c)[HS],
+                                           float (&hout)[HS], f32x4 *gs, f32x2 *cs) {
+    using G = Geo16<HS>;
+    constexpr int KBH = G::KBH;
+    constexpr int KB = L0 ? G::KB0 : G::KB1;
+    // active k-blocks: at t = 0 the h_{t-1} blocks are all zero
+    constexpr int KLO = (L0 && FIRST) ? G::XBLK : 0;
+    constexpr int KHI = FIRST ? (L0 ? G::XBLK + 1 : KBH) : KB;
+    f16x8 bh[KB], bl[KB];
+#pragma unroll
+    for (int kb = KLO; kb < KHI; ++kb) {
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float e = 0.0f;
+            if (L0) {
+                const int s = 8 * kb + j;
+                if (kb < KBH && s < HS) e = FIRST ? 0.0f : hp[s < HS ? s : 0];
+                else if (kb == G::XBLK && j == 5) e = x0;
+                else if (kb == G::XBLK && j == 6) e = x1;
+            } else if (kb < KBH) {
+                const int s = 8 * kb + j;
+                if (s < HS) e = x[s < HS ? s : 0];
+            } else {
+                const int s = 8 * (kb - KBH) + j;
+                if (s < HS) e = hp[s < HS ? s : 0];
+            }
+            v[j] = e;
+        }
+        split8(v, bh[kb], bl[kb]);
+    }
+    f16x8 ah = lds_frag16(lw, (0 * KB + KLO) * 2, lane), al = lds_frag16(lw, (0 * KB + KLO) * 2 + 1, lane);
+    f32x4 prev = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int r = 0; r < HS; ++r) {
+        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int kb = KLO; kb < KHI; ++kb) {
+            sched_fence();
+            f16x8 nh = ah, nl = al;
+            if (kb + 1 < KHI) {
+                nh = lds_frag16(lw, (r * KB + kb + 1) * 2, lane);
+                nl = lds_frag16(lw, (r * KB + kb + 1) * 2 + 1, lane);
+            } else if (r + 1 < HS) {
+                nh = lds_frag16(lw, ((r + 1) * KB + KLO) * 2, lane);
+                nl = lds_frag16(lw, ((r + 1) * KB + KLO) * 2 + 1, lane);
+            }
+            acc = mma3(ah, al, bh[kb], bl[kb], acc);
+            if (kb == KLO && r > 0)
+                fwd_pointwise<FIRST, STORE>(prev, c[r - 1], hout[r - 1], gs + (r - 1) * kWave,
+                                            cs + (r - 1) * kWave, lane);
+            ah = nh;
+            al = nl;
+        }
+        prev = acc;
+    }
+    sched_fence();
+    fwd_pointwise<FIRST, STORE>(prev, c[HS - 1], hout[HS - 1], gs + (HS - 1) * kWave,
+                                cs + (HS - 1) * kWave, lane);
+}
+
+#if FCR_F16
+#define FCR_FWD_CELL fwd16_cell
+#define FCR_FGEO Geo16
+#else
+#define FCR_FWD_CELL fwd_cell
+#define FCR_FGEO Geo
+#endif
+
 template <int HS, bool STORE>
 __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kernel(FwdArgs a) {
-    using G = Geo<HS>;
+    using G = FCR_FGEO<HS>;
     extern __shared__ __attribute__((aligned(16))) float lw[];
     float *lw0 = lw + G::FA1;                   // resident layer-0 fragments
     float *lfnp = lw0 + G::FA0;                 // resident controller records
@@ -205,7 +280,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             const float x0 = w0[0], x1 = w1[0];
             rot_left(w0);
             rot_left(w1);
-            fwd_cell<HS, true, true, STORE>(lw0, lane, x0, x1, hp, hp, c, hout, FCR_G(0, 0), FCR_C(0, 0));
+            FCR_FWD_CELL<HS, true, true, STORE>(lw0, lane, x0, x1, hp, hp, c, hout, FCR_G(0, 0), FCR_C(0, 0));
             store_quads<HS>(hs0, hout, lane);
 #pragma unroll
             for (int r = 0; r < HS; ++r) hp[r] = hout[r];
@@ -214,7 +289,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             const float x0 = w0[0], x1 = w1[0];
             rot_left(w0);
             rot_left(w1);
-            fwd_cell<HS, true, false, STORE>(lw0, lane, x0, x1, hp, hp, c, hout, FCR_G(0, t), FCR_C(0, t));
+            FCR_FWD_CELL<HS, true, false, STORE>(lw0, lane, x0, x1, hp, hp, c, hout, FCR_G(0, t), FCR_C(0, t));
             store_quads<HS>(hs0 + (size_t)t * qcell, hout, lane);
 #pragma unroll
             for (int r = 0; r < HS; ++r) hp[r] = hout[r];
@@ -227,7 +302,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             stagger();
             load_quads<HS>(xc, src, lane);
             load_quads<HS>(xn, src + qcell, lane);
-            fwd_cell<HS, false, true, STORE>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, FCR_G(l, 0), FCR_C(l, 0));
+            FCR_FWD_CELL<HS, false, true, STORE>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, FCR_G(l, 0), FCR_C(l, 0));
             if (l == 1) store_quads<HS>(hs1, hout, lane);
 #pragma unroll
             for (int r = 0; r < HS; ++r) {
@@ -236,7 +311,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             }
             for (int t = 1; t < kL; ++t) {
                 load_quads<HS>(xn, src + (size_t)(t + 1 < kL ? t + 1 : t) * qcell, lane);
-                fwd_cell<HS, false, false, STORE>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, FCR_G(l, t),
+                FCR_FWD_CELL<HS, false, false, STORE>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, FCR_G(l, t),
                                                   FCR_C(l, t));
                 if (l == 1) store_quads<HS>(hs1 + (size_t)t * qcell, hout, lane);
 #pragma unroll

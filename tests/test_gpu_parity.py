@@ -142,7 +142,9 @@ def test_shard_independence(ref_params):
     for k in ("loss", "command", "error"):
         assert np.array_equal(full[k][32:64], part[k]), k
     assert np.array_equal(full["xhat"][32:64], part["xhat"])
-    assert relerr(full["g_u0"][32:64] * B, part["g_u0"] * 32) <= 1e-6
+    # the gradients carry 1/B: B=96 vs 32 is not a power-of-two rescaling, so the split-f16 operands of
+    # the backward products round differently (fcr_f16.h) — equal to ~1e-6, not bit-equal
+    assert relerr(full["g_u0"][32:64] * B, part["g_u0"] * 32) <= 4e-6
 
 
 @pytest.mark.parametrize("B", [1, 17, 1000])
