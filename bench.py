@@ -225,6 +225,9 @@ def main():
                          "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
                          "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src},
             "kernels_ms": {"fwd": f_ms, "bwd": b_ms},
+            # the design's own HBM traffic (activation records and hand-off slabs, PMC-measured) against
+            # 8 TB/s: how close the dominant kernel runs to the bandwidth its data movement needs
+            "hbm_traffic_frac": (traffic / (dom[1] * 1e-3) / (HBM_PEAK_GBS * 1e9)) if traffic else None,
             "hbm_roofline_frac": value / world / hbm_roof,
             "loss": float(loss.item()),
         }

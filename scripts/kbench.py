@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--horizon", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--sustain", type=int, default=0, help="then time this many back-to-back launches per lib")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     B, N = a.batch, a.horizon
@@ -95,6 +96,23 @@ def main():
                 ref = snap
             err = max(float(np.abs(snap[k] - ref[k]).max() / max(np.abs(ref[k]).max(), 1e-30)) for k in snap)
             results[i] = err
+    if a.sustain:
+        # back-to-back launches with no host sync (the clock the chip holds under sustained load)
+        for i, lib in enumerate(libs):
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.sustain + 1)]
+            evs[0].record()
+            for k in range(a.sustain):
+                lib.fcr_forward(ctypes.byref(dims), ctypes.byref(w), p(X), p(u0), p(S), None, p(outs["loss"]),
+                                p(outs["cost"]), p(outs["command"]), p(outs["error"]), p(outs["pred"]),
+                                p(outs["xhat"]), 1, p(ws), nbytes, st)
+                evs[2 * k + 1].record()
+                lib.fcr_backward(ctypes.byref(dims), p(X), p(S), p(outs["pred"]), p(dl), p(outs["gu0"]),
+                                 p(outs["gwi"]), p(outs["gbi"]), p(outs["gwo"]), p(ws), nbytes, st)
+                evs[2 * k + 2].record()
+            torch.cuda.synchronize()
+            h = a.sustain // 2
+            times[i]["fwd"] = [evs[2 * k].elapsed_time(evs[2 * k + 1]) for k in range(h, a.sustain)]
+            times[i]["bwd"] = [evs[2 * k + 1].elapsed_time(evs[2 * k + 2]) for k in range(h, a.sustain)]
     for i, path in enumerate(a.libs):
         f, b = np.median(times[i]["fwd"]), np.median(times[i]["bwd"])
         print(json.dumps({"lib": os.path.basename(path), "fwd_ms": round(f, 3), "bwd_ms": round(b, 3),
