@@ -12,6 +12,7 @@
 #include "fcr_bwd.h"
 #include "fcr_common.h"
 #include "fcr_fwd.h"
+#include "fcr_img.h"
 #include "fcr_pack.h"
 
 namespace fcr {
@@ -29,8 +30,8 @@ int fail(int code, const char *fmt, ...) {
 }
 
 struct Layout {
-    int HS, nw, nw_pad, NB0, NB1;
-    size_t fa[3], ba[3], fcp, fcb, fnp, xhat, dv, loss_part, fnn_part, gates, cstore, dseq, dxrow, total;
+    int HS, nw, nw_pad;
+    size_t fa[3], img[3], fcp, fcb, fnp, xhat, dv, loss_part, fnn_part, hseq, cseq, xw, dseq, dxrow, total;
     int ctrl_blocks;
 };
 
@@ -59,8 +60,6 @@ Layout make_layout(const fcr_dims *d, int with_backward) {
     L.nw = (d->B + kTile - 1) / kTile;
     constexpr int kPad = kFwdWaves > kBwdWaves ? kFwdWaves : kBwdWaves;
     L.nw_pad = (L.nw + kPad - 1) / kPad * kPad;  // covers both launch geometries
-    L.NB0 = (L.HS + 2 + 3) / 4;
-    L.NB1 = (2 * L.HS + 3) / 4;
     size_t off = 0;
     auto take = [&](size_t bytes) {
         const size_t o = off;
@@ -68,18 +67,9 @@ Layout make_layout(const fcr_dims *d, int with_backward) {
         return o;
     };
     const int HS = L.HS;
-#if FCR_F16
     for (int l = 0; l < kLayers; ++l) L.fa[l] = take(f16_fwd_bytes(HS, l));
-    for (int l = 0; l < kLayers; ++l) L.ba[l] = take(f16_bwd_bytes(HS, l));
-#else
-    const int KQ0 = (2 + HS + 3) / 4 * 4, KQ1 = (2 * HS + 3) / 4 * 4;
-    L.fa[0] = take(sizeof(float) * HS * KQ0 * kWave);
-    L.fa[1] = take(sizeof(float) * HS * KQ1 * kWave);
-    L.fa[2] = take(sizeof(float) * HS * KQ1 * kWave);
-    L.ba[0] = take(sizeof(float) * L.NB0 * 4 * HS * kWave);
-    L.ba[1] = take(sizeof(float) * L.NB1 * 4 * HS * kWave);
-    L.ba[2] = take(sizeof(float) * L.NB1 * 4 * HS * kWave);
-#endif
+    if (with_backward)
+        for (int l = 0; l < kLayers; ++l) L.img[l] = take(img_bytes(HS, l));
     L.fcp = take(sizeof(float) * kOut * HS * 4);
     L.fcb = take(sizeof(float) * kOut);
     L.fnp = take(sizeof(float) * kMS * 4 * kFnpStride);
@@ -88,12 +78,14 @@ Layout make_layout(const fcr_dims *d, int with_backward) {
     L.dv = take(sizeof(float) * (size_t)d->B * d->N);
     L.ctrl_blocks = (int)(((long long)d->B * d->N + kCtrlItems - 1) / kCtrlItems);
     L.fnn_part = take(sizeof(float) * (size_t)L.ctrl_blocks * d->ctrl_hidden * 5);
-    // sequence hand-off slab: forward h of layers 0/1, then (same addresses) backward dx of layers 2/1
-    L.dseq = take(sizeof(f32x4) * (size_t)L.nw_pad * d->N * 2 * kL * ((HS + 3) / 4) * kWave);
+    // sequence slabs (fcr_common.h): h of every cell always (layers 0, 1 are the next phase's input);
+    // c, the window rows and the backward's dx / window-row-gradient slabs only with a backward
+    const size_t qcells = (size_t)L.nw_pad * d->N * kLayers * kL * ((HS + 3) / 4) * kWave;
+    L.hseq = take(sizeof(f32x4) * qcells);
     if (with_backward) {
-        const size_t cells = (size_t)L.nw_pad * d->N * kLayers * kL * HS * kWave;
-        L.gates = take(sizeof(f32x4) * cells);
-        L.cstore = take(sizeof(f32x2) * cells);
+        L.cseq = take(sizeof(f32x4) * qcells);
+        L.xw = take(sizeof(f32x2) * (size_t)L.nw_pad * d->N * kL * kWave);
+        L.dseq = take(sizeof(f32x4) * (size_t)L.nw_pad * d->N * 2 * kL * ((HS + 3) / 4) * kWave);
         L.dxrow = take(sizeof(f32x2) * (size_t)L.nw_pad * d->N * kL * kWave);
     }
     L.total = off;
@@ -104,7 +96,7 @@ Packed packed_ptrs(const Layout &L, char *ws) {
     Packed p;
     for (int l = 0; l < kLayers; ++l) {
         p.fa[l] = (const float *)(ws + L.fa[l]);
-        p.ba[l] = (const float *)(ws + L.ba[l]);
+        p.img[l] = (const float *)(ws + L.img[l]);
     }
     p.fcp = (const float *)(ws + L.fcp);
     p.fcb = (const float *)(ws + L.fcb);
@@ -120,7 +112,7 @@ int launch_check(const char *what) {
 
 template <int HS, bool STORE>
 int launch_fwd_t(const FwdArgs &fa, const Layout &L, hipStream_t s) {
-    const int lds = FCR_FGEO<HS>::LDS_FWD;
+    const int lds = Geo16<HS>::LDS_FWD;
     static bool attr_set = false;
     if (!attr_set) {
         const hipError_t e = hipFuncSetAttribute((const void *)fcr_fwd_kernel<HS, STORE>,
@@ -135,12 +127,12 @@ int launch_fwd_t(const FwdArgs &fa, const Layout &L, hipStream_t s) {
 
 template <int HS>
 int launch_fwd(const FwdArgs &fa, const Layout &L, hipStream_t s) {
-    return fa.gates ? launch_fwd_t<HS, true>(fa, L, s) : launch_fwd_t<HS, false>(fa, L, s);
+    return fa.cseq ? launch_fwd_t<HS, true>(fa, L, s) : launch_fwd_t<HS, false>(fa, L, s);
 }
 
 template <int HS>
 int launch_bwd(const BwdArgs &ba, const Layout &L, hipStream_t s) {
-    const int lds = FCR_BGEO<HS>::LDS_BWD;
+    const int lds = BwdLds<HS>::BYTES;
     static bool attr_set = false;
     if (!attr_set) {
         const hipError_t e = hipFuncSetAttribute((const void *)fcr_bwd_kernel<HS>,
@@ -198,8 +190,6 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
     for (int l = 0; l < kLayers; ++l) {
         pa.wih[l] = w->w_ih[l];
         pa.whh[l] = w->w_hh[l];
-        pa.fa[l] = (float *)(base + L.fa[l]);
-        pa.ba[l] = (float *)(base + L.ba[l]);
     }
     pa.fcw = w->fc_w;
     pa.fcb = w->fc_b;
@@ -210,27 +200,16 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
     pa.fcbo = (float *)(base + L.fcb);
     pa.fnp = (float *)(base + L.fnp);
     for (int l = 0; l < kLayers; ++l) {
-#if FCR_F16
         const int nf = (int)(f16_fwd_bytes(L.HS, l) / 4);   // one thread per (hi, lo) pair
         hipLaunchKernelGGL(pack_fwd16_kernel, dim3((nf + 255) / 256), dim3(256), 0, s, pa, l,
                            (_Float16 *)(base + L.fa[l]));
         if ((rc = launch_check("pack_fwd16_kernel"))) return rc;
         if (with_backward) {
-            const int nb = (int)(f16_bwd_bytes(L.HS, l) / 4);
-            hipLaunchKernelGGL(pack_bwd16_kernel, dim3((nb + 255) / 256), dim3(256), 0, s, pa, l,
-                               (_Float16 *)(base + L.ba[l]));
-            if ((rc = launch_check("pack_bwd16_kernel"))) return rc;
+            const int ni = (int)(img_bytes(L.HS, l) / 4);
+            hipLaunchKernelGGL(pack_img_kernel, dim3((ni + 255) / 256), dim3(256), 0, s, pa, l,
+                               (_Float16 *)(base + L.img[l]));
+            if ((rc = launch_check("pack_img_kernel"))) return rc;
         }
-#else
-        const int nf = L.HS * (l == 0 ? (2 + L.HS + 3) / 4 * 4 : (2 * L.HS + 3) / 4 * 4) * kWave;
-        hipLaunchKernelGGL(pack_fwd_kernel, dim3((nf + 255) / 256), dim3(256), 0, s, pa, l);
-        if ((rc = launch_check("pack_fwd_kernel"))) return rc;
-        if (with_backward) {
-            const int nb = (l == 0 ? L.NB0 : L.NB1) * 4 * L.HS * kWave;
-            hipLaunchKernelGGL(pack_bwd_kernel, dim3((nb + 255) / 256), dim3(256), 0, s, pa, l);
-            if ((rc = launch_check("pack_bwd_kernel"))) return rc;
-        }
-#endif
     }
     hipLaunchKernelGGL(pack_misc_kernel, dim3(2), dim3(256), 0, s, pa);
     if ((rc = launch_check("pack_misc_kernel"))) return rc;
@@ -250,9 +229,9 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
     fa.xhat_user = xhat;
     fa.xhat_ws = (float *)(base + L.xhat);
     fa.loss_part = (float *)(base + L.loss_part);
-    fa.hseq = (f32x4 *)(base + L.dseq);
-    fa.gates = with_backward ? (f32x4 *)(base + L.gates) : nullptr;
-    fa.cstore = with_backward ? (f32x2 *)(base + L.cstore) : nullptr;
+    fa.hseq = (f32x4 *)(base + L.hseq);
+    fa.cseq = with_backward ? (f32x4 *)(base + L.cseq) : nullptr;
+    fa.xw = with_backward ? (f32x2 *)(base + L.xw) : nullptr;
     fa.p = packed_ptrs(L, base);
     switch (d->H) {
         case 16: rc = launch_fwd<4>(fa, L, s); break;
@@ -289,8 +268,9 @@ int fcr_backward(const fcr_dims *d, const float *X, const float *states, const f
     ba.prediction = prediction;
     ba.xhat = (const float *)(base + L.xhat);
     ba.dloss = dloss;
-    ba.gates = (const f32x4 *)(base + L.gates);
-    ba.cstore = (const f32x2 *)(base + L.cstore);
+    ba.hseq = (const f32x4 *)(base + L.hseq);
+    ba.cseq = (const f32x4 *)(base + L.cseq);
+    ba.xw = (const f32x2 *)(base + L.xw);
     ba.dseq = (f32x4 *)(base + L.dseq);
     ba.dxrow = (f32x2 *)(base + L.dxrow);
     ba.g_u0 = g_u0;

@@ -1,18 +1,23 @@
 // fcr_bwd.h — backward of the rollout (what loss.backward(), Functions.py:655, computes for the
 // controller): reverse over windows; per window three layer phases (2 -> 1 -> 0), each reverse over
-// t = 9..0 with that layer's transposed MFMA fragments resident in LDS.
+// t = 9..0, with that layer's weight image resident in LDS (fcr_img.h).
 //
-// Per cell the stored activations (i,f,g,o,c_t) and c_{t-1} come back from HBM one cell ahead of use
-// (prefetch into VGPRs; the weights come from LDS on lgkmcnt, so no weight read ever waits behind the
-// in-order vmcnt of these HBM loads).
+// Recompute, not store: each cell rebuilds its gate pre-activations from (x_t, h_{t-1}, c_{t-1}) —
+// the forward kept h and c (8 B per unit slot) — with the very products and pointwise arithmetic of
+// the forward kernel (fwd_operand, mma3 in the same k order, lstm_point_grad), and feeds the local
+// derivatives straight into the gradient product [dx ; dh_prev] = Wᵀ·dgates. Both products read the
+// same LDS image: row reads for W·[x;h], ds_read_b64_tr_b16 for Wᵀ·dgates. Against storing the
+// derivatives (24 B per slot written by the forward, read here), this halves the HBM traffic of
+// the two kernels for 2x the matrix work of this one — the split-f16 matrix cores have it to spare.
 #pragma once
 #include "fcr_common.h"
 #include "fcr_f16.h"
+#include "fcr_img.h"
 
 namespace fcr {
 
 // d loss / d (gate pre-activations) of one unit slot, and the carried dc (torch LSTM semantics), from
-// the coefficients the forward stored: P = (dh/dc, dh/do_pre, dc/di_pre, dc/df_pre), Q = (dc/dg_pre, f).
+// P = (dh/dc, dh/do, dc/di, dc/df), Q = (dc/dg, f).
 __device__ __forceinline__ void cell_grad(const f32x4 P, const f32x2 Q, float dh, float &dc_rec, float &di,
                                           float &df, float &dg, float &dO) {
     const float dc = dc_rec + dh * P[0];
@@ -23,226 +28,177 @@ __device__ __forceinline__ void cell_grad(const f32x4 P, const f32x2 Q, float dh
     dc_rec = dc * Q[1];
 }
 
-// Stored coefficients of one cell — (dh/dc, dh/do, dc/di, dc/df) and (dc/dg, f) per unit slot — and the incoming dh
-// from the layer above (dx of layer l+1 at this t, handed over through a per-wave global slab in
-// 4-slot quads). A single buffer rolls through the cells: right after slot r of the current cell is
-// consumed, slot r of the NEXT cell (in reverse order) is loaded into the same registers, so every HBM
-// load is in flight for one cell. Per cell that is 2*HS + ceil(HS/4) loads: within vmcnt's 63.
+// Inputs of one backward cell, fetched one cell ahead: each register group is refilled for the next
+// cell right after this cell consumed it (x, h_{t-1}, din at the top, c_{t-1} quad by quad).
 template <int HS>
-struct CellBuf {
-    f32x4 g[HS];
-    f32x2 cc[HS];
-    f32x4 dq[Geo<HS>::HQ];     // din quads (only read by cells whose layer has an input from above)
-    __device__ __forceinline__ float din(int r) const { return dq[r >> 2][r & 3]; }
+struct CellIn {
+    f32x4 x[Geo<HS>::HQ];   // layer >= 1: layer-below h_t; layer 0: x[0] = (column q, column 4, -, -)
+    f32x4 h[Geo<HS>::HQ];   // h_{t-1}
+    f32x4 c[Geo<HS>::HQ];   // c_{t-1}
+    f32x4 d[Geo<HS>::HQ];   // din = dx of the layer above at t (layers 0, 1)
 };
 
-// Where the next cell's data lives: buffer descriptors over this wave's own regions (wave-uniform,
-// SGPRs) and the cell's byte offsets in them (SGPRs), so every load's address is one shared lane
-// offset VGPR — no 64-bit address pairs per slot for the compiler to keep live.
-struct NextCell {
-    __amdgpu_buffer_rsrc_t rg, rc, rd;   // gates (P), cstore (Q), dseq (din) regions of this wave
-    uint32_t g, c, din;                  // byte offsets of the cell; din always valid (layer 2 ignores it)
-    bool ld_din;                         // the cell reads a din (layers 0, 1): only then fetch it — a
-                                         // fetched-but-unused register is reused at once, i.e. waited for
+// Where the next cell's inputs live: buffer descriptors over this wave's own slab regions (SGPRs)
+// and byte offsets (SGPRs), so every load's address is one shared lane-offset VGPR.
+struct NextIn {
+    __amdgpu_buffer_rsrc_t rh, rc, rx, rd;   // hseq, cseq, xw, dseq
+    uint32_t x, h, c, d;
+    bool l0, hc, din;   // next is a layer-0 cell (x from xw); t > 0 (h, c exist); reads a din
 };
 
-// Nothing here may touch the loaded values (a use at load time would make the wave wait for them).
-template <int HS, bool DQ = true>
-__device__ __forceinline__ void load_slot(CellBuf<HS> &cb, const NextCell &n, int r, int lane) {
-    cb.g[r] = buf_ld4(n.rg, lane * 16, n.g + r * kWave * 16);
-    cb.cc[r] = buf_ld2(n.rc, lane * 8, n.c + r * kWave * 8);
-    if (DQ && ((r & 3) == 3 || r == HS - 1))   // quad consumed
-        cb.dq[r >> 2] = buf_ld4(n.rd, lane * 16, n.din + (r >> 2) * kWave * 16);
-}
 template <int HS>
-__device__ __forceinline__ void load_din(CellBuf<HS> &cb, const NextCell &n, int lane) {
-#pragma unroll
-    for (int k = 0; k < Geo<HS>::HQ; ++k) cb.dq[k] = buf_ld4(n.rd, lane * 16, n.din + k * kWave * 16);
-}
-
-// One backward cell: [dx ; dh_prev] = W^T . dgates over NB output tiles. dh (in: carried dh from
-// t+1; out: dh_prev), dc carried in place. The incoming dh from above is cb.din (DIN) or ext.
-// L0: outputs dxq (col q) and dx4 (col 4, lane group 0); else dxo (unit slots of the layer-below h).
-// lw = transposed fragments [tau][r][lane][gamma]: one ds_read_b128 per output tile and unit slot
-// feeds the four gate k-steps. cb holds this cell on entry and the next cell on exit.
-template <int HS, bool L0, bool DIN>
-__device__ __forceinline__ void bwd_cell(const float *__restrict__ lw, int lane, const float (&ext)[HS],
-                                         float (&dh)[HS], float (&dc)[HS], float (&dxo)[HS], float &dxq,
-                                         float &dx4, CellBuf<HS> &cb, const NextCell &nx) {
-    constexpr int NB = L0 ? Geo<HS>::NB0 : Geo<HS>::NB1;
-    f32x4 acc[NB];
-#pragma unroll
-    for (int k = 0; k < NB; ++k) acc[k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#if FCR_BWD_PIPE == 1
-    // software pipeline: region r issues slot r's MFMAs while the VALU computes slot r+1's gradients
-    // (and its fragment reads land), so the in-order issue never waits on a VALU chain.
-    f32x4 w[2][NB];
-    float d[2][4];
-#pragma unroll
-    for (int k = 0; k < NB; ++k) w[0][k] = lds_quad(lw, k * HS, lane);
-    cell_grad(cb.g[0], cb.cc[0], dh[0] + (DIN ? cb.din(0) : ext[0]), dc[0], d[0][0], d[0][1],
-              d[0][2], d[0][3]);
-#pragma unroll
-    for (int r = 0; r < HS; ++r) {
-        sched_fence();
-        const int cu = r & 1, nu = cu ^ 1;
-        if (r + 1 < HS) {
-#pragma unroll
-            for (int k = 0; k < NB; ++k) w[nu][k] = lds_quad(lw, k * HS + r + 1, lane);
-            cell_grad(cb.g[r + 1], cb.cc[r + 1], dh[r + 1] + (DIN ? cb.din(r + 1) : ext[r + 1]),
-                      dc[r + 1], d[nu][0], d[nu][1], d[nu][2], d[nu][3]);
-        }
-#pragma unroll
-        for (int gm = 0; gm < 4; ++gm)
-#pragma unroll
-            for (int k = 0; k < NB; ++k) acc[k] = mfma(w[cu][k][gm], d[cu][gm], acc[k]);
-        load_slot<HS>(cb, nx, r, lane);
-    }
-#elif FCR_BWD_PIPE == 2
-    // single-buffered pipeline: slot r+1's gradients beside slot r's MFMAs; slot r+1's fragment reads
-    // are issued after slot r's last MFMA (fenced), so they can reuse the operand registers.
-    f32x4 w[NB];
-    float d[4];
-#pragma unroll
-    for (int k = 0; k < NB; ++k) w[k] = lds_quad(lw, k * HS, lane);
-    cell_grad(cb.g[0], cb.cc[0], dh[0] + (DIN ? cb.din(0) : ext[0]), dc[0], d[0], d[1], d[2], d[3]);
-#pragma unroll
-    for (int r = 0; r < HS; ++r) {
-        sched_fence();
-        float dn[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (r + 1 < HS)
-            cell_grad(cb.g[r + 1], cb.cc[r + 1], dh[r + 1] + (DIN ? cb.din(r + 1) : ext[r + 1]), dc[r + 1],
-                      dn[0], dn[1], dn[2], dn[3]);
-#pragma unroll
-        for (int gm = 0; gm < 4; ++gm)
-#pragma unroll
-            for (int k = 0; k < NB; ++k) acc[k] = mfma(w[k][gm], d[gm], acc[k]);
-        sched_fence();
-        if (r + 1 < HS) {
-#pragma unroll
-            for (int k = 0; k < NB; ++k) w[k] = lds_quad(lw, k * HS + r + 1, lane);
-        }
-        load_slot<HS>(cb, nx, r, lane);
-#pragma unroll
-        for (int gm = 0; gm < 4; ++gm) d[gm] = dn[gm];
-    }
-#else
-#pragma unroll
-    for (int r = 0; r < HS; ++r) {
-        sched_fence();
-        f32x4 w[NB];   // issued first; the cell-gradient VALU below covers the LDS latency
-#pragma unroll
-        for (int k = 0; k < NB; ++k) w[k] = lds_quad(lw, k * HS + r, lane);
-        float d[4];
-        cell_grad(cb.g[r], cb.cc[r], dh[r] + (DIN ? cb.din(r) : ext[r]), dc[r], d[0], d[1],
-                  d[2], d[3]);
-#pragma unroll
-        for (int gm = 0; gm < 4; ++gm)
-#pragma unroll
-            for (int k = 0; k < NB; ++k) acc[k] = mfma(w[k][gm], d[gm], acc[k]);
-        load_slot<HS>(cb, nx, r, lane);
-    }
-#endif
-    sched_fence();
-    if (L0) {
-#pragma unroll
-        for (int s = 0; s < HS; ++s) dh[s] = acc[s >> 2][s & 3];
-        dxq = acc[HS >> 2][HS & 3];
-        dx4 = acc[(HS + 1) >> 2][(HS + 1) & 3];
+__device__ __forceinline__ void load_xhd(CellIn<HS> &ci, const NextIn &n, int lane) {
+    constexpr int HQ = Geo<HS>::HQ;
+    if (n.l0) {
+        const f32x2 v = buf_ld2(n.rx, lane * 8, n.x);
+        ci.x[0][0] = v[0];
+        ci.x[0][1] = v[1];
     } else {
 #pragma unroll
-        for (int s = 0; s < HS; ++s) {
-            dxo[s] = acc[s >> 2][s & 3];
-            dh[s] = acc[(HS + s) >> 2][(HS + s) & 3];
-        }
+        for (int k = 0; k < HQ; ++k) ci.x[k] = buf_ld4(n.rh, lane * 16, n.x + k * kWave * 16);
+    }
+    if (n.hc) {
+#pragma unroll
+        for (int k = 0; k < HQ; ++k) ci.h[k] = buf_ld4(n.rh, lane * 16, n.h + k * kWave * 16);
+    }
+    if (n.din) {
+#pragma unroll
+        for (int k = 0; k < HQ; ++k) ci.d[k] = buf_ld4(n.rd, lane * 16, n.d + k * kWave * 16);
     }
 }
 
-// The same cell on the f16 matrix cores (fcr_f16.h). k-block kb = unit slots 2kb, 2kb+1 x gates; the
-// lane's own dgates of those slots are its B operand, so no data moves between lanes. The dgates of a
-// trajectory are scaled by 2^(13-e) (e = exponent of the largest |dh|+|dc| over its slots, which bounds
-// every dgate) before the hi/lo split, and the products scaled back: both exact powers of two.
-// Region kb issues block kb's MFMAs beside the VALU work of block kb+1 (gradients, scale, split).
-#ifndef FCR_B16_AT
-#define FCR_B16_AT 0      // tile step of region kb that builds block kb+1's operands
-#endif
-#ifndef FCR_B16_FINE
-#define FCR_B16_FINE 1    // one scheduling region per (kb, tile) instead of per kb
-#endif
-template <int HS, bool L0, bool DIN>
-__device__ __forceinline__ void bwd16_cell(const float *__restrict__ lw, int lane, const float (&ext)[HS],
-                                           float (&dh)[HS], float (&dc)[HS], float (&dxo)[HS], float &dxq,
-                                           float &dx4, CellBuf<HS> &cb, const NextCell &nx) {
+// inverse exp2 pre-scales of the packed gate rows (fcr_img.h), folded into the dgate scaling
+constexpr float kInvNegLog2e = 1.0f / kNegLog2e;
+constexpr float kInvTwoLog2e = 1.0f / kTwoLog2e;
+
+// One backward cell for 16 trajectories. L0: outputs dh_prev and the window-row gradients dxq (column
+// q), dx4 (column 4, lane group 0); else dxo (layer-below h slots) and dh_prev. DIN: the incoming dh
+// from above is ci.d (else ext). FIRST: t = 0 (h_{t-1} = c_{t-1} = 0). fb/tb: the lane's image
+// addresses (fcr_img.h). On exit `ci` holds the next cell's inputs (or their loads are in flight).
+//
+// Per trajectory the dgates are scaled by 2^(13-e) (e = exponent of the largest |dh|+|dc| over its
+// slots, which bounds every dgate) before the f16 split, and the products scaled back: both exact.
+// Schedule: region kb issues the transposed products of dgate block kb (slots 2kb, 2kb+1) beside the
+// recomputed forward tiles 2kb+2, 2kb+3 and their gradients, which form block kb+1.
+template <int HS, bool L0, bool DIN, bool FIRST>
+__device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, const float (&ext)[HS],
+                                         float (&dh)[HS], float (&dc)[HS], float (&dxo)[HS], float &dxq,
+                                         float &dx4, CellIn<HS> &ci, const NextIn &nx) {
+    using I = Img<HS, L0>;
     using G = Geo16<HS>;
-    constexpr int NB = L0 ? G::NB0 : G::NB1;
-    constexpr int KBB = G::KBB;
+    constexpr int KB = I::KB, NB = I::NB, KBB = I::KBB;
+    constexpr uint32_t TILE = 16 * I::RB;               // one slot's 16 image rows
+    constexpr uint32_t LO = (uint32_t)I::ROWS * I::RB;  // lo image
+    constexpr int KLO = (L0 && FIRST) ? G::XBLK : 0;
+    constexpr int KHI = FIRST ? (L0 ? G::XBLK + 1 : G::KX1) : KB;
+
+    // ---- incoming dh, and the trajectory's power-of-two scale ----
     float m = 0.0f;
 #pragma unroll
     for (int r = 0; r < HS; ++r) {
-        dh[r] += DIN ? cb.din(r) : ext[r];
+        dh[r] += DIN ? ci.d[r >> 2][r & 3] : ext[r];
         m = fmaxf(m, fabsf(dh[r]) + fabsf(dc[r]));
     }
-    // every din is consumed: the next cell's come in now, a whole cell ahead of the wait for them
-    if (nx.ld_din) load_din<HS>(cb, nx, lane);
     m = fmaxf(m, __shfl_xor(m, 16));
     m = fmaxf(m, __shfl_xor(m, 32));
     const int e = max(__builtin_amdgcn_frexp_expf(m), -100);   // m < 2^e; all-zero -> e = 0
     const float up = __builtin_amdgcn_ldexpf(1.0f, 13 - e), down = __builtin_amdgcn_ldexpf(1.0f, e - 13);
-    // B operand of block kb: scaled dgates of slots 2kb, 2kb+1 (j = 4*(slot&1) + gate)
-    auto block = [&](int kb, f16x8 &bh, f16x8 &bl) {
+    const float sg0 = up * kInvNegLog2e, sg2 = up * kInvTwoLog2e;   // gates i, f, o / g
+
+    // ---- the recomputation's B operands (this cell's x_t and h_{t-1}) ----
+    f16x8 bh[KB], bl[KB];
+    {
+        float xv[HS], hv[HS];
+#pragma unroll
+        for (int s = 0; s < HS; ++s) {
+            xv[s] = L0 ? 0.0f : ci.x[s >> 2][s & 3];
+            hv[s] = FIRST ? 0.0f : ci.h[s >> 2][s & 3];
+        }
+        const float x0 = ci.x[0][0], x1 = ci.x[0][1];
+#pragma unroll
+        for (int kb = KLO; kb < KHI; ++kb) fwd_operand<HS, L0, FIRST>(kb, x0, x1, xv, hv, bh[kb], bl[kb]);
+    }
+    load_xhd<HS>(ci, nx, lane);   // x, h, din of this cell are consumed
+
+    // recomputed forward tile r -> scaled dgates of slot r (4 values)
+    auto fwd_grad = [&](int r, float *v) {
+        f32x4 a = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int kb = KLO; kb < KHI; ++kb) {
+            const uint32_t a0 = (fb ^ (8u * (8 * kb))) + r * TILE, a1 = (fb ^ (8u * (8 * kb + 1))) + r * TILE;
+            f16x8 ah, al;
+            const f16x4 h0 = lds_b64_f16(a0), h1 = lds_b64_f16(a1);
+            const f16x4 l0 = lds_b64_f16(a0 + LO), l1 = lds_b64_f16(a1 + LO);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                ah[k] = h0[k];
+                ah[4 + k] = h1[k];
+                al[k] = l0[k];
+                al[4 + k] = l1[k];
+            }
+            a = mma3(ah, al, bh[kb], bl[kb], a);
+        }
+        f32x4 P;
+        f32x2 Q;
+        lstm_point_grad<FIRST>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], P, Q);
+        float di, df, dg, dO;
+        cell_grad(P, Q, dh[r], dc[r], di, df, dg, dO);
+        v[0] = di * sg0;
+        v[1] = df * sg0;
+        v[2] = dg * sg2;
+        v[3] = dO * sg0;
+        // c_{t-1} quad of slots 4k..4k+3 consumed: the next cell's comes in
+        if (((r & 3) == 3 || r == HS - 1) && nx.hc)
+            ci.c[r >> 2] = buf_ld4(nx.rc, lane * 16, nx.c + (r >> 2) * kWave * 16);
+    };
+    auto dgate_block = [&](int kbb, f16x8 &gh, f16x8 &gl) {
         float v[8];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            const int r = 2 * kb + u;
+            const int r = 2 * kbb + u;
             if (r < HS) {
-                float dcs = dc[r] * up;
-                cell_grad(cb.g[r], cb.cc[r], dh[r] * up, dcs, v[4 * u], v[4 * u + 1], v[4 * u + 2], v[4 * u + 3]);
-                dc[r] = dcs * down;
+                fwd_grad(r, v + 4 * u);
             } else {
                 v[4 * u] = v[4 * u + 1] = v[4 * u + 2] = v[4 * u + 3] = 0.0f;
             }
         }
-        split8(v, bh, bl);
+        split8(v, gh, gl);
     };
+
     f32x4 acc[NB];
 #pragma unroll
     for (int k = 0; k < NB; ++k) acc[k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    f16x8 bh[2], bl[2];
-    block(0, bh[0], bl[0]);
-    f16x8 ah = lds_frag16(lw, 0, lane), al = lds_frag16(lw, 1, lane);
+    f16x8 gh[2], gl[2];
+    dgate_block(0, gh[0], gl[0]);
 #pragma unroll
-    for (int kb = 0; kb < KBB; ++kb) {
-        const int cu = kb & 1, nu = cu ^ 1;
+    for (int kbb = 0; kbb < KBB; ++kbb) {
+        sched_fence();
+        const int cu = kbb & 1, nu = cu ^ 1;
+        const bool two = 2 * kbb + 1 < HS;
 #pragma unroll
-        for (int t = 0; t < NB; ++t) {
-            // one scheduling region per (kb, tile): fragment (t, kb) is in (ah, al); the next one in
-            // (tau, kb) order is fetched beside its MFMAs, and block kb+1 is built in the first region
-            if (FCR_B16_FINE || t == 0) sched_fence();
-            f16x8 nh = ah, nl = al;
-            const int nt = t + 1 < NB ? t + 1 : 0, nk = t + 1 < NB ? kb : kb + 1;
-            if (nk < KBB) {
-                nh = lds_frag16(lw, (nt * KBB + nk) * 2, lane);
-                nl = lds_frag16(lw, (nt * KBB + nk) * 2 + 1, lane);
+        for (int tau = 0; tau < NB; ++tau) {
+            const uint32_t at = (tb ^ (8u * (8 * (tau >> 1) + (tau & 1)))) + 2 * kbb * TILE;
+            f16x8 ah, al;
+            const f16x4 h0 = lds_tr_f16(at), l0 = lds_tr_f16(at + LO);
+            f16x4 h1 = {0, 0, 0, 0}, l1 = {0, 0, 0, 0};
+            if (two) {
+                h1 = lds_tr_f16(at + TILE);
+                l1 = lds_tr_f16(at + TILE + LO);
             }
-            if (t == (FCR_B16_AT < NB ? FCR_B16_AT : NB - 1) && kb + 1 < KBB) block(kb + 1, bh[nu], bl[nu]);
-            // the products only feed the cell's outputs, so IR passes would sink every MFMA to the
-            // end of the cell (all fragments live at once); naming the accumulator here keeps block
-            // kb-1's MFMAs ahead of this point (issued ~NB*3 MFMAs ago: no hazard wait)
-            if (kb > 0) asm volatile("" : "+v"(acc[t]));
-            acc[t] = mma3(ah, al, bh[cu], bl[cu], acc[t]);
-            ah = nh;
-            al = nl;
-        }
-        // slots 2kb+2, 2kb+3 were consumed by block(kb+1): their next-cell records may load now
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int r = 2 * (kb + 1) + u;
-            if (kb == 0 && u == 0) {
-                load_slot<HS, false>(cb, nx, 0, lane);
-                load_slot<HS, false>(cb, nx, 1, lane);
+            for (int k = 0; k < 4; ++k) {
+                ah[k] = h0[k];
+                ah[4 + k] = h1[k];
+                al[k] = l0[k];
+                al[4 + k] = l1[k];
             }
-            if (r < HS) load_slot<HS, false>(cb, nx, r, lane);
+            // the products only feed the cell's outputs, so IR passes would sink every MFMA to the end
+            // of the cell (all fragments live at once); naming the accumulator keeps block kb-1's
+            // MFMAs ahead of this point (issued ~NB*3 MFMAs ago: no hazard wait)
+            if (kbb > 0) asm volatile("" : "+v"(acc[tau]));
+            acc[tau] = mma3(ah, al, gh[cu], gl[cu], acc[tau]);
         }
+        if (kbb + 1 < KBB) dgate_block(kbb + 1, gh[nu], gl[nu]);
     }
     sched_fence();
     if (L0) {
@@ -259,24 +215,26 @@ __device__ __forceinline__ void bwd16_cell(const float *__restrict__ lw, int lan
     }
 }
 
-#if FCR_F16
-#define FCR_BWD_CELL bwd16_cell
-#define FCR_BGEO Geo16
-#else
-#define FCR_BWD_CELL bwd_cell
-#define FCR_BGEO Geo
-#endif
+template <int HS>
+struct BwdLds {
+    static constexpr int IMG1 = Img<HS, false>::BYTES, IMG0 = Img<HS, true>::BYTES;
+    static constexpr int FNP = kMS * 4 * kFnpStride, FCP = kOut * HS * 4;
+    static constexpr int BYTES = IMG1 + IMG0 + (FNP + FCP) * 4;
+    static_assert(BYTES <= 163840, "weight images exceed the 160 KiB LDS");
+};
 
 template <int HS>
 __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kernel(BwdArgs a) {
-    using G = FCR_BGEO<HS>;
+    using LD = BwdLds<HS>;
+    using I1 = Img<HS, false>;
+    using I0 = Img<HS, true>;
     extern __shared__ __attribute__((aligned(16))) float lw[];
-    float *lw0 = lw + G::BA1;                   // resident layer-0 fragments
-    float *lfnp = lw0 + G::BA0;                 // resident controller records
-    float *lfcp = lfnp + G::FNP;                // resident fc.weight (lane layout)
-    lds_copy(lw0, a.p.ba[0], G::BA0);
-    lds_copy(lfnp, a.p.fnp, G::FNP);
-    lds_copy(lfcp, a.p.fcp, G::FCP);
+    float *lw0 = lw + LD::IMG1 / 4;             // resident layer-0 image
+    float *lfnp = lw0 + LD::IMG0 / 4;           // resident controller records
+    float *lfcp = lfnp + LD::FNP;               // resident fc.weight (lane layout)
+    lds_copy(lw0, a.p.img[0], LD::IMG0 / 4);
+    lds_copy(lfnp, a.p.fnp, LD::FNP);
+    lds_copy(lfcp, a.p.fcp, LD::FCP);
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int q = lane >> 4, sl = lane & 15;
@@ -292,55 +250,58 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
     const float s84 = a.states[(size_t)bc * kL * kIn + (kL - 2) * kIn + 4];
     const float *pred = a.prediction + (size_t)bc * N;
     const float *xh = a.xhat + (size_t)bc * N * kOut;
+    const ImgLane<I1::RB> L1 = img_lane<I1::RB>(lds_offset(lw), lane);
+    const ImgLane<I0::RB> L0 = img_lane<I0::RB>(lds_offset(lw0), lane);
 
     // window-row gradients dx(w, t) (lane group q: column q; lane group 0 also column 4) go to a
     // per-wave slab; row rho = w + t of the extended sequence sums the windows that contained it.
-    const __amdgpu_buffer_rsrc_t rx = wave_rsrc(a.dxrow + (size_t)wave * N * kL * kWave, (size_t)N * kL * kWave * 8);
+    const __amdgpu_buffer_rsrc_t rr = wave_rsrc(a.dxrow + (size_t)wave * N * kL * kWave, (size_t)N * kL * kWave * 8);
     auto row_grad = [&](int rho) {   // sum over windows w = max(0, rho-9) .. min(N-1, rho) of dx(w, rho-w)
         f32x2 acc2 = {0.0f, 0.0f};
         const int w_hi = rho < N - 1 ? rho : N - 1;
         const int w_lo = rho - (kL - 1) > 0 ? rho - (kL - 1) : 0;
-        for (int w = w_hi; w >= w_lo; --w) acc2 += buf_ld2(rx, lane * 8, (uint32_t)((w * kL + (rho - w)) * kWave * 8));
+        for (int w = w_hi; w >= w_lo; --w) acc2 += buf_ld2(rr, lane * 8, (uint32_t)((w * kL + (rho - w)) * kWave * 8));
         return acc2;
     };
     float dh[HS], dc[HS], dxo[HS], dab[HS];
 
-    const size_t cell = (size_t)HS * kWave;
-    const size_t wave_base = (size_t)wave * N * kLayers * kL * cell;
-    const size_t qcell = (size_t)Geo<HS>::HQ * kWave;   // one cell of the dx slab, in quads
-    const size_t seq_base = (size_t)wave * N * 2 * kL * qcell;
-    // stored activations of cell (j, l, t); dx handed from layer src+... : slab (j, l_from, t), l_from = 2 or 1
-    // cell offsets inside this wave's regions (elements), and the absolute slab cell for stores
-    auto gcell = [&](int j, int l, int t) { return ((size_t)(j * kLayers + l) * kL + t) * cell; };
-    auto srel = [&](int j, int lfrom, int t) { return ((size_t)(j * 2 + (2 - lfrom)) * kL + t) * qcell; };
-    const size_t wave_cells = (size_t)N * kLayers * kL * cell;
-    const __amdgpu_buffer_rsrc_t rg = wave_rsrc(a.gates + wave_base, wave_cells * 16);
-    const __amdgpu_buffer_rsrc_t rc = wave_rsrc(a.cstore + wave_base, wave_cells * 8);
-    const __amdgpu_buffer_rsrc_t rd = wave_rsrc(a.dseq + seq_base, (size_t)N * 2 * kL * qcell * 16);
+    // this wave's slab regions
+    const size_t qcell = (size_t)Geo<HS>::HQ * kWave;   // one cell of a sequence slab, in quads
+    const size_t seq_sz = (size_t)N * kLayers * kL * qcell;
+    const size_t dseq_sz = (size_t)N * 2 * kL * qcell;
+    NextIn nb;
+    nb.rh = wave_rsrc(a.hseq + (size_t)wave * seq_sz, seq_sz * 16);
+    nb.rc = wave_rsrc(a.cseq + (size_t)wave * seq_sz, seq_sz * 16);
+    nb.rx = wave_rsrc(a.xw + (size_t)wave * N * kL * kWave, (size_t)N * kL * kWave * 8);
+    nb.rd = wave_rsrc(a.dseq + (size_t)wave * dseq_sz, dseq_sz * 16);
+    f32x4 *dseq_w = a.dseq + (size_t)wave * dseq_sz;
+    auto hoff = [&](int j, int l, int t) { return (uint32_t)(((size_t)(j * kLayers + l) * kL + t) * qcell * 16); };
+    auto doff = [&](int j, int lfrom, int t) { return ((size_t)(j * 2 + (2 - lfrom)) * kL + t) * qcell; };
     auto next_of = [&](int j, int l, int t) {   // the cell processed after (j, l, t)
-        NextCell n;
-        n.rg = rg;
-        n.rc = rc;
-        n.rd = rd;
+        NextIn n = nb;
         int nj = j, nl = l, nt = t - 1;
         if (t == 0) {
             nt = kL - 1;
             nl = l - 1;
             if (l == 0) { nl = 2; nj = j - 1; }
         }
-        if (nj < 0) { nj = 0; nl = 0; nt = 0; }   // past the last cell: reload it (harmless)
-        const size_t gb = gcell(nj, nl, nt);
-        n.g = (uint32_t)(gb * 16);
-        n.c = (uint32_t)(gb * 8);
-        n.din = (uint32_t)((nl < 2 ? srel(nj, nl + 1, nt) : 0) * 16);
-        n.ld_din = nl < 2;
+        const bool none = nj < 0;   // past the last cell: load nothing
+        if (none) { nj = 0; nl = 2; nt = 0; }
+        n.l0 = nl == 0;
+        n.x = nl == 0 ? (uint32_t)((nj * kL + nt) * kWave * 8) : hoff(nj, nl > 0 ? nl - 1 : 0, nt);
+        n.hc = nt > 0 && !none;
+        n.h = hoff(nj, nl, nt > 0 ? nt - 1 : 0);
+        n.c = n.h;
+        n.din = nl < 2 && !none;
+        n.d = (uint32_t)((nl < 2 ? doff(nj, nl + 1, nt) : 0) * 16);
         return n;
     };
-    CellBuf<HS> cb;
+    CellIn<HS> ci;
     {
-        NextCell first = next_of(N - 1, 2, kL);   // t = kL -> (N-1, 2, 9)
+        const NextIn f = next_of(N - 1, 2, kL);   // t = kL -> (N-1, 2, 9)
+        load_xhd<HS>(ci, f, lane);
 #pragma unroll
-        for (int r = 0; r < HS; ++r) load_slot<HS>(cb, first, r, lane);
+        for (int k = 0; k < Geo<HS>::HQ; ++k) ci.c[k] = buf_ld4(f.rc, lane * 16, f.c + k * kWave * 16);
     }
 
     for (int j = N - 1; j >= 0; --j) {
@@ -354,7 +315,7 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         float d3 = 0.0f;
         if (j <= N - 2) {
             // row 10+j = (xhat_j, u_{j+1}) is complete once windows j+1 .. j+10 are done
-            const f32x2 G = row_grad(kL + j);   // row 10+j = (xhat_j, u_{j+1})
+            const f32x2 G = row_grad(kL + j);
             d0 += __shfl(G[0], sl);
             d1 += __shfl(G[0], sl + 16);
             d2 += __shfl(G[0], sl + 32);
@@ -391,32 +352,47 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
             dh_out[r] = fp[0] * d0 + fp[HS * 4] * d1 + fp[2 * HS * 4] * d2 + fp[3 * HS * 4] * d3;
         }
         float unused0, unused1;
-        lds_fill(lw, a.p.ba[2], G::BA1);
+        lds_fill(lw, a.p.img[2], LD::IMG1 / 4);
         stagger();
 #pragma unroll
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
-        for (int t = kL - 1; t >= 0; --t) {
+        for (int t = kL - 1; t >= 1; --t) {
 #pragma unroll
             for (int r = 0; r < HS; ++r) dab[r] = (t == kL - 1) ? dh_out[r] : 0.0f;
-            FCR_BWD_CELL<HS, false, false>(lw, lane, dab, dh, dc, dxo, unused0, unused1, cb, next_of(j, 2, t));
-            store_quads<HS>(a.dseq + seq_base + srel(j, 2, t), dxo, lane);
+            bwd_cell<HS, false, false, false>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0, unused1, ci,
+                                              next_of(j, 2, t));
+            store_quads<HS>(dseq_w + doff(j, 2, t), dxo, lane);
         }
+#pragma unroll
+        for (int r = 0; r < HS; ++r) dab[r] = 0.0f;
+        bwd_cell<HS, false, false, true>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0, unused1, ci,
+                                         next_of(j, 2, 0));
+        store_quads<HS>(dseq_w + doff(j, 2, 0), dxo, lane);
         // ---- layer 1 ----
-        lds_fill(lw, a.p.ba[1], G::BA1);
+        lds_fill(lw, a.p.img[1], LD::IMG1 / 4);
         stagger();
 #pragma unroll
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
-        for (int t = kL - 1; t >= 0; --t) {
-            FCR_BWD_CELL<HS, false, true>(lw, lane, dab, dh, dc, dxo, unused0, unused1, cb, next_of(j, 1, t));
-            store_quads<HS>(a.dseq + seq_base + srel(j, 1, t), dxo, lane);
+        for (int t = kL - 1; t >= 1; --t) {
+            bwd_cell<HS, false, true, false>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0, unused1, ci,
+                                             next_of(j, 1, t));
+            store_quads<HS>(dseq_w + doff(j, 1, t), dxo, lane);
         }
+        bwd_cell<HS, false, true, true>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0, unused1, ci,
+                                        next_of(j, 1, 0));
+        store_quads<HS>(dseq_w + doff(j, 1, 0), dxo, lane);
         // ---- layer 0: dx -> window-row gradients ----
 #pragma unroll
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
-        for (int t = kL - 1; t >= 0; --t) {
+        for (int t = kL - 1; t >= 1; --t) {
             float dxq, dx4;
-            FCR_BWD_CELL<HS, true, true>(lw0, lane, dab, dh, dc, dxo, dxq, dx4, cb, next_of(j, 0, t));
-            buf_st2(rx, lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{dxq, dx4});   // row j+t
+            bwd_cell<HS, true, true, false>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci, next_of(j, 0, t));
+            buf_st2(rr, lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{dxq, dx4});   // row j+t
+        }
+        {
+            float dxq, dx4;
+            bwd_cell<HS, true, true, true>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci, next_of(j, 0, 0));
+            buf_st2(rr, lane * 8, (uint32_t)((j * kL) * kWave * 8), f32x2{dxq, dx4});   // row j
         }
     }
     const float g_u0_rows = row_grad(kL - 1)[1];   // row 9, col 4 = u0 (Functions.py:1396)

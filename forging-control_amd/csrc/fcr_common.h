@@ -1,15 +1,8 @@
 // fcr_common.h — shared constants, device helpers and kernel argument blocks.
 //
-// Fragment geometry (H = LSTM hidden, HS = ceil(H/4) "unit slots"; unit u = 4*slot + q where
-// q = lane>>4 is the lane group):
-//   forward  tile r (16 D rows = units 4r..4r+3 x gates i,f,g,o), fragments [r][k/4][lane][k%4], k-steps:
-//       layer 0 : KS0 = 2 + HS   (2 steps over the 5 window columns, HS over h_{t-1})
-//       layer>=1: KS1 = 2 * HS   (HS over the layer-below h_t, HS over h_{t-1})
-//   backward output tile tau (16 D rows = 4 slots x 4 lane groups), fragments [tau][r][lane][gamma],
-//       k-steps KB = 4 * HS
-//       (slot r, gate gamma) -> s' = 4r + gamma:
-//       layer 0 : NB0 = ceil((HS+2)/4) tiles  (slots < HS: dh_prev; slot HS: dx col q; HS+1: dx col 4)
-//       layer>=1: NB1 = ceil(2HS/4) tiles     (slots < HS: dx; HS..2HS-1: dh_prev)
+// Lane mapping: one wave = 16 trajectories (MFMA columns); hidden unit u = 4*slot + q lives in lane
+// group q = lane>>4, register slot `slot` (HS = ceil(H/4) slots). Operand geometry: fcr_f16.h (forward
+// fragments) and fcr_img.h (the backward's dual-use weight image).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>
@@ -29,69 +22,43 @@ constexpr int kOut = 4;          // [y_dot, p1, p2, z]
 constexpr int kCtrlIn = 3;       // [y_dot, z, ref]
 constexpr int kMS = 13;          // controller hidden slots (units 4m+q), hidden <= 52
 constexpr int kFnpStride = 8;    // floats per (m, q) controller record: W0 W1 W2 b wout 0 0 0
-#ifndef FCR_F16
-#define FCR_F16 1               // gate products on the f16 matrix cores with fp32-accurate splitting
-#endif
-#ifndef FCR_FWD_TILE_REGION
-#define FCR_FWD_TILE_REGION 0   // 1: one scheduling region per gate tile (next tile's reads prefetched)
-#endif
-#ifndef FCR_FWD_CHAINS
-#define FCR_FWD_CHAINS 2        // accumulator chains per gate tile in the forward (2 or 4)
-#endif
 #ifndef FCR_FWD_WAVES
 #define FCR_FWD_WAVES 8
 #endif
 constexpr int kFwdWaves = FCR_FWD_WAVES;  // waves per forward workgroup (8 = 2 per SIMD)
-#ifndef FCR_BWD_PIPE
-#define FCR_BWD_PIPE 1     // software-pipelined backward cell (see fcr_bwd.h)
-#endif
 #ifndef FCR_BWD_WAVES
 #define FCR_BWD_WAVES 8
 #endif
-constexpr int kBwdWaves = FCR_BWD_WAVES;   // waves per backward workgroup (8 = 2 per SIMD)     // waves per backward workgroup (1 per SIMD, 512 VGPRs)
+constexpr int kBwdWaves = FCR_BWD_WAVES;   // waves per backward workgroup (8 = 2 per SIMD)
 constexpr float kP1Max = 2.122366f;  // Functions.py:1411 (32e6 / p1 max_abs_)
 constexpr float kP2Max = 1.036233f;  // Functions.py:1411 (32e6 / p2 max_abs_)
 
 template <int HS>
 struct Geo {
-    static constexpr int KS0 = 2 + HS;
-    static constexpr int KS1 = 2 * HS;
-    static constexpr int KB = 4 * HS;
     static constexpr int HQ = (HS + 3) / 4;   // 16-B quads per unit-slot vector (sequence slabs)
-    static constexpr int NB0 = (HS + 2 + 3) / 4;
-    static constexpr int NB1 = (2 * HS + 3) / 4;
-    static constexpr int KQ0 = (KS0 + 3) / 4 * 4;  // k-steps padded to whole k-quads
-    static constexpr int KQ1 = (KS1 + 3) / 4 * 4;
-    static constexpr int FA0 = HS * KQ0 * kWave;  // floats
-    static constexpr int FA1 = HS * KQ1 * kWave;
-    static constexpr int BA0 = NB0 * KB * kWave;
-    static constexpr int BA1 = NB1 * KB * kWave;
-    // LDS map (floats): [0, A) the layer-1/2 fragments of the current phase (refilled per phase),
-    // [A, A+B) the layer-0 fragments (resident for the whole kernel), then the controller records,
-    // fc.weight in lane layout and fc.bias (resident).
-    static constexpr int FNP = kMS * 4 * kFnpStride;
-    static constexpr int FCP = kOut * HS * 4;
-    static constexpr int MISC = FNP + FCP + 4;
-    static constexpr int LDS_FWD = (FA1 + FA0 + MISC) * 4;  // bytes
-    static constexpr int LDS_BWD = (BA1 + BA0 + MISC) * 4;
 };
 
 struct Packed {                    // device pointers into the workspace
-    const float *fa[3];            // forward fragments  [r][s][64]
-    const float *ba[3];            // backward fragments [tau][s'][64]
+    const float *fa[3];            // forward fragments (fcr_f16.h) [r][kb][hi|lo][64][8 halves]
+    const float *img[3];           // backward weight images (fcr_img.h) [hi|lo][row][RB bytes]
     const float *fcp;              // fc.weight in lane layout [o][slot][q]
     const float *fcb;              // fc.bias [4]
     const float *fnp;              // controller records [m][q][8]
 };
 
+// Sequence slabs (per wave, each address written once per call):
+//   hseq, cseq [wave][j][layer][t][quad][64]  h_t and c_t of every cell, 4 unit slots per 16-B quad
+//   xw         [wave][j][t][64]               layer-0 window row t of window j (col q, col 4)
+//   dseq       [wave][j][2][t][quad][64]      backward dx of layers 2, 1 (inputs of layers 1, 0)
+//   dxrow      [wave][j][t][64]               backward window-row gradients (col q, col 4)
 struct FwdArgs {
     int B, N;
     float alpha;
     const float *X, *u0, *states, *noise;
     float *cost, *command, *error, *prediction, *xhat_user, *xhat_ws, *loss_part;
-    f32x4 *hseq;     // [wave][j][2][t][quad][64] layer-0/1 outputs handed to the next layer phase
-    f32x4 *gates;    // [wave][j][l][t][slot][64] (dh/dc, dh/do, dc/di, dc/df) per cell, or null
-    f32x2 *cstore;   // [wave][j][l][t][slot][64] (dc/dg, f) per cell, or null
+    f32x4 *hseq;     // layers 0, 1 always (the next phase's input); layer 2 with `keep`
+    f32x4 *cseq;     // with `keep` (null otherwise)
+    f32x2 *xw;       // with `keep`
     Packed p;
 };
 
@@ -99,10 +66,10 @@ struct BwdArgs {
     int B, N, hidden;
     float alpha;
     const float *X, *states, *prediction, *xhat, *dloss;
-    const f32x4 *gates;
-    const f32x2 *cstore;
-    f32x4 *dseq;     // [wave][j][2][t][quad][64] dx of layers 2 and 1 (inputs of layers 1 and 0)
-    f32x2 *dxrow;    // [wave][j][t][64] window-row gradients (col q in lane group q, col 4 in group 0)
+    const f32x4 *hseq, *cseq;
+    const f32x2 *xw;
+    f32x4 *dseq;
+    f32x2 *dxrow;
     float *g_u0;
     float *dv;       // [B][N] d loss / d (controller pre-Hardtanh output) of the call fed by step j
     Packed p;

@@ -1,4 +1,5 @@
-// fcr_pack.h — weight packing into MFMA fragment order, and fixed-order reductions.
+// fcr_pack.h — small-parameter packing (controller, readout) and fixed-order reductions. The LSTM
+// weights are packed by pack_fwd16_kernel (fcr_f16.h) and pack_img_kernel (fcr_img.h).
 #pragma once
 #include "fcr_common.h"
 
@@ -7,89 +8,8 @@ namespace fcr {
 struct PackArgs {
     int H, HS, CH;
     const float *wih[3], *whh[3], *fcw, *fcb, *cwi, *cbi, *cwo;
-    float *fa[3], *ba[3], *fcp, *fcbo, *fnp;
+    float *fcp, *fcbo, *fnp;
 };
-
-// Forward fragment, layout [r][k/4][lane][k%4]: element (r, s, lane) is A[rho][k] of k-step s with
-// rho = lane&15 -> unit 4r+(rho>>2), gate rho&3 (torch row gate*H + unit); k = lane>>4 -> input
-// index of k-step s (layer 0: s<2 window column 4s+k, else h unit 4(s-2)+k; layer>=1: s<HS
-// layer-below unit 4s+k, else h unit 4(s-HS)+k). Padding (unit >= H, column >= 5, s >= KS) is 0.
-__global__ void pack_fwd_kernel(PackArgs a, int l) {
-    const int H = a.H, HS = a.HS;
-    const int KS = l == 0 ? 2 + HS : 2 * HS;
-    const int KQ = (KS + 3) / 4 * 4;
-    const int n = HS * KQ * kWave;
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= n) return;
-    const int e = idx & 3, lane = (idx >> 2) & 63, rq = idx >> 8;
-    const int qd = rq % (KQ / 4), r = rq / (KQ / 4);
-    const int s = 4 * qd + e;
-    const int rho = lane & 15, kq = lane >> 4;
-    const int unit = 4 * r + (rho >> 2), gate = rho & 3;
-    float v = 0.0f;
-    if (unit < H && s < KS) {
-        const int grow = gate * H + unit;
-        if (l == 0) {
-            if (s < 2) {
-                const int col = 4 * s + kq;
-                if (col < kIn) v = a.wih[0][grow * kIn + col];
-            } else {
-                const int u = 4 * (s - 2) + kq;
-                if (u < H) v = a.whh[0][grow * H + u];
-            }
-        } else {
-            if (s < HS) {
-                const int u = 4 * s + kq;
-                if (u < H) v = a.wih[l][grow * H + u];
-            } else {
-                const int u = 4 * (s - HS) + kq;
-                if (u < H) v = a.whh[l][grow * H + u];
-            }
-        }
-    }
-    a.fa[l][idx] = v * (gate == 2 ? kTwoLog2e : kNegLog2e);   // exp2 argument scaling, see fwd_pointwise
-}
-
-// Backward fragment, layout [tau][r][lane][gamma]: element is A'[rho][k] of k-step s' = 4r+gamma
-// with rho = lane&15 -> output slot sigma = 4tau+(rho&3) in lane group qo = rho>>2, and
-// k = lane>>4 -> gate row gamma*H + 4r + k. Output slots: layer>=1: sigma<HS dx unit 4sigma+qo
-// (W_ih column), HS<=sigma<2HS dh_prev unit 4(sigma-HS)+qo (W_hh column); layer 0: sigma<HS dh_prev,
-// sigma==HS dx column qo, sigma==HS+1 dx column 4 (qo==0 only).
-__global__ void pack_bwd_kernel(PackArgs a, int l) {
-    const int H = a.H, HS = a.HS;
-    const int NB = l == 0 ? (HS + 2 + 3) / 4 : (2 * HS + 3) / 4;
-    const int n = NB * HS * kWave * 4;
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= n) return;
-    const int gate = idx & 3, lane = (idx >> 2) & 63, tr = idx >> 8;
-    const int r = tr % HS, tau = tr / HS;
-    const int rho = lane & 15, kq = lane >> 4;
-    const int sigma = 4 * tau + (rho & 3), qo = rho >> 2;
-    const int unit_k = 4 * r + kq;
-    float v = 0.0f;
-    if (unit_k < H) {
-        const int grow = gate * H + unit_k;
-        if (l == 0) {
-            if (sigma < HS) {
-                const int u = 4 * sigma + qo;
-                if (u < H) v = a.whh[0][grow * H + u];
-            } else if (sigma == HS) {
-                v = a.wih[0][grow * kIn + qo];
-            } else if (sigma == HS + 1 && qo == 0) {
-                v = a.wih[0][grow * kIn + 4];
-            }
-        } else {
-            if (sigma < HS) {
-                const int u = 4 * sigma + qo;
-                if (u < H) v = a.wih[l][grow * H + u];
-            } else if (sigma < 2 * HS) {
-                const int u = 4 * (sigma - HS) + qo;
-                if (u < H) v = a.whh[l][grow * H + u];
-            }
-        }
-    }
-    a.ba[l][idx] = v;
-}
 
 __global__ void pack_misc_kernel(PackArgs a) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
