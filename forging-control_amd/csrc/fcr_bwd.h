@@ -40,31 +40,34 @@ struct CellIn {
 
 // Where the next cell's inputs live: buffer descriptors over this wave's own slab regions (SGPRs)
 // and byte offsets (SGPRs), so every load's address is one shared lane-offset VGPR.
+// What the next cell reads is known at compile time from where the current one sits in its phase
+// (NX_L0: x from the window rows; NX_HC: t > 0, so h_{t-1}, c_{t-1} exist; NX_DIN: a din from above):
+// only those are fetched. A fetched-but-unused register would be reused at once, i.e. waited for.
 struct NextIn {
     __amdgpu_buffer_rsrc_t rh, rc, rx, rd;   // hseq, cseq, xw, dseq
     uint32_t x, h, c, d;
-    bool l0, hc, din;   // next is a layer-0 cell (x from xw); t > 0 (h, c exist); reads a din
 };
 
-template <int HS>
+template <int HS, int k = 0>
+__device__ __forceinline__ void ld_quads(f32x4 (&dst)[Geo<HS>::HQ], __amdgpu_buffer_rsrc_t r, uint32_t off, int lane) {
+    if constexpr (k < Geo<HS>::HQ) {
+        dst[k] = buf_ldq<quad_n<HS, k>()>(r, lane * 16, off + k * kWave * 16);
+        ld_quads<HS, k + 1>(dst, r, off, lane);
+    }
+}
+
+template <int HS, bool NX_L0, bool NX_HC, bool NX_DIN>
 __device__ __forceinline__ void load_xhd(CellIn<HS> &ci, const NextIn &n, int lane) {
     constexpr int HQ = Geo<HS>::HQ;
-    if (n.l0) {
+    if (NX_L0) {
         const f32x2 v = buf_ld2(n.rx, lane * 8, n.x);
         ci.x[0][0] = v[0];
         ci.x[0][1] = v[1];
     } else {
-#pragma unroll
-        for (int k = 0; k < HQ; ++k) ci.x[k] = buf_ld4(n.rh, lane * 16, n.x + k * kWave * 16);
+        ld_quads<HS>(ci.x, n.rh, n.x, lane);
     }
-    if (n.hc) {
-#pragma unroll
-        for (int k = 0; k < HQ; ++k) ci.h[k] = buf_ld4(n.rh, lane * 16, n.h + k * kWave * 16);
-    }
-    if (n.din) {
-#pragma unroll
-        for (int k = 0; k < HQ; ++k) ci.d[k] = buf_ld4(n.rd, lane * 16, n.d + k * kWave * 16);
-    }
+    if (NX_HC) ld_quads<HS>(ci.h, n.rh, n.h, lane);
+    if (NX_DIN) ld_quads<HS>(ci.d, n.rd, n.d, lane);
 }
 
 // inverse exp2 pre-scales of the packed gate rows (fcr_img.h), folded into the dgate scaling
@@ -80,7 +83,10 @@ constexpr float kInvTwoLog2e = 1.0f / kTwoLog2e;
 // slots, which bounds every dgate) before the f16 split, and the products scaled back: both exact.
 // Schedule: region kb issues the transposed products of dgate block kb (slots 2kb, 2kb+1) beside the
 // recomputed forward tiles 2kb+2, 2kb+3 and their gradients, which form block kb+1.
-template <int HS, bool L0, bool DIN, bool FIRST>
+#ifndef FCR_BWD_LAUNDER
+#define FCR_BWD_LAUNDER 1
+#endif
+template <int HS, bool L0, bool DIN, bool FIRST, bool NX_L0, bool NX_HC, bool NX_DIN>
 __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, const float (&ext)[HS],
                                          float (&dh)[HS], float (&dc)[HS], float (&dxo)[HS], float &dxq,
                                          float &dx4, CellIn<HS> &ci, const NextIn &nx) {
@@ -118,7 +124,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
 #pragma unroll
         for (int kb = KLO; kb < KHI; ++kb) fwd_operand<HS, L0, FIRST>(kb, x0, x1, xv, hv, bh[kb], bl[kb]);
     }
-    load_xhd<HS>(ci, nx, lane);   // x, h, din of this cell are consumed
+    load_xhd<HS, NX_L0, NX_HC, NX_DIN>(ci, nx, lane);   // x, h, din of this cell are consumed
 
     // recomputed forward tile r -> scaled dgates of slot r (4 values)
     auto fwd_grad = [&](int r, float *v) {
@@ -148,8 +154,10 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
         v[2] = dg * sg2;
         v[3] = dO * sg0;
         // c_{t-1} quad of slots 4k..4k+3 consumed: the next cell's comes in
-        if (((r & 3) == 3 || r == HS - 1) && nx.hc)
+        if (NX_HC && (r & 3) == 3)
             ci.c[r >> 2] = buf_ld4(nx.rc, lane * 16, nx.c + (r >> 2) * kWave * 16);
+        if (NX_HC && r == HS - 1 && (r & 3) != 3)
+            ci.c[r >> 2] = buf_ldq<quad_n<HS, (HS - 1) / 4>()>(nx.rc, lane * 16, nx.c + (r >> 2) * kWave * 16);
     };
     auto dgate_block = [&](int kbb, f16x8 &gh, f16x8 &gl) {
         float v[8];
@@ -173,6 +181,10 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
 #pragma unroll
     for (int kbb = 0; kbb < KBB; ++kbb) {
         sched_fence();
+#if FCR_BWD_LAUNDER
+        // recompute the XOR'ed image addresses in every region instead of keeping ~30 of them live
+        asm volatile("" : "+v"(fb), "+v"(tb));
+#endif
         const int cu = kbb & 1, nu = cu ^ 1;
         const bool two = 2 * kbb + 1 < HS;
 #pragma unroll
@@ -285,23 +297,18 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
             nl = l - 1;
             if (l == 0) { nl = 2; nj = j - 1; }
         }
-        const bool none = nj < 0;   // past the last cell: load nothing
-        if (none) { nj = 0; nl = 2; nt = 0; }
-        n.l0 = nl == 0;
+        if (nj < 0) { nj = 0; nl = 2; nt = 9; }   // past the last cell: reload a valid one (harmless)
         n.x = nl == 0 ? (uint32_t)((nj * kL + nt) * kWave * 8) : hoff(nj, nl > 0 ? nl - 1 : 0, nt);
-        n.hc = nt > 0 && !none;
         n.h = hoff(nj, nl, nt > 0 ? nt - 1 : 0);
         n.c = n.h;
-        n.din = nl < 2 && !none;
         n.d = (uint32_t)((nl < 2 ? doff(nj, nl + 1, nt) : 0) * 16);
         return n;
     };
     CellIn<HS> ci;
     {
         const NextIn f = next_of(N - 1, 2, kL);   // t = kL -> (N-1, 2, 9)
-        load_xhd<HS>(ci, f, lane);
-#pragma unroll
-        for (int k = 0; k < Geo<HS>::HQ; ++k) ci.c[k] = buf_ld4(f.rc, lane * 16, f.c + k * kWave * 16);
+        load_xhd<HS, false, true, false>(ci, f, lane);
+        ld_quads<HS>(ci.c, f.rc, f.c, lane);
     }
 
     for (int j = N - 1; j >= 0; --j) {
@@ -356,42 +363,55 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         stagger();
 #pragma unroll
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
-        for (int t = kL - 1; t >= 1; --t) {
+        // t = 9 .. 2: the next cell is t-1 of the same layer; t = 1: the next is the FIRST cell (no
+        // h, c); t = 0: the next is t = 9 of the layer below (or of layer 2 of the previous window)
+        for (int t = kL - 1; t >= 2; --t) {
 #pragma unroll
             for (int r = 0; r < HS; ++r) dab[r] = (t == kL - 1) ? dh_out[r] : 0.0f;
-            bwd_cell<HS, false, false, false>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0, unused1, ci,
-                                              next_of(j, 2, t));
+            bwd_cell<HS, false, false, false, false, true, false>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
+                                                                unused1, ci, next_of(j, 2, t));
             store_quads<HS>(dseq_w + doff(j, 2, t), dxo, lane);
         }
 #pragma unroll
         for (int r = 0; r < HS; ++r) dab[r] = 0.0f;
-        bwd_cell<HS, false, false, true>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0, unused1, ci,
-                                         next_of(j, 2, 0));
+        bwd_cell<HS, false, false, false, false, false, false>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
+                                                             unused1, ci, next_of(j, 2, 1));
+        store_quads<HS>(dseq_w + doff(j, 2, 1), dxo, lane);
+        bwd_cell<HS, false, false, true, false, true, true>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
+                                                          unused1, ci, next_of(j, 2, 0));
         store_quads<HS>(dseq_w + doff(j, 2, 0), dxo, lane);
         // ---- layer 1 ----
         lds_fill(lw, a.p.img[1], LD::IMG1 / 4);
         stagger();
 #pragma unroll
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
-        for (int t = kL - 1; t >= 1; --t) {
-            bwd_cell<HS, false, true, false>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0, unused1, ci,
-                                             next_of(j, 1, t));
+        for (int t = kL - 1; t >= 2; --t) {
+            bwd_cell<HS, false, true, false, false, true, true>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
+                                                              unused1, ci, next_of(j, 1, t));
             store_quads<HS>(dseq_w + doff(j, 1, t), dxo, lane);
         }
-        bwd_cell<HS, false, true, true>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0, unused1, ci,
-                                        next_of(j, 1, 0));
+        bwd_cell<HS, false, true, false, false, false, true>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
+                                                           unused1, ci, next_of(j, 1, 1));
+        store_quads<HS>(dseq_w + doff(j, 1, 1), dxo, lane);
+        bwd_cell<HS, false, true, true, true, true, true>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
+                                                        unused1, ci, next_of(j, 1, 0));
         store_quads<HS>(dseq_w + doff(j, 1, 0), dxo, lane);
         // ---- layer 0: dx -> window-row gradients ----
 #pragma unroll
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
-        for (int t = kL - 1; t >= 1; --t) {
+        for (int t = kL - 1; t >= 2; --t) {
             float dxq, dx4;
-            bwd_cell<HS, true, true, false>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci, next_of(j, 0, t));
+            bwd_cell<HS, true, true, false, true, true, true>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
+                                                            next_of(j, 0, t));
             buf_st2(rr, lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{dxq, dx4});   // row j+t
         }
         {
             float dxq, dx4;
-            bwd_cell<HS, true, true, true>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci, next_of(j, 0, 0));
+            bwd_cell<HS, true, true, false, true, false, true>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
+                                                             next_of(j, 0, 1));
+            buf_st2(rr, lane * 8, (uint32_t)((j * kL + 1) * kWave * 8), f32x2{dxq, dx4});   // row j+1
+            bwd_cell<HS, true, true, true, false, true, false>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
+                                                             next_of(j, 0, 0));
             buf_st2(rr, lane * 8, (uint32_t)((j * kL) * kWave * 8), f32x2{dxq, dx4});   // row j
         }
     }

@@ -154,6 +154,30 @@ __device__ __forceinline__ f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t voff
 __device__ __forceinline__ f32x2 buf_ld2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     return __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0));
 }
+// Quad k of a unit-slot vector with only its first n (1..4) slots loaded: a padding lane of a partial
+// last quad that is loaded but never read is a register the compiler reuses at once — i.e. waits for.
+template <int n>
+__device__ __forceinline__ f32x4 buf_ldq(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    f32x4 q = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (n == 4) {
+        q = buf_ld4(r, voff, soff);
+    } else if (n == 3) {
+        typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+        const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)voff, (int)soff, 0);
+        q[0] = __builtin_bit_cast(float, v[0]);
+        q[1] = __builtin_bit_cast(float, v[1]);
+        q[2] = __builtin_bit_cast(float, v[2]);
+    } else if (n == 2) {
+        const f32x2 v = buf_ld2(r, voff, soff);
+        q[0] = v[0];
+        q[1] = v[1];
+    } else {
+        q[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, (int)soff, 0));
+    }
+    return q;
+}
+template <int HS, int k>
+constexpr int quad_n() { return HS - 4 * k >= 4 ? 4 : HS - 4 * k; }
 
 __device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, f32x2 v) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int, v), r,
@@ -189,10 +213,16 @@ template <int HS>
 __device__ __forceinline__ void load_quads(float (&v)[HS], const f32x4 *src, int lane) {
 #pragma unroll
     for (int k = 0; k < (HS + 3) / 4; ++k) {
-        const f32x4 q = src[k * kWave + lane];
+        const float *p = reinterpret_cast<const float *>(src + k * kWave + lane);
+        if (4 * k + 4 <= HS) {   // full quad
+            const f32x4 q = src[k * kWave + lane];
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-            if (4 * k + e < HS) v[4 * k + e] = q[e];
+            for (int e = 0; e < 4; ++e) v[4 * k + e] = q[e];
+        } else {                 // partial last quad: only the slots that exist (see buf_ldq)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (4 * k + e < HS) v[4 * k + e] = p[e];
+        }
     }
 }
 
