@@ -31,7 +31,7 @@ int fail(int code, const char *fmt, ...) {
 
 struct Layout {
     int HS, nw, nw_pad;
-    size_t fa[3], img[3], fcp, fcb, fnp, xhat, dv, loss_part, fnn_part, hseq, cseq, xw, dseq, dxrow, total;
+    size_t fa[3], img[3], fcp, fcb, fnp, xhat, dv, loss_part, fnn_part, hseq, cseq, xw, dseq, dxrow, stamp, total;
     int ctrl_blocks;
 };
 
@@ -88,6 +88,9 @@ Layout make_layout(const fcr_dims *d, int with_backward) {
         L.dseq = take(sizeof(f32x4) * (size_t)L.nw_pad * d->N * 2 * kL * ((HS + 3) / 4) * kWave);
         L.dxrow = take(sizeof(f32x2) * (size_t)L.nw_pad * d->N * kL * kWave);
     }
+#if FCR_STAMP
+    L.stamp = take(sizeof(unsigned long long) * L.nw_pad * 8);
+#endif
     L.total = off;
     return L;
 }
@@ -154,6 +157,11 @@ extern "C" {
 const char *fcr_last_error(void) { return g_err; }
 
 int fcr_abi_version(void) { return FCR_ABI_VERSION; }
+
+#if FCR_STAMP
+// diagnostic builds: byte offset (in ws) of the per-wave cycle sums [nw_pad][8] of the backward
+size_t fcr_debug_stamp_offset(const fcr_dims *d) { return make_layout(d, 1).stamp; }
+#endif
 
 int fcr_workspace_size(const fcr_dims *dims, int with_backward, size_t *bytes) {
     int rc = check_dims(dims);
@@ -275,6 +283,9 @@ int fcr_backward(const fcr_dims *d, const float *X, const float *states, const f
     ba.dxrow = (f32x2 *)(base + L.dxrow);
     ba.g_u0 = g_u0;
     ba.dv = (float *)(base + L.dv);
+#if FCR_STAMP
+    ba.stamp = (unsigned long long *)(base + L.stamp);
+#endif
     ba.p = packed_ptrs(L, base);
     switch (d->H) {
         case 16: rc = launch_bwd<4>(ba, L, s); break;

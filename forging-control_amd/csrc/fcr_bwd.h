@@ -72,7 +72,6 @@ __device__ __forceinline__ void load_xhd(CellIn<HS> &ci, const NextIn &n, int la
 
 // inverse exp2 pre-scales of the packed gate rows (fcr_img.h), folded into the dgate scaling
 constexpr float kInvNegLog2e = 1.0f / kNegLog2e;
-constexpr float kInvTwoLog2e = 1.0f / kTwoLog2e;
 
 // One backward cell for 16 trajectories. L0: outputs dh_prev and the window-row gradients dxq (column
 // q), dx4 (column 4, lane group 0); else dxo (layer-below h slots) and dh_prev. DIN: the incoming dh
@@ -86,10 +85,35 @@ constexpr float kInvTwoLog2e = 1.0f / kTwoLog2e;
 #ifndef FCR_BWD_LAUNDER
 #define FCR_BWD_LAUNDER 1
 #endif
+#ifndef FCR_PRIO
+#define FCR_PRIO 1
+#endif
+#ifndef FCR_STAMP
+#define FCR_STAMP 0   // diagnostic: per-wave s_memtime sums of the cell's sections (ws tail)
+#endif
+struct Stamps {
+    unsigned long long t[8];   // prologue, regions, epilogue, cells, -, window head, fill 2, fill 1
+};
+__device__ __forceinline__ unsigned long long stamp_now() {
+#if FCR_STAMP
+    return __builtin_amdgcn_s_memtime();
+#else
+    return 0;
+#endif
+}
+
 template <int HS, bool L0, bool DIN, bool FIRST, bool NX_L0, bool NX_HC, bool NX_DIN>
 __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, const float (&ext)[HS],
                                          float (&dh)[HS], float (&dc)[HS], float (&dxo)[HS], float &dxq,
-                                         float &dx4, CellIn<HS> &ci, const NextIn &nx) {
+                                         float &dx4, CellIn<HS> &ci, const NextIn &nx, Stamps &sp) {
+    const unsigned long long t0 = stamp_now();
+#if FCR_PRIO
+    // the two waves of a SIMD take turns at the higher issue priority, cell by cell, so neither runs
+    // ahead of the other between the phase barriers (oldest-first arbitration otherwise skews them)
+    if (sp.t[4] & 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+    sp.t[4] ^= 1;
+#endif
     using I = Img<HS, L0>;
     using G = Geo16<HS>;
     constexpr int KB = I::KB, NB = I::NB, KBB = I::KBB;
@@ -109,7 +133,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     m = fmaxf(m, __shfl_xor(m, 32));
     const int e = max(__builtin_amdgcn_frexp_expf(m), -100);   // m < 2^e; all-zero -> e = 0
     const float up = __builtin_amdgcn_ldexpf(1.0f, 13 - e), down = __builtin_amdgcn_ldexpf(1.0f, e - 13);
-    const float sg0 = up * kInvNegLog2e, sg2 = up * kInvTwoLog2e;   // gates i, f, o / g
+    const float sg0 = up * kInvNegLog2e;   // dgate scale (the g row's -0.5 is applied per slot)
 
     // ---- the recomputation's B operands (this cell's x_t and h_{t-1}) ----
     f16x8 bh[KB], bl[KB];
@@ -126,15 +150,22 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     }
     load_xhd<HS, NX_L0, NX_HC, NX_DIN>(ci, nx, lane);   // x, h, din of this cell are consumed
 
-    // recomputed forward tile r -> scaled dgates of slot r (4 values)
-    auto fwd_grad = [&](int r, float *v) {
-        f32x4 a = {0.0f, 0.0f, 0.0f, 0.0f};
+    // Recomputed forward tile r: its MFMA chain, issued two regions before its result is used (two
+    // accumulators over alternate k-blocks halve the dependent-MFMA chain).
+    auto fwd_tile = [&](int r, f32x4 &a) {
+        // the lo image through its own (opaque) base: with a visible constant distance the compiler
+        // pairs each hi and lo read into one ds_read2st64_b64, whose banking is not conflict-free
+        uint32_t fbl = fb + LO;
+        asm volatile("" : "+v"(fbl));
+        f32x4 a2 = {0.0f, 0.0f, 0.0f, 0.0f};
+        a = a2;
 #pragma unroll
         for (int kb = KLO; kb < KHI; ++kb) {
             const uint32_t a0 = (fb ^ (8u * (8 * kb))) + r * TILE, a1 = (fb ^ (8u * (8 * kb + 1))) + r * TILE;
+            const uint32_t b0 = (fbl ^ (8u * (8 * kb))) + r * TILE, b1 = (fbl ^ (8u * (8 * kb + 1))) + r * TILE;
             f16x8 ah, al;
             const f16x4 h0 = lds_b64_f16(a0), h1 = lds_b64_f16(a1);
-            const f16x4 l0 = lds_b64_f16(a0 + LO), l1 = lds_b64_f16(a1 + LO);
+            const f16x4 l0 = lds_b64_f16(b0), l1 = lds_b64_f16(b1);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 ah[k] = h0[k];
@@ -142,42 +173,60 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
                 al[k] = l0[k];
                 al[4 + k] = l1[k];
             }
-            a = mma3(ah, al, bh[kb], bl[kb], a);
+            if (((kb - KLO) & 1) == 0) a = mma3(ah, al, bh[kb], bl[kb], a);
+            else a2 = mma3(ah, al, bh[kb], bl[kb], a2);
         }
+        if (KHI - KLO > 1) a += a2;
+    };
+    // pointwise + cell gradient of slot r from its pre-activations -> 4 scaled dgates
+    auto slot_grad = [&](int r, f32x4 a, float *v) {
         f32x4 P;
         f32x2 Q;
         lstm_point_grad<FIRST>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], P, Q);
         float di, df, dg, dO;
         cell_grad(P, Q, dh[r], dc[r], di, df, dg, dO);
-        v[0] = di * sg0;
-        v[1] = df * sg0;
-        v[2] = dg * sg2;
-        v[3] = dO * sg0;
+        v[0] = di;              // the trajectory scale (and the exp2 pre-scale) is applied in the split;
+        v[1] = df;              // the g row's pre-scale is -2x that of i, f, o: exact
+        v[2] = dg * -0.5f;
+        v[3] = dO;
         // c_{t-1} quad of slots 4k..4k+3 consumed: the next cell's comes in
         if (NX_HC && (r & 3) == 3)
             ci.c[r >> 2] = buf_ld4(nx.rc, lane * 16, nx.c + (r >> 2) * kWave * 16);
         if (NX_HC && r == HS - 1 && (r & 3) != 3)
             ci.c[r >> 2] = buf_ldq<quad_n<HS, (HS - 1) / 4>()>(nx.rc, lane * 16, nx.c + (r >> 2) * kWave * 16);
     };
-    auto dgate_block = [&](int kbb, f16x8 &gh, f16x8 &gl) {
+    // forward MFMAs of slot pair kbb into fa[.][0..1]
+    auto fwd_pair = [&](int kbb, f32x4 (&fp)[2]) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            if (2 * kbb + u < HS) fwd_tile(2 * kbb + u, fp[u]);
+    };
+    // dgate block kbb (B operand of the transposed product) from the pair's pre-activations
+    auto dgate_block = [&](int kbb, const f32x4 (&fp)[2], f16x8 &gh, f16x8 &gl) {
         float v[8];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int r = 2 * kbb + u;
             if (r < HS) {
-                fwd_grad(r, v + 4 * u);
+                slot_grad(r, fp[u], v + 4 * u);
             } else {
                 v[4 * u] = v[4 * u + 1] = v[4 * u + 2] = v[4 * u + 3] = 0.0f;
             }
         }
-        split8(v, gh, gl);
+        split8s(v, sg0, gh, gl);
     };
 
+    // Pipeline: region kbb issues the forward MFMAs of pair kbb+2, the transposed products of dgate
+    // block kbb, and the pointwise/gradient VALU of pair kbb+1 (whose MFMAs were issued a region ago).
     f32x4 acc[NB];
 #pragma unroll
     for (int k = 0; k < NB; ++k) acc[k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    f32x4 fa[3][2];
     f16x8 gh[2], gl[2];
-    dgate_block(0, gh[0], gl[0]);
+    fwd_pair(0, fa[0]);
+    if (KBB > 1) fwd_pair(1, fa[1]);
+    dgate_block(0, fa[0], gh[0], gl[0]);
+    const unsigned long long t1 = stamp_now();
 #pragma unroll
     for (int kbb = 0; kbb < KBB; ++kbb) {
         sched_fence();
@@ -187,6 +236,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
 #endif
         const int cu = kbb & 1, nu = cu ^ 1;
         const bool two = 2 * kbb + 1 < HS;
+        if (kbb + 2 < KBB) fwd_pair(kbb + 2, fa[(kbb + 2) % 3]);
 #pragma unroll
         for (int tau = 0; tau < NB; ++tau) {
             const uint32_t at = (tb ^ (8u * (8 * (tau >> 1) + (tau & 1)))) + 2 * kbb * TILE;
@@ -210,9 +260,10 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
             if (kbb > 0) asm volatile("" : "+v"(acc[tau]));
             acc[tau] = mma3(ah, al, gh[cu], gl[cu], acc[tau]);
         }
-        if (kbb + 1 < KBB) dgate_block(kbb + 1, gh[nu], gl[nu]);
+        if (kbb + 1 < KBB) dgate_block(kbb + 1, fa[(kbb + 1) % 3], gh[nu], gl[nu]);
     }
     sched_fence();
+    const unsigned long long t2 = stamp_now();
     if (L0) {
 #pragma unroll
         for (int s = 0; s < HS; ++s) dh[s] = acc[s >> 2][s & 3] * down;
@@ -224,6 +275,13 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
             dxo[s] = acc[s >> 2][s & 3] * down;
             dh[s] = acc[(HS + s) >> 2][(HS + s) & 3] * down;
         }
+    }
+    if (FCR_STAMP) {
+        const unsigned long long t3 = stamp_now();
+        sp.t[0] += t1 - t0;
+        sp.t[1] += t2 - t1;
+        sp.t[2] += t3 - t2;
+        sp.t[3] += 1;
     }
 }
 
@@ -304,6 +362,8 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         n.d = (uint32_t)((nl < 2 ? doff(nj, nl + 1, nt) : 0) * 16);
         return n;
     };
+    Stamps sp = {{0, 0, 0, 0, (unsigned long long)((threadIdx.x >> 8) & 1), 0, 0, 0}};
+    const unsigned long long tk0 = stamp_now();
     CellIn<HS> ci;
     {
         const NextIn f = next_of(N - 1, 2, kL);   // t = kL -> (N-1, 2, 9)
@@ -312,6 +372,7 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
     }
 
     for (int j = N - 1; j >= 0; --j) {
+        const unsigned long long tw0 = stamp_now();
         const float *lfnp_j = opaque(lfnp), *lfcp_j = opaque(lfcp);
         const float x0 = xh[j * kOut + 0], x1 = xh[j * kOut + 1], x2 = xh[j * kOut + 2],
                     x3 = xh[j * kOut + 3];
@@ -359,8 +420,14 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
             dh_out[r] = fp[0] * d0 + fp[HS * 4] * d1 + fp[2 * HS * 4] * d2 + fp[3 * HS * 4] * d3;
         }
         float unused0, unused1;
-        lds_fill(lw, a.p.img[2], LD::IMG1 / 4);
+        const unsigned long long tw1 = stamp_now();
+        lds_fill<LD::IMG1, kBwdWaves>(lw, a.p.img[2]);
         stagger();
+        if (FCR_STAMP) {
+            const unsigned long long tw2 = stamp_now();
+            sp.t[5] += tw1 - tw0;
+            sp.t[6] += tw2 - tw1;
+        }
 #pragma unroll
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
         // t = 9 .. 2: the next cell is t-1 of the same layer; t = 1: the next is the FIRST cell (no
@@ -369,32 +436,34 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
 #pragma unroll
             for (int r = 0; r < HS; ++r) dab[r] = (t == kL - 1) ? dh_out[r] : 0.0f;
             bwd_cell<HS, false, false, false, false, true, false>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
-                                                                unused1, ci, next_of(j, 2, t));
+                                                                unused1, ci, next_of(j, 2, t), sp);
             store_quads<HS>(dseq_w + doff(j, 2, t), dxo, lane);
         }
 #pragma unroll
         for (int r = 0; r < HS; ++r) dab[r] = 0.0f;
         bwd_cell<HS, false, false, false, false, false, false>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
-                                                             unused1, ci, next_of(j, 2, 1));
+                                                             unused1, ci, next_of(j, 2, 1), sp);
         store_quads<HS>(dseq_w + doff(j, 2, 1), dxo, lane);
         bwd_cell<HS, false, false, true, false, true, true>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
-                                                          unused1, ci, next_of(j, 2, 0));
+                                                          unused1, ci, next_of(j, 2, 0), sp);
         store_quads<HS>(dseq_w + doff(j, 2, 0), dxo, lane);
         // ---- layer 1 ----
-        lds_fill(lw, a.p.img[1], LD::IMG1 / 4);
+        const unsigned long long tw3 = stamp_now();
+        lds_fill<LD::IMG1, kBwdWaves>(lw, a.p.img[1]);
         stagger();
+        if (FCR_STAMP) sp.t[7] += stamp_now() - tw3;
 #pragma unroll
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
         for (int t = kL - 1; t >= 2; --t) {
             bwd_cell<HS, false, true, false, false, true, true>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
-                                                              unused1, ci, next_of(j, 1, t));
+                                                              unused1, ci, next_of(j, 1, t), sp);
             store_quads<HS>(dseq_w + doff(j, 1, t), dxo, lane);
         }
         bwd_cell<HS, false, true, false, false, false, true>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
-                                                           unused1, ci, next_of(j, 1, 1));
+                                                           unused1, ci, next_of(j, 1, 1), sp);
         store_quads<HS>(dseq_w + doff(j, 1, 1), dxo, lane);
         bwd_cell<HS, false, true, true, true, true, true>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
-                                                        unused1, ci, next_of(j, 1, 0));
+                                                        unused1, ci, next_of(j, 1, 0), sp);
         store_quads<HS>(dseq_w + doff(j, 1, 0), dxo, lane);
         // ---- layer 0: dx -> window-row gradients ----
 #pragma unroll
@@ -402,16 +471,16 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         for (int t = kL - 1; t >= 2; --t) {
             float dxq, dx4;
             bwd_cell<HS, true, true, false, true, true, true>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
-                                                            next_of(j, 0, t));
+                                                            next_of(j, 0, t), sp);
             buf_st2(rr, lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{dxq, dx4});   // row j+t
         }
         {
             float dxq, dx4;
             bwd_cell<HS, true, true, false, true, false, true>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
-                                                             next_of(j, 0, 1));
+                                                             next_of(j, 0, 1), sp);
             buf_st2(rr, lane * 8, (uint32_t)((j * kL + 1) * kWave * 8), f32x2{dxq, dx4});   // row j+1
             bwd_cell<HS, true, true, true, false, true, false>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
-                                                             next_of(j, 0, 0));
+                                                             next_of(j, 0, 0), sp);
             buf_st2(rr, lane * 8, (uint32_t)((j * kL) * kWave * 8), f32x2{dxq, dx4});   // row j
         }
     }
@@ -420,6 +489,17 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
     float du0 = 2.0f * alpha * wgt * (pred[0] - s84);
     if (N > 1) du0 += 2.0f * alpha * wgt * (pred[0] - pred[1]);
     if (valid && q == 0) a.g_u0[b] = g_u0_rows + du0;
+    if (FCR_STAMP && lane == 0) {
+        unsigned long long *o = a.stamp + (size_t)wave * 8;
+        o[0] = sp.t[0];
+        o[1] = sp.t[1];
+        o[2] = sp.t[2];
+        o[3] = sp.t[3];
+        o[4] = stamp_now() - tk0;
+        o[5] = sp.t[5];
+        o[6] = sp.t[6];
+        o[7] = sp.t[7];
+    }
 }
 
 }  // namespace fcr

@@ -72,6 +72,7 @@ struct BwdArgs {
     f32x2 *dxrow;
     float *g_u0;
     float *dv;       // [B][N] d loss / d (controller pre-Hardtanh output) of the call fed by step j
+    unsigned long long *stamp;   // FCR_STAMP diagnostic builds only: per-wave cycle sums
     Packed p;
 };
 
@@ -191,9 +192,19 @@ __device__ __forceinline__ void lds_copy(float *lw, const float *__restrict__ sr
     for (int i = threadIdx.x; i < nfloats / 4; i += blockDim.x) d4[i] = s4[i];
 }
 // Refill the per-phase region. Every wave of the workgroup calls this at the same program point.
-__device__ __forceinline__ void lds_fill(float *lw, const float *__restrict__ src, int nfloats) {
+// Refill the per-phase LDS region with LDS-DMA (global_load_lds_dwordx4: each wave instruction moves
+// one 1 KiB chunk straight into LDS, no VGPRs): after the barrier that retires the old image, every
+// wave issues its chunks back to back; the barrier after them waits for the DMA (vmcnt) and publishes.
+template <int NBYTES, int NWAVES>
+__device__ __forceinline__ void lds_fill(float *lw, const float *__restrict__ src) {
+    static_assert(NBYTES % 1024 == 0, "image must be whole 1 KiB chunks");
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     __syncthreads();
-    lds_copy(lw, src, nfloats);
+    for (int c = wv; c < NBYTES / 1024; c += NWAVES)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void *)((const char *)src + c * 1024 + lane * 16),
+            (__attribute__((address_space(3))) void *)((__attribute__((address_space(3))) char *)lw + c * 1024), 16,
+            0, 0);
     __syncthreads();
 }
 

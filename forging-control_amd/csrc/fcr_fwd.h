@@ -166,7 +166,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
 #pragma unroll
         for (int l = 1; l < kLayers; ++l) {
             const bool keep_h = l == 1 || STORE;   // layer 2's h_t is only the backward's h_{t-1}
-            lds_fill(lw, a.p.fa[l], G::FA1);
+            lds_fill<G::FA1 * 4, kFwdWaves>(lw, a.p.fa[l]);
             stagger();
             load_quads<HS>(xc, SEQ_H(l - 1, 0), lane);
             load_quads<HS>(xn, SEQ_H(l - 1, 1), lane);

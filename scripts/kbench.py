@@ -34,7 +34,7 @@ def bind(path):
     return lib
 
 
-def main():
+def main(return_state=False):
     ap = argparse.ArgumentParser()
     ap.add_argument("libs", nargs="+")
     ap.add_argument("--batch", type=int, default=65536)
@@ -113,6 +113,8 @@ def main():
             h = a.sustain // 2
             times[i]["fwd"] = [evs[2 * k].elapsed_time(evs[2 * k + 1]) for k in range(h, a.sustain)]
             times[i]["bwd"] = [evs[2 * k + 1].elapsed_time(evs[2 * k + 2]) for k in range(h, a.sustain)]
+    if return_state:
+        return {"dims": dims, "ws": ws}
     for i, path in enumerate(a.libs):
         f, b = np.median(times[i]["fwd"]), np.median(times[i]["bwd"])
         print(json.dumps({"lib": os.path.basename(path), "fwd_ms": round(f, 3), "bwd_ms": round(b, 3),

@@ -1,0 +1,39 @@
+"""Read the backward's per-wave section cycle sums from an FCR_STAMP=1 build (diagnostic).
+
+    python scripts/stamp.py forging-control_amd/lib/libfcr_stamp.so [--batch 65536]
+Sections per cell: prologue (top: scale, operands, first forward pair), region loop, epilogue."""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+import kbench  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("lib")
+ap.add_argument("--batch", type=int, default=65536)
+a = ap.parse_args()
+sys.argv = [sys.argv[0], a.lib, "--batch", str(a.batch), "--rounds", "2"]
+lib = ctypes.CDLL(os.path.abspath(a.lib))
+lib.fcr_debug_stamp_offset.argtypes = [ctypes.POINTER(kbench._n.FcrDims)]
+lib.fcr_debug_stamp_offset.restype = ctypes.c_size_t
+state = kbench.main(return_state=True)
+dims, ws = state["dims"], state["ws"]
+off = lib.fcr_debug_stamp_offset(ctypes.byref(dims))
+nw = (a.batch + 15) // 16
+st = ws[off:off + nw * 64].view(torch.int64).reshape(nw, 8).cpu().numpy().astype(np.float64)
+cells = st[:, 3]
+print(f"waves {nw}, cells/wave {cells.mean():.0f}")
+names = ["prologue", "regions", "epilogue"]
+for k, nm in enumerate(names):
+    print(f"  {nm:9s} {np.mean(st[:, k] / cells):9.0f} cycles/cell")
+for k, nm in ((5, "window head (row grads, controller bwd)"), (6, "layer-2 image fill + barriers"), (7, "layer-1 image fill + barriers")):
+    print(f"  {nm:40s} {np.mean(st[:, k]) / 10:9.0f} cycles/window")
+print(f"  cell total {np.mean((st[:, 0] + st[:, 1] + st[:, 2]) / cells):9.0f} cycles/cell;"
+      f" kernel wave lifetime {np.mean(st[:, 4]):.3e} cycles, {np.mean(st[:, 4] / cells):.0f} per cell")
