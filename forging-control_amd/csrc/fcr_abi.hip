@@ -37,6 +37,12 @@ struct Layout {
 
 size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// Kernels are instantiated for 4, 8 and 13 unit slots (H <= 16, 32, 52); a smaller H runs in the next
+// tier with its padding units' weights zero — their gates stay at i = f = o = 1/2, g = 0, so c = h = 0
+// and they add nothing to any product (tests/test_gpu_parity.py: H = 40 against the oracle).
+constexpr int kMaxSlots = 13;
+int slot_tier(int H) { return H <= 16 ? 4 : (H <= 32 ? 8 : 13); }
+
 int check_dims(const fcr_dims *d) {
     if (!d) return fail(FCR_EINVAL, "dims is NULL");
     if (d->B < 1) return fail(FCR_EINVAL, "B=%d must be >= 1", d->B);
@@ -48,15 +54,15 @@ int check_dims(const fcr_dims *d) {
                     d->out_dim, d->ctrl_in);
     if (d->ctrl_hidden < 1 || d->ctrl_hidden > 4 * kMS)
         return fail(FCR_EUNSUPPORTED, "ctrl_hidden=%d: built for 1..52", d->ctrl_hidden);
-    if (!(d->H == 16 || d->H == 32 || d->H == 50))
-        return fail(FCR_EUNSUPPORTED, "H=%d: built for 16, 32, 50 (LDS-resident fragments)", d->H);
+    if (d->H < 1 || d->H > 4 * kMaxSlots)
+        return fail(FCR_EUNSUPPORTED, "H=%d: built for 1..%d (LDS-resident weight images)", d->H, 4 * kMaxSlots);
     if ((long long)d->B * d->N > (1LL << 31)) return fail(FCR_EINVAL, "B*N too large");
     return FCR_OK;
 }
 
 Layout make_layout(const fcr_dims *d, int with_backward) {
     Layout L{};
-    L.HS = (d->H + 3) / 4;
+    L.HS = slot_tier(d->H);
     L.nw = (d->B + kTile - 1) / kTile;
     constexpr int kPad = kFwdWaves > kBwdWaves ? kFwdWaves : kBwdWaves;
     L.nw_pad = (L.nw + kPad - 1) / kPad * kPad;  // covers both launch geometries
@@ -241,10 +247,10 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
     fa.cseq = with_backward ? (f32x4 *)(base + L.cseq) : nullptr;
     fa.xw = with_backward ? (f32x2 *)(base + L.xw) : nullptr;
     fa.p = packed_ptrs(L, base);
-    switch (d->H) {
-        case 16: rc = launch_fwd<4>(fa, L, s); break;
-        case 32: rc = launch_fwd<8>(fa, L, s); break;
-        case 50: rc = launch_fwd<13>(fa, L, s); break;
+    switch (L.HS) {
+        case 4: rc = launch_fwd<4>(fa, L, s); break;
+        case 8: rc = launch_fwd<8>(fa, L, s); break;
+        case 13: rc = launch_fwd<13>(fa, L, s); break;
         default: rc = fail(FCR_EUNSUPPORTED, "H=%d", d->H);
     }
     if (rc) return rc;
@@ -287,10 +293,10 @@ int fcr_backward(const fcr_dims *d, const float *X, const float *states, const f
     ba.stamp = (unsigned long long *)(base + L.stamp);
 #endif
     ba.p = packed_ptrs(L, base);
-    switch (d->H) {
-        case 16: rc = launch_bwd<4>(ba, L, s); break;
-        case 32: rc = launch_bwd<8>(ba, L, s); break;
-        case 50: rc = launch_bwd<13>(ba, L, s); break;
+    switch (L.HS) {
+        case 4: rc = launch_bwd<4>(ba, L, s); break;
+        case 8: rc = launch_bwd<8>(ba, L, s); break;
+        case 13: rc = launch_bwd<13>(ba, L, s); break;
         default: rc = fail(FCR_EUNSUPPORTED, "H=%d", d->H);
     }
     if (rc) return rc;

@@ -23,9 +23,10 @@ __device__ __forceinline__ void rot_left(float (&w)[kL]) {
 // One LSTM cell for 16 trajectories on the f16 matrix cores (fcr_f16.h): fragments
 // [r][kb][hi|lo][lane][8 halves]. L0: input is the window row (x0: column q in lane group q, x1:
 // column 4 in lane group 0); otherwise x = the layer-below h_t. FIRST: t = 0 (h_{t-1} = 0: those
-// k-blocks are skipped). The B operands are split once per cell and shared by all tiles; each k-block
-// is its own scheduling region with the next block's two fragment reads in flight; the cell update of
-// tile r-1 is issued in the first region of tile r, beside its MFMAs.
+// k-blocks are skipped). The B operands are split once per cell and shared by all tiles. Tiles go in
+// pairs, each with two accumulators over alternate k-blocks: four independent MFMA chains per
+// scheduling region (one region per k-block, the next block's four fragment reads in flight), and the
+// cell update of the previous pair issued in the first region of the next, beside its MFMAs.
 template <int HS, bool L0, bool FIRST>
 __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lane, float x0, float x1,
                                            const float (&x)[HS], const float (&hp)[HS], float (&c)[HS],
@@ -34,34 +35,57 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
     constexpr int KB = L0 ? G::KB0 : G::KB1;
     constexpr int KLO = (L0 && FIRST) ? G::XBLK : 0;
     constexpr int KHI = FIRST ? (L0 ? G::XBLK + 1 : G::KX1) : KB;
+    constexpr int NP = (HS + 1) / 2;   // tile pairs
     f16x8 bh[KB], bl[KB];
 #pragma unroll
     for (int kb = KLO; kb < KHI; ++kb) fwd_operand<HS, L0, FIRST>(kb, x0, x1, x, hp, bh[kb], bl[kb]);
-    f16x8 ah = lds_frag16(lw, KLO * 2, lane), al = lds_frag16(lw, KLO * 2 + 1, lane);
-    f32x4 prev = {0.0f, 0.0f, 0.0f, 0.0f};
+    // fragment reads of (tile r, block kb): hi, lo
+    auto rd = [&](int r, int kb, f16x8 &h, f16x8 &l) {
+        h = lds_frag16(lw, (r * KB + kb) * 2, lane);
+        l = lds_frag16(lw, (r * KB + kb) * 2 + 1, lane);
+    };
+    f16x8 ah[2], al[2];
+    rd(0, KLO, ah[0], al[0]);
+    if (HS > 1) rd(1, KLO, ah[1], al[1]);
+    f32x4 prev[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
 #pragma unroll
-    for (int r = 0; r < HS; ++r) {
-        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int p = 0; p < NP; ++p) {
+        const int r0 = 2 * p, r1 = 2 * p + 1;
+        const bool two = r1 < HS;
+        f32x4 acc[2][2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc[u][0] = acc[u][1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int kb = KLO; kb < KHI; ++kb) {
             sched_fence();
-            f16x8 nh = ah, nl = al;
+            // next region's fragments: (same pair, kb+1), else (next pair, KLO)
+            f16x8 nh[2] = {ah[0], ah[1]}, nl[2] = {al[0], al[1]};
             if (kb + 1 < KHI) {
-                nh = lds_frag16(lw, (r * KB + kb + 1) * 2, lane);
-                nl = lds_frag16(lw, (r * KB + kb + 1) * 2 + 1, lane);
-            } else if (r + 1 < HS) {
-                nh = lds_frag16(lw, ((r + 1) * KB + KLO) * 2, lane);
-                nl = lds_frag16(lw, ((r + 1) * KB + KLO) * 2 + 1, lane);
+                rd(r0, kb + 1, nh[0], nl[0]);
+                if (two) rd(r1, kb + 1, nh[1], nl[1]);
+            } else if (p + 1 < NP) {
+                rd(r0 + 2, KLO, nh[0], nl[0]);
+                if (r1 + 2 < HS) rd(r1 + 2, KLO, nh[1], nl[1]);
             }
-            acc = mma3(ah, al, bh[kb], bl[kb], acc);
-            if (kb == KLO && r > 0) lstm_point<FIRST>(prev, c[r - 1], c[r - 1], hout[r - 1]);
-            ah = nh;
-            al = nl;
+            const int ch = (kb - KLO) & 1;
+            acc[0][ch] = mma3(ah[0], al[0], bh[kb], bl[kb], acc[0][ch]);
+            if (two) acc[1][ch] = mma3(ah[1], al[1], bh[kb], bl[kb], acc[1][ch]);
+            if (kb == KLO && p > 0) {
+                lstm_point<FIRST>(prev[0], c[r0 - 2], c[r0 - 2], hout[r0 - 2]);
+                lstm_point<FIRST>(prev[1], c[r1 - 2], c[r1 - 2], hout[r1 - 2]);
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                ah[u] = nh[u];
+                al[u] = nl[u];
+            }
         }
-        prev = acc;
+        prev[0] = acc[0][0] + acc[0][1];
+        prev[1] = acc[1][0] + acc[1][1];
     }
     sched_fence();
-    lstm_point<FIRST>(prev, c[HS - 1], c[HS - 1], hout[HS - 1]);
+    lstm_point<FIRST>(prev[0], c[2 * NP - 2], c[2 * NP - 2], hout[2 * NP - 2]);
+    if (2 * NP - 1 < HS) lstm_point<FIRST>(prev[1], c[2 * NP - 1], c[2 * NP - 1], hout[2 * NP - 1]);
 }
 
 template <int HS, bool STORE>

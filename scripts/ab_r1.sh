@@ -5,6 +5,6 @@ cd $R
 mkdir -p gpurun_out
 timeout -k 10 400 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
 tail -3 gpurun_out/pytest_gpu.log
-LIBS="forging-control_amd/lib/libfcr_v3.so forging-control_amd/lib/libfcr.so $(ls forging-control_amd/lib/libfcr_*.so | grep -v _v3)"
+LIBS="forging-control_amd/lib/libfcr.so $(ls forging-control_amd/lib/libfcr_*.so)"
 timeout -k 10 400 python scripts/kbench.py $LIBS --rounds 2 --sustain 40 > gpurun_out/kbench.log 2>&1
 grep lib gpurun_out/kbench.log

@@ -215,3 +215,21 @@ def test_bad_shapes_raise(ref_params):
     X = torch.zeros(8, 3, device=DEV)
     with pytest.raises(ValueError):
         fca.MPCLoss(10, 20.0)(sim, ctrl, X, ctrl(X), torch.zeros(8, 9, 5, device=DEV), DEV)
+
+
+@pytest.mark.parametrize("H,B,N", [(40, 48, 4), (7, 33, 3), (21, 17, 2), (52, 20, 3)])
+def test_any_hidden_size_up_to_52(H, B, N):
+    """A hidden size between the built tiers (16, 32, 52 units) runs with zero padding units; checked
+    against the fp64 oracle on seeded synthetic weights (parity unpinned: no reference output)."""
+    from tests.golden.make_golden import synth_params
+    params = synth_params(H, 100 + H)
+    X, S, _ = _synth(B, N, 200 + H)
+    u0 = _u0(params, X)
+    o = run(params, X, u0, S, N, 20.0)
+    _, f, tape = R.rollout_forward(params, X, u0, S, N, 20.0)
+    g = R.rollout_backward(params, tape)
+    for k in FEATS:
+        assert relerr(o[k], f[k]) <= TOL, (H, k, relerr(o[k], f[k]))
+    assert relerr(o["xhat"], f["xhat"]) <= TOL
+    for k, _ in GRADS:
+        assert relerr(o[k], g[k]) <= TOL, (H, k, relerr(o[k], g[k]))
