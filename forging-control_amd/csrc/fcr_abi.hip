@@ -4,6 +4,7 @@
 // /root/reference/Unsupervised Learning/Functions.py:646 and :655. All launches are stream-ordered on
 // the caller's stream; nothing here allocates or synchronises.
 #include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -14,6 +15,7 @@
 #include "fcr_fwd.h"
 #include "fcr_img.h"
 #include "fcr_pack.h"
+#include "fcr_wide.h"
 
 namespace fcr {
 namespace {
@@ -41,6 +43,8 @@ size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 // tier with its padding units' weights zero — their gates stay at i = f = o = 1/2, g = 0, so c = h = 0
 // and they add nothing to any product (tests/test_gpu_parity.py: H = 40 against the oracle).
 constexpr int kMaxSlots = 13;
+constexpr int kMaxWideH = 2048;   // H > 4*kMaxSlots: the GEMM-per-cell path (fcr_wide.h)
+bool is_wide(const fcr_dims *d) { return d->H > 4 * kMaxSlots; }
 int slot_tier(int H) { return H <= 16 ? 4 : (H <= 32 ? 8 : 13); }
 
 int check_dims(const fcr_dims *d) {
@@ -54,8 +58,8 @@ int check_dims(const fcr_dims *d) {
                     d->out_dim, d->ctrl_in);
     if (d->ctrl_hidden < 1 || d->ctrl_hidden > 4 * kMS)
         return fail(FCR_EUNSUPPORTED, "ctrl_hidden=%d: built for 1..52", d->ctrl_hidden);
-    if (d->H < 1 || d->H > 4 * kMaxSlots)
-        return fail(FCR_EUNSUPPORTED, "H=%d: built for 1..%d (LDS-resident weight images)", d->H, 4 * kMaxSlots);
+    if (d->H < 1 || d->H > kMaxWideH)
+        return fail(FCR_EUNSUPPORTED, "H=%d: built for 1..%d", d->H, kMaxWideH);
     if ((long long)d->B * d->N > (1LL << 31)) return fail(FCR_EINVAL, "B*N too large");
     return FCR_OK;
 }
@@ -153,6 +157,243 @@ int launch_bwd(const BwdArgs &ba, const Layout &L, hipStream_t s) {
     return launch_check("fcr_bwd_kernel");
 }
 
+// ---------------------------------------------------------------------------------------------
+// H > 52: GEMM-per-cell path (fcr_wide.h)
+// ---------------------------------------------------------------------------------------------
+struct WideLayout {
+    size_t wih[3], whh[3], fcw, fcb, cwi, cbi, cwo, fcp, fcbo, fnp, xhat, tot, cmd, err, X0, Hs, Cs, G;
+    size_t Act, dH, dC, D[2], rowg, dv, fnn_part, total;
+    int ctrl_blocks;
+};
+
+WideLayout make_wide(const fcr_dims *d, int with_backward) {
+    WideLayout L{};
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += align_up(bytes);
+        return o;
+    };
+    const size_t B = d->B, N = d->N, H = d->H, F = sizeof(float);
+    for (int l = 0; l < kLayers; ++l) {
+        L.wih[l] = take(F * 4 * H * (l == 0 ? kIn : H));
+        L.whh[l] = take(F * 4 * H * H);
+    }
+    L.fcw = take(F * kOut * H);
+    L.fcb = take(F * kOut);
+    L.cwi = take(F * d->ctrl_hidden * kCtrlIn);
+    L.cbi = take(F * d->ctrl_hidden);
+    L.cwo = take(F * d->ctrl_hidden);
+    L.fcp = take(F * kOut * kMaxSlots * 4);
+    L.fcbo = take(F * kOut);
+    L.fnp = take(F * kMS * 4 * kFnpStride);
+    L.xhat = take(F * B * N * kOut);
+    L.tot = take(F * B);
+    L.cmd = take(F * B);
+    L.err = take(F * B);
+    L.X0 = take(F * kL * B * kIn);
+    L.Hs = take(F * kLayers * kL * B * H);
+    L.Cs = take(F * kLayers * kL * B * H);
+    L.G = take(F * B * 4 * H);
+    if (with_backward) {
+        L.Act = take(F * kLayers * kL * B * 4 * H);
+        L.dH = take(F * B * H);
+        L.dC = take(F * B * H);
+        L.D[0] = take(F * kL * B * H);
+        L.D[1] = take(F * kL * B * H);
+        L.rowg = take(F * (N + kL - 1) * B * kIn);
+        L.dv = take(F * B * N);
+        L.ctrl_blocks = (int)(((long long)B * N + kCtrlItems - 1) / kCtrlItems);
+        L.fnn_part = take(F * (size_t)L.ctrl_blocks * d->ctrl_hidden * 5);
+    }
+    L.total = off;
+    return L;
+}
+
+rocblas_handle blas_on(hipStream_t s) {
+    thread_local rocblas_handle h = nullptr;
+    if (!h && rocblas_create_handle(&h) != rocblas_status_success) return nullptr;
+    rocblas_set_stream(h, s);
+    return h;
+}
+
+// G (row-major B x 4H) (+)= X (B x K) . W^T, W row-major (4H x K) as torch stores it
+int gemm_xwt(rocblas_handle h, int B, int H4, int K, const float *W, const float *X, float beta, float *G) {
+    const float one = 1.0f;
+    const rocblas_status st = rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, H4, B, K, &one,
+                                            W, K, X, K, &beta, G, H4);
+    return st == rocblas_status_success ? FCR_OK : fail(FCR_EHIP, "rocblas_sgemm (forward) failed: %d", (int)st);
+}
+// dX (row-major B x K) (+)= dG (B x 4H) . W (4H x K)
+int gemm_gw(rocblas_handle h, int B, int H4, int K, const float *W, const float *dG, float beta, float *dX) {
+    const float one = 1.0f;
+    const rocblas_status st = rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, K, B, H4, &one, W,
+                                            K, dG, H4, &beta, dX, K);
+    return st == rocblas_status_success ? FCR_OK : fail(FCR_EHIP, "rocblas_sgemm (backward) failed: %d", (int)st);
+}
+
+WideArgs wide_args(const fcr_dims *d, const WideLayout &L, char *base) {
+    WideArgs a{};
+    a.B = d->B;
+    a.N = d->N;
+    a.H = d->H;
+    a.CH = d->ctrl_hidden;
+    a.alpha = d->alpha;
+    a.fcw = (const float *)(base + L.fcw);
+    a.fcb = (const float *)(base + L.fcb);
+    a.cwi = (const float *)(base + L.cwi);
+    a.cbi = (const float *)(base + L.cbi);
+    a.cwo = (const float *)(base + L.cwo);
+    a.xhat = (float *)(base + L.xhat);
+    a.tot = (float *)(base + L.tot);
+    a.cmd = (float *)(base + L.cmd);
+    a.err = (float *)(base + L.err);
+    a.X0 = (float *)(base + L.X0);
+    a.Hs = (float *)(base + L.Hs);
+    a.Cs = (float *)(base + L.Cs);
+    a.G = (float *)(base + L.G);
+    a.Act = L.Act ? (float *)(base + L.Act) : nullptr;
+    a.dH = L.dH ? (float *)(base + L.dH) : nullptr;
+    a.dC = L.dC ? (float *)(base + L.dC) : nullptr;
+    a.rowg = L.rowg ? (float *)(base + L.rowg) : nullptr;
+    a.dv = L.dv ? (float *)(base + L.dv) : nullptr;
+    return a;
+}
+
+// One window's cells, forward: 3 layers x 10 steps of [GEMM x_t W_ih^T, GEMM h_{t-1} W_hh^T, cell]
+int wide_cells(rocblas_handle h, const WideArgs &a, const WideLayout &L, char *base, bool keep_act, hipStream_t s) {
+    const int B = a.B, H = a.H;
+    const size_t cell = (size_t)B * H;
+    const int nb = (int)((cell + 255) / 256);
+    int rc;
+    for (int l = 0; l < kLayers; ++l) {
+        const float *wih = (const float *)(base + L.wih[l]), *whh = (const float *)(base + L.whh[l]);
+        for (int t = 0; t < kL; ++t) {
+            const float *x = l == 0 ? a.X0 + (size_t)t * B * kIn : a.Hs + ((size_t)(l - 1) * kL + t) * cell;
+            if ((rc = gemm_xwt(h, B, 4 * H, l == 0 ? kIn : H, wih, x, 0.0f, a.G))) return rc;
+            if (t > 0 && (rc = gemm_xwt(h, B, 4 * H, H, whh, a.Hs + ((size_t)l * kL + t - 1) * cell, 1.0f, a.G)))
+                return rc;
+            hipLaunchKernelGGL(wide_cell_kernel, dim3(nb), dim3(256), 0, s, (const float *)a.G,
+                               t > 0 ? (const float *)(a.Cs + ((size_t)l * kL + t - 1) * cell) : nullptr,
+                               a.Cs + ((size_t)l * kL + t) * cell, a.Hs + ((size_t)l * kL + t) * cell,
+                               keep_act ? a.Act + ((size_t)l * kL + t) * cell * 4 : nullptr, B, H);
+            if ((rc = launch_check("wide_cell_kernel"))) return rc;
+        }
+    }
+    return FCR_OK;
+}
+
+int wide_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const float *u0, const float *states,
+                 const float *noise, float *loss, float *cost, float *command, float *error, float *prediction,
+                 float *xhat, int with_backward, char *base, hipStream_t s) {
+    const WideLayout L = make_wide(d, with_backward);
+    const size_t H = d->H, F = sizeof(float);
+    int rc;
+    // private copies of every parameter the backward needs (fcr_backward takes no weights)
+    auto cp = [&](size_t off, const float *src, size_t n) {
+        return hipMemcpyAsync(base + off, src, n * F, hipMemcpyDeviceToDevice, s);
+    };
+    for (int l = 0; l < kLayers; ++l) {
+        if (cp(L.wih[l], w->w_ih[l], 4 * H * (l == 0 ? kIn : H)) || cp(L.whh[l], w->w_hh[l], 4 * H * H))
+            return fail(FCR_EHIP, "hipMemcpyAsync (weights) failed");
+    }
+    if (cp(L.fcw, w->fc_w, kOut * H) || cp(L.fcb, w->fc_b, kOut) || cp(L.cwi, w->ctrl_w_inp, d->ctrl_hidden * kCtrlIn) ||
+        cp(L.cbi, w->ctrl_b_inp, d->ctrl_hidden) || cp(L.cwo, w->ctrl_w_out, d->ctrl_hidden))
+        return fail(FCR_EHIP, "hipMemcpyAsync (parameters) failed");
+    PackArgs pa{};   // controller records for ctrl_grad_kernel (the fc part is unused on this path)
+    pa.H = kMaxSlots * 4;
+    pa.HS = kMaxSlots;
+    pa.CH = d->ctrl_hidden;
+    pa.fcw = (const float *)(base + L.fcw);   // read only for units < 52 <= H: in bounds
+    pa.fcb = w->fc_b;
+    pa.cwi = w->ctrl_w_inp;
+    pa.cbi = w->ctrl_b_inp;
+    pa.cwo = w->ctrl_w_out;
+    pa.fcp = (float *)(base + L.fcp);
+    pa.fcbo = (float *)(base + L.fcbo);
+    pa.fnp = (float *)(base + L.fnp);
+    hipLaunchKernelGGL(pack_misc_kernel, dim3(2), dim3(256), 0, s, pa);
+    if ((rc = launch_check("pack_misc_kernel"))) return rc;
+
+    rocblas_handle h = blas_on(s);
+    if (!h) return fail(FCR_EHIP, "rocblas_create_handle failed");
+    WideArgs a = wide_args(d, L, base);
+    a.X = X;
+    a.u0 = u0;
+    a.states = states;
+    a.noise = noise;
+    a.pred = prediction;
+    const int nb = (d->B + 255) / 256;
+    for (int j = 0; j < d->N; ++j) {
+        hipLaunchKernelGGL(wide_window_kernel<true>, dim3(nb), dim3(256), 0, s, a, j);
+        if ((rc = launch_check("wide_window_kernel"))) return rc;
+        if ((rc = wide_cells(h, a, L, base, false, s))) return rc;
+        hipLaunchKernelGGL(wide_readout_kernel, dim3(nb), dim3(256), 0, s, a, j,
+                           (const float *)(a.Hs + ((size_t)2 * kL + kL - 1) * d->B * H));
+        if ((rc = launch_check("wide_readout_kernel"))) return rc;
+    }
+    hipLaunchKernelGGL(wide_finish_kernel, dim3(nb), dim3(256), 0, s, a, cost, command, error, xhat);
+    if ((rc = launch_check("wide_finish_kernel"))) return rc;
+    hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(256), 0, s, (const float *)cost, d->B, d->B, loss);
+    return launch_check("loss_reduce_kernel");
+}
+
+int wide_backward(const fcr_dims *d, const float *X, const float *states, const float *prediction,
+                  const float *dloss, float *g_u0, float *g_w_inp, float *g_b_inp, float *g_w_out, char *base,
+                  hipStream_t s) {
+    const WideLayout L = make_wide(d, 1);
+    const int B = d->B, H = d->H;
+    const size_t cell = (size_t)B * H;
+    const int nb = (B + 255) / 256, nc = (int)((cell + 255) / 256);
+    int rc;
+    rocblas_handle h = blas_on(s);
+    if (!h) return fail(FCR_EHIP, "rocblas_create_handle failed");
+    WideArgs a = wide_args(d, L, base);
+    a.X = X;
+    a.states = states;
+    a.pred = (float *)prediction;
+    a.dloss = dloss;
+    float *D[2] = {(float *)(base + L.D[0]), (float *)(base + L.D[1])};
+    if (hipMemsetAsync(a.rowg, 0, sizeof(float) * (size_t)(d->N + kL - 1) * B * kIn, s) != hipSuccess)
+        return fail(FCR_EHIP, "hipMemsetAsync failed");
+    for (int j = d->N - 1; j >= 0; --j) {
+        hipLaunchKernelGGL(wide_head_kernel, dim3(nb), dim3(256), 0, s, a, j);
+        if ((rc = launch_check("wide_head_kernel"))) return rc;
+        hipLaunchKernelGGL(wide_window_kernel<false>, dim3(nb), dim3(256), 0, s, a, j);
+        if ((rc = launch_check("wide_window_kernel"))) return rc;
+        if ((rc = wide_cells(h, a, L, base, true, s))) return rc;   // checkpoint: recompute the window
+        for (int l = kLayers - 1; l >= 0; --l) {
+            const float *wih = (const float *)(base + L.wih[l]), *whh = (const float *)(base + L.whh[l]);
+            if (l < kLayers - 1 && hipMemsetAsync(a.dH, 0, sizeof(float) * cell, s) != hipSuccess)
+                return fail(FCR_EHIP, "hipMemsetAsync failed");
+            if (hipMemsetAsync(a.dC, 0, sizeof(float) * cell, s) != hipSuccess) return fail(FCR_EHIP, "hipMemsetAsync failed");
+            for (int t = kL - 1; t >= 0; --t) {
+                const size_t c_off = ((size_t)l * kL + t) * cell;
+                hipLaunchKernelGGL(wide_cell_bwd_kernel, dim3(nc), dim3(256), 0, s, (const float *)(a.Act + c_off * 4),
+                                   (const float *)(a.Cs + c_off), t > 0 ? (const float *)(a.Cs + c_off - cell) : nullptr,
+                                   (const float *)a.dH, l < kLayers - 1 ? (const float *)(D[l] + (size_t)t * cell) : nullptr,
+                                   a.dC, a.G, B, H);
+                if ((rc = launch_check("wide_cell_bwd_kernel"))) return rc;
+                if (l > 0) {
+                    if ((rc = gemm_gw(h, B, 4 * H, H, wih, a.G, 0.0f, D[l - 1] + (size_t)t * cell))) return rc;
+                } else {   // layer 0: the window rows' gradients, row j + t
+                    if ((rc = gemm_gw(h, B, 4 * H, kIn, wih, a.G, 1.0f, a.rowg + (size_t)(j + t) * B * kIn))) return rc;
+                }
+                if (t > 0 && (rc = gemm_gw(h, B, 4 * H, H, whh, a.G, 0.0f, a.dH))) return rc;
+            }
+        }
+    }
+    hipLaunchKernelGGL(wide_gu0_kernel, dim3(nb), dim3(256), 0, s, a, g_u0);
+    if ((rc = launch_check("wide_gu0_kernel"))) return rc;
+    float *part = (float *)(base + L.fnn_part);
+    hipLaunchKernelGGL(ctrl_grad_kernel, dim3(L.ctrl_blocks), dim3(kCtrlBlock), 0, s, X, (const float *)a.xhat,
+                       (const float *)a.dv, (const float *)(base + L.fnp), d->B, d->N, d->ctrl_hidden, part);
+    if ((rc = launch_check("ctrl_grad_kernel"))) return rc;
+    hipLaunchKernelGGL(grad_reduce_kernel, dim3(d->ctrl_hidden * 5), dim3(256), 0, s, (const float *)part,
+                       L.ctrl_blocks, d->ctrl_hidden, g_w_inp, g_b_inp, g_w_out);
+    return launch_check("grad_reduce_kernel");
+}
+
 }  // namespace
 }  // namespace fcr
 
@@ -173,7 +414,7 @@ int fcr_workspace_size(const fcr_dims *dims, int with_backward, size_t *bytes) {
     int rc = check_dims(dims);
     if (rc) return rc;
     if (!bytes) return fail(FCR_EINVAL, "bytes is NULL");
-    *bytes = make_layout(dims, with_backward).total;
+    *bytes = is_wide(dims) ? make_wide(dims, with_backward).total : make_layout(dims, with_backward).total;
     return FCR_OK;
 }
 
@@ -191,6 +432,12 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
     if (!w->fc_w || !w->fc_b || !w->ctrl_w_inp || !w->ctrl_b_inp || !w->ctrl_w_out)
         return fail(FCR_EINVAL, "fcr_forward: a weight pointer is NULL");
     if (((uintptr_t)ws) & 255) return fail(FCR_EINVAL, "fcr_forward: ws must be 256-byte aligned");
+    if (is_wide(d)) {
+        const size_t need = make_wide(d, with_backward).total;
+        if (ws_bytes < need) return fail(FCR_EWORKSPACE, "fcr_forward: ws has %zu bytes, needs %zu", ws_bytes, need);
+        return wide_forward(d, w, X, u0, states, noise, loss, cost, command, error, prediction, xhat, with_backward,
+                            (char *)ws, (hipStream_t)stream);
+    }
     const Layout L = make_layout(d, with_backward);
     if (ws_bytes < L.total)
         return fail(FCR_EWORKSPACE, "fcr_forward: ws has %zu bytes, needs %zu", ws_bytes, L.total);
@@ -267,6 +514,12 @@ int fcr_backward(const fcr_dims *d, const float *X, const float *states, const f
     if (!X || !states || !prediction || !dloss || !g_u0 || !g_w_inp || !g_b_inp || !g_w_out || !ws)
         return fail(FCR_EINVAL, "fcr_backward: a required pointer is NULL");
     if (((uintptr_t)ws) & 255) return fail(FCR_EINVAL, "fcr_backward: ws must be 256-byte aligned");
+    if (is_wide(d)) {
+        const size_t need = make_wide(d, 1).total;
+        if (ws_bytes < need) return fail(FCR_EWORKSPACE, "fcr_backward: ws has %zu bytes, needs %zu", ws_bytes, need);
+        return wide_backward(d, X, states, prediction, dloss, g_u0, g_w_inp, g_b_inp, g_w_out, (char *)ws,
+                             (hipStream_t)stream);
+    }
     const Layout L = make_layout(d, 1);
     if (ws_bytes < L.total)
         return fail(FCR_EWORKSPACE, "fcr_backward: ws has %zu bytes, needs %zu", ws_bytes, L.total);

@@ -1,0 +1,209 @@
+// fcr_wide.h — device kernels of the rollout for hidden sizes above the LDS-resident tiers (H > 52;
+// H = 256, N = 25). There a layer's weights (4H x (in+H) fp32, 2 MB at H = 256)
+// no longer fit in LDS next to anything else, and one cell of one trajectory is a 1 MFLOP GEMV, so the
+// cell product is done batch-wide as a plain fp32 GEMM on rocBLAS (M = B trajectories) and everything
+// around it — cell update, window build, controller, readout, costs, their backward — is hand-written
+// here, one thread per (trajectory, unit) or per trajectory, batch-major so every access is coalesced.
+//
+// Data (fcr_abi.hip, wide layout), all row-major with the batch index outermost inside a slice:
+//   X0  [10][B][5]        layer-0 input rows of the current window (Functions.py:1395-1396, 1433-1434)
+//   Hs, Cs [3][10][B][H]  h_t, c_t of every cell of the current window
+//   Act [3][10][B][4H]    gate activations (i, f, g, o) of the window, kept by the backward's recompute
+//   G   [B][4H]           gate pre-activations (forward) / d loss / d pre-activations (backward)
+//   rowg [N+9][B][5]      d loss / d (extended window row r): every window's layer-0 input gradient
+//                         lands in rows j..j+9 — the row-gradient bookkeeping of fcr_bwd.h, batch-wide
+// The backward keeps nothing from the forward but xhat and the predictions: it recomputes each
+// window's cells (a checkpoint per window) before running that window's reverse pass.
+#pragma once
+#include "fcr_common.h"
+
+namespace fcr {
+
+struct WideArgs {
+    int B, N, H, CH;
+    float alpha;
+    const float *X, *u0, *states, *noise;
+    const float *fcw, *fcb, *cwi, *cbi, *cwo;
+    float *xhat, *pred, *tot, *cmd, *err;
+    float *X0, *Hs, *Cs, *Act, *G, *dH, *dC, *rowg, *dv;
+    const float *dloss;
+};
+
+
+// controller (FNNModel.forward, Functions.py:261-289) pre-Hardtanh output, and its ReLU inputs' signs
+__device__ __forceinline__ float wide_fnn(const WideArgs &a, float x0, float x3, float ref) {
+    float v = 0.0f;
+    for (int k = 0; k < a.CH; ++k) {
+        const float z = a.cwi[k * kCtrlIn + 0] * x0 + a.cwi[k * kCtrlIn + 1] * x3 + a.cwi[k * kCtrlIn + 2] * ref + a.cbi[k];
+        v += a.cwo[k] * relu(z);
+    }
+    return v;
+}
+
+// extended window row r of trajectory b: rows 0..9 = states (row 9 col 4 = u0), row 10+m = (xhat_m, u_{m+1})
+__device__ __forceinline__ float ext_row(const WideArgs &a, int b, int r, int col) {
+    if (r < kL) {
+        if (r == kL - 1 && col == kIn - 1) return a.pred[(size_t)b * a.N];   // u_0 (prediction[:, 0])
+        return a.states[((size_t)b * kL + r) * kIn + col];
+    }
+    const int m = r - kL;
+    return col < kOut ? a.xhat[((size_t)b * a.N + m) * kOut + col] : a.pred[(size_t)b * a.N + m + 1];
+}
+
+// Window j of the forward: the controller call that produces u_j (j > 0, Functions.py:1421-1430), the
+// command cost (:1405, :1446), and the window's layer-0 input rows. CTRL = false: rows only (recompute).
+template <bool CTRL>
+__global__ void wide_window_kernel(WideArgs a, int j) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= a.B) return;
+    if (CTRL) {
+        const float ref = a.X[(size_t)b * kCtrlIn + 2];
+        float u, cmd;
+        if (j == 0) {
+            u = a.u0[b];
+            cmd = a.alpha * sq(a.states[((size_t)b * kL + kL - 2) * kIn + kIn - 1] - u);
+            a.tot[b] = cmd;
+            a.cmd[b] = cmd;
+            a.err[b] = 0.0f;
+        } else {
+            const float *xh = a.xhat + ((size_t)b * a.N + j - 1) * kOut;
+            u = hardtanh(wide_fnn(a, xh[0], xh[3], ref));
+            cmd = a.alpha * sq(a.pred[(size_t)b * a.N + j - 1] - u);
+            a.tot[b] += cmd;
+            a.cmd[b] += cmd;
+        }
+        a.pred[(size_t)b * a.N + j] = u;
+    }
+    for (int t = 0; t < kL; ++t)
+        for (int col = 0; col < kIn; ++col) a.X0[((size_t)t * a.B + b) * kIn + col] = ext_row(a, b, j + t, col);
+}
+
+// Cell update from the gate pre-activations G [B][4H] (torch gate order i|f|g|o): c, h; and, for the
+// backward's recompute, the activations.
+__global__ void wide_cell_kernel(const float *__restrict__ G, const float *__restrict__ c_prev, float *c_out,
+                                 float *h_out, float *act, int B, int H) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)B * H) return;
+    const size_t b = idx / H, u = idx % H;
+    const float *g4 = G + b * 4 * H + u;
+    const float i = sigm(g4[0]), f = sigm(g4[H]), g = tanh_f(g4[2 * H]), o = sigm(g4[3 * H]);
+    const float c = (c_prev ? f * c_prev[idx] : 0.0f) + i * g;
+    c_out[idx] = c;
+    h_out[idx] = o * tanh_f(c);
+    if (act) {
+        float *a4 = act + b * 4 * H + u;
+        a4[0] = i;
+        a4[H] = f;
+        a4[2 * H] = g;
+        a4[3 * H] = o;
+    }
+}
+
+// Readout fc(h_9 of layer 2) (Functions.py:377), noise (:1400-1402), and the step's error and
+// constraint costs (:1405-1414, :1443-1452).
+__global__ void wide_readout_kernel(WideArgs a, int j, const float *__restrict__ h) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= a.B) return;
+    float xo[kOut];
+    for (int o = 0; o < kOut; ++o) {
+        float s = 0.0f;
+        for (int u = 0; u < a.H; ++u) s += a.fcw[o * a.H + u] * h[(size_t)b * a.H + u];
+        xo[o] = s + a.fcb[o] + (a.noise ? a.noise[((size_t)b * a.N + j) * kOut + o] : 0.0f);
+        a.xhat[((size_t)b * a.N + j) * kOut + o] = xo[o];
+    }
+    const float ref = a.X[(size_t)b * kCtrlIn + 2];
+    const float err = sq(xo[0] - ref);
+    const float con = relu(-xo[1]) + relu(-xo[2]) + relu(xo[1] - kP1Max) + relu(xo[2] - kP2Max);
+    a.tot[b] += err + con;
+    a.err[b] += err;
+}
+
+// per-trajectory outputs (Functions.py:1458-1460)
+__global__ void wide_finish_kernel(WideArgs a, float *cost, float *command, float *error, float *xhat_user) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= a.B) return;
+    cost[b] = a.tot[b] / (float)a.N;
+    command[b] = a.cmd[b] / (float)a.N;
+    error[b] = a.err[b] / (float)a.N;
+    if (xhat_user)
+        for (int k = 0; k < a.N * kOut; ++k) xhat_user[(size_t)b * a.N * kOut + k] = a.xhat[(size_t)b * a.N * kOut + k];
+}
+
+// Backward head of window j: d loss / d xhat_j from the step costs and from every later window that
+// read row 10+j (rowg), the controller's backward at (xhat_j[0], xhat_j[3], ref) (stores dv for the
+// parameter gradients), and dh_9 of layer 2 = fc.Wᵀ dxhat_j into dH. Same algebra as fcr_bwd.h.
+__global__ void wide_head_kernel(WideArgs a, int j) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= a.B) return;
+    const int N = a.N;
+    const float wgt = a.dloss[0] / ((float)a.B * (float)N);
+    const float ref = a.X[(size_t)b * kCtrlIn + 2];
+    const float *xh = a.xhat + ((size_t)b * N + j) * kOut;
+    float d0 = wgt * 2.0f * (xh[0] - ref);
+    float d1 = wgt * ((-xh[1] > 0.0f ? -1.0f : 0.0f) + (xh[1] - kP1Max > 0.0f ? 1.0f : 0.0f));
+    float d2 = wgt * ((-xh[2] > 0.0f ? -1.0f : 0.0f) + (xh[2] - kP2Max > 0.0f ? 1.0f : 0.0f));
+    float d3 = 0.0f;
+    if (j <= N - 2) {
+        const float *G = a.rowg + ((size_t)(kL + j) * a.B + b) * kIn;
+        d0 += G[0];
+        d1 += G[1];
+        d2 += G[2];
+        d3 += G[3];
+        const float *pr = a.pred + (size_t)b * N;
+        float du = 2.0f * a.alpha * wgt * (pr[j + 1] - pr[j]);
+        if (j + 2 < N) du += 2.0f * a.alpha * wgt * (pr[j + 1] - pr[j + 2]);
+        du += G[4];
+        const float v = wide_fnn(a, xh[0], xh[3], ref);
+        const float dv = (v > -1.0f && v < 1.0f) ? du : 0.0f;
+        float dca = 0.0f, dcb = 0.0f;
+        for (int k = 0; k < a.CH; ++k) {
+            const float z = a.cwi[k * kCtrlIn + 0] * xh[0] + a.cwi[k * kCtrlIn + 1] * xh[3] + a.cwi[k * kCtrlIn + 2] * ref + a.cbi[k];
+            const float dz = z > 0.0f ? dv * a.cwo[k] : 0.0f;
+            dca += dz * a.cwi[k * kCtrlIn + 0];
+            dcb += dz * a.cwi[k * kCtrlIn + 1];
+        }
+        a.dv[(size_t)b * N + j] = dv;
+        d0 += dca;
+        d3 += dcb;
+    } else {
+        a.dv[(size_t)b * N + j] = 0.0f;
+    }
+    for (int u = 0; u < a.H; ++u)
+        a.dH[(size_t)b * a.H + u] = a.fcw[u] * d0 + a.fcw[a.H + u] * d1 + a.fcw[2 * a.H + u] * d2 + a.fcw[3 * a.H + u] * d3;
+}
+
+// Backward of one cell: from the activations, c_t, c_{t-1}, the incoming dh (carried dH + din from the
+// layer above) and the carried dc: d loss / d (gate pre-activations) into dG, and dc_{t-1} into dC.
+__global__ void wide_cell_bwd_kernel(const float *__restrict__ act, const float *__restrict__ c,
+                                     const float *__restrict__ c_prev, const float *__restrict__ dH,
+                                     const float *__restrict__ din, float *dC, float *dG, int B, int H) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)B * H) return;
+    const size_t b = idx / H, u = idx % H;
+    const float *a4 = act + b * 4 * H + u;
+    const float i = a4[0], f = a4[H], g = a4[2 * H], o = a4[3 * H];
+    const float tc = tanh_f(c[idx]);
+    const float cp = c_prev ? c_prev[idx] : 0.0f;
+    const float dh = dH[idx] + (din ? din[idx] : 0.0f);
+    const float dct = dC[idx] + dh * o * (1.0f - tc * tc);
+    float *d4 = dG + b * 4 * H + u;
+    d4[0] = dct * g * i * (1.0f - i);
+    d4[H] = dct * cp * f * (1.0f - f);
+    d4[2 * H] = dct * i * (1.0f - g * g);
+    d4[3 * H] = dh * tc * o * (1.0f - o);
+    dC[idx] = dct * f;
+}
+
+// d loss / d u0 (Functions.py:1396 row 9 col 4, and the command costs cmd_0, cmd_1)
+__global__ void wide_gu0_kernel(WideArgs a, float *g_u0) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= a.B) return;
+    const float wgt = a.dloss[0] / ((float)a.B * (float)a.N);
+    const float *pr = a.pred + (size_t)b * a.N;
+    const float s84 = a.states[((size_t)b * kL + kL - 2) * kIn + kIn - 1];
+    float du0 = 2.0f * a.alpha * wgt * (pr[0] - s84);
+    if (a.N > 1) du0 += 2.0f * a.alpha * wgt * (pr[0] - pr[1]);
+    g_u0[b] = a.rowg[((size_t)(kL - 1) * a.B + b) * kIn + kIn - 1] + du0;
+}
+
+}  // namespace fcr

@@ -22,7 +22,17 @@ def case_names():
 
 def load_case(name):
     c = dict(np.load(os.path.join(GOLDEN, f"case_{name}.npz")))
-    w = dict(np.load(os.path.join(GOLDEN, f"weights_{str(c['weights'])}.npz")))
+    wname = str(c["weights"])
+    if wname.startswith("synth_"):   # large synthetic weights are stored by seed (make_golden.py)
+        from tests.golden.make_golden import synth_params
+        _, H, seed = wname.split("_")
+        p = synth_params(int(H), int(seed))
+        w = {"W_inp": p["W_inp"], "b_inp": p["b_inp"], "W_out": p["W_out"], "fcW": p["fcW"], "fcb": p["fcb"]}
+        for k in range(3):
+            w[f"Wih{k}"] = p["Wih"][k]
+            w[f"Whh{k}"] = p["Whh"][k]
+    else:
+        w = dict(np.load(os.path.join(GOLDEN, f"weights_{wname}.npz")))
     params = {
         "Wih": [w[f"Wih{k}"].astype(np.float64) for k in range(3)],
         "Whh": [w[f"Whh{k}"].astype(np.float64) for k in range(3)],

@@ -140,8 +140,29 @@ def pack_params(params):
     return {k: np.asarray(v, np.float32) for k, v in d.items()}
 
 
+# Cases whose weights are synthetic and large are stored by seed, not by value: "synth_<H>_<seed>"
+# names synth_params(H, seed) (conftest.load_case regenerates them; float32-exact by construction).
+SYNTH_CASES = {
+    "h64_b24_n3": (64, 11, 24, 3, 11, False),
+    "h256_b8_n25": (256, 9, 8, 25, 9, False),       # SURVEY §8(c)/(d) config 5 shape at B = 8
+}
+
+
+def make_synth_cases(only=None):
+    for name, (H, pseed, B, N, seed, wide) in SYNTH_CASES.items():
+        if only and name not in only:
+            continue
+        c = make_case(name, synth_params(H, pseed), B, N, seed, wide=wide)
+        c["weights"] = f"synth_{H}_{pseed}"
+        np.savez_compressed(os.path.join(OUT, f"case_{name}.npz"), **{k: np.asarray(v) for k, v in c.items()})
+
+
 def main():
     torch.set_num_threads(8)
+    if len(sys.argv) > 2 and sys.argv[1] == "--only":
+        make_synth_cases(set(sys.argv[2:]))
+        return
+    make_synth_cases()
     ref = load_ref_params(False)
     refn = load_ref_params(True)
     h16 = synth_params(16, 7)
