@@ -4,7 +4,9 @@ Drop-in for the hot path of marcowus/forging-control: ``MPCLoss`` (the batched c
 the FNN controller through the 3-layer LSTM plant surrogate, Functions.py:1336-1472) and its
 backward, as hand-written HIP kernels behind the C ABI in include/fcr.h.
 """
-from . import _native, distributed, rollout
+from . import _native, distributed, inference, rollout
 from .functions import FNNModel, LSTMModel, MPCLoss, NeuralNetwork
+from .inference import controller_step, simulate_step, simulator_make_step
 
-__all__ = ["FNNModel", "LSTMModel", "MPCLoss", "NeuralNetwork", "rollout", "distributed", "_native"]
+__all__ = ["FNNModel", "LSTMModel", "MPCLoss", "NeuralNetwork", "rollout", "distributed", "inference",
+           "simulate_step", "controller_step", "simulator_make_step", "_native"]

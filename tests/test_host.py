@@ -93,3 +93,13 @@ def test_grad_allreduce_equals_global_mean_gloo_world2():
     for r in (0, 1):
         assert np.allclose(res[r][0], ref, atol=1e-6)
         assert abs(res[r][1] - loss.item()) < 1e-6
+
+
+def test_inference_refuses_cpu_tensors():
+    """No CPU fallback: the product path needs the ROCm device (the oracle is test infrastructure)."""
+    import pytest
+    import torch
+    import forging_control_amd as fca
+    sim = fca.LSTMModel(5, 50, 4, 3)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        fca.simulate_step(sim, torch.zeros(2, 10, 5))
