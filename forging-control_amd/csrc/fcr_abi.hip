@@ -99,7 +99,7 @@ Layout make_layout(const fcr_dims *d, int with_backward) {
         L.dxrow = take(sizeof(f32x2) * (size_t)L.nw_pad * d->N * kL * kWave);
     }
 #if FCR_STAMP
-    L.stamp = take(sizeof(unsigned long long) * L.nw_pad * 8);
+    L.stamp = take(sizeof(unsigned long long) * L.nw_pad * 16);   // [backward 8 | forward 8] per wave
 #endif
     L.total = off;
     return L;
@@ -494,6 +494,9 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
     fa.cseq = with_backward ? (f32x4 *)(base + L.cseq) : nullptr;
     fa.xw = with_backward ? (f32x2 *)(base + L.xw) : nullptr;
     fa.p = packed_ptrs(L, base);
+#if FCR_STAMP
+    fa.stamp = (unsigned long long *)(base + L.stamp) + (size_t)L.nw_pad * 8;
+#endif
     switch (L.HS) {
         case 4: rc = launch_fwd<4>(fa, L, s); break;
         case 8: rc = launch_fwd<8>(fa, L, s); break;

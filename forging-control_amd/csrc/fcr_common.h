@@ -59,6 +59,7 @@ struct FwdArgs {
     f32x4 *hseq;     // layers 0, 1 always (the next phase's input); layer 2 with `keep`
     f32x4 *cseq;     // with `keep` (null otherwise)
     f32x2 *xw;       // with `keep`
+    unsigned long long *stamp;   // FCR_STAMP diagnostic builds only
     Packed p;
 };
 

@@ -27,10 +27,19 @@ __device__ __forceinline__ void rot_left(float (&w)[kL]) {
 // pairs, each with two accumulators over alternate k-blocks: four independent MFMA chains per
 // scheduling region (one region per k-block, the next block's four fragment reads in flight), and the
 // cell update of the previous pair issued in the first region of the next, beside its MFMAs.
+#ifndef FCR_FWD_PRIO
+#define FCR_FWD_PRIO 1
+#endif
 template <int HS, bool L0, bool FIRST>
 __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lane, float x0, float x1,
                                            const float (&x)[HS], const float (&hp)[HS], float (&c)[HS],
-                                           float (&hout)[HS]) {
+                                           float (&hout)[HS], unsigned &turn) {
+#if FCR_FWD_PRIO
+    // the two waves of a SIMD take turns at the higher issue priority, cell by cell (fcr_bwd.h)
+    if (turn & 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+    turn ^= 1;
+#endif
     using G = Geo16<HS>;
     constexpr int KB = L0 ? G::KB0 : G::KB1;
     constexpr int KLO = (L0 && FIRST) ? G::XBLK : 0;
@@ -88,6 +97,17 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
     if (2 * NP - 1 < HS) lstm_point<FIRST>(prev[1], c[2 * NP - 1], c[2 * NP - 1], hout[2 * NP - 1]);
 }
 
+#ifndef FCR_STAMP
+#define FCR_STAMP 0
+#endif
+__device__ __forceinline__ unsigned long long fstamp() {
+#if FCR_STAMP
+    return __builtin_amdgcn_s_memtime();
+#else
+    return 0;
+#endif
+}
+
 template <int HS, bool STORE>
 __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kernel(FwdArgs a) {
     using G = Geo16<HS>;
@@ -134,7 +154,11 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
     f32x4 *cs_wave = a.cseq + wseq;
     f32x2 *xw_wave = a.xw + (size_t)wave * N * kL * kWave;
 
+    unsigned long long st_fill = 0, st_l0 = 0, st_l12 = 0, st_head = 0;
+    unsigned turn = (threadIdx.x >> 8) & 1;   // waves w and w+4 share a SIMD: start out of phase
+    const unsigned long long st_k0 = fstamp();
     for (int j = 0; j < N; ++j) {
+        const unsigned long long st_w0 = fstamp();
         const float *lfnp_j = opaque(lfnp), *lfcp_j = opaque(lfcp), *lfcb_j = opaque(lfcb);
         float pred = u0;
         if (j > 0) {                                                   // Functions.py:1421-1434
@@ -157,6 +181,8 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
         f32x4 *csj = cs_wave + (size_t)j * kLayers * kL * qcell;
 #define SEQ_H(l, t) (hsj + (size_t)((l) * kL + (t)) * qcell)
 #define SEQ_C(l, t) (csj + (size_t)((l) * kL + (t)) * qcell)
+        const unsigned long long st_w1 = fstamp();
+        st_head += st_w1 - st_w0;
         // ---- layer 0 over the window (Functions.py:374) ----
         __syncthreads();   // resident blocks are in place (first window) — no refill for layer 0
         stagger();
@@ -164,7 +190,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             const float x0 = w0[0], x1 = w1[0];
             rot_left(w0);
             rot_left(w1);
-            fwd16_cell<HS, true, true>(lw0, lane, x0, x1, hp, hp, c, hout);
+            fwd16_cell<HS, true, true>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
             store_quads<HS>(SEQ_H(0, 0), hout, lane);
             if (STORE) {
                 xw_wave[(size_t)j * kL * kWave + lane] = f32x2{x0, x1};
@@ -177,7 +203,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             const float x0 = w0[0], x1 = w1[0];
             rot_left(w0);
             rot_left(w1);
-            fwd16_cell<HS, true, false>(lw0, lane, x0, x1, hp, hp, c, hout);
+            fwd16_cell<HS, true, false>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
             store_quads<HS>(SEQ_H(0, t), hout, lane);
             if (STORE) {
                 xw_wave[((size_t)j * kL + t) * kWave + lane] = f32x2{x0, x1};
@@ -190,11 +216,15 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
 #pragma unroll
         for (int l = 1; l < kLayers; ++l) {
             const bool keep_h = l == 1 || STORE;   // layer 2's h_t is only the backward's h_{t-1}
+            const unsigned long long st_f0 = fstamp();
+            if (l == 1) st_l0 += st_f0 - st_w1;
             lds_fill<G::FA1 * 4, kFwdWaves>(lw, a.p.fa[l]);
+            const unsigned long long st_f1 = fstamp();
+            st_fill += st_f1 - st_f0;
             stagger();
             load_quads<HS>(xc, SEQ_H(l - 1, 0), lane);
             load_quads<HS>(xn, SEQ_H(l - 1, 1), lane);
-            fwd16_cell<HS, false, true>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout);
+            fwd16_cell<HS, false, true>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
             if (keep_h) store_quads<HS>(SEQ_H(l, 0), hout, lane);
             if (STORE) store_quads<HS>(SEQ_C(l, 0), c, lane);
 #pragma unroll
@@ -204,7 +234,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             }
             for (int t = 1; t < kL; ++t) {
                 load_quads<HS>(xn, SEQ_H(l - 1, t + 1 < kL ? t + 1 : t), lane);
-                fwd16_cell<HS, false, false>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout);
+                fwd16_cell<HS, false, false>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
                 if (keep_h && !(l == 2 && t + 1 == kL)) store_quads<HS>(SEQ_H(l, t), hout, lane);
                 if (STORE && t + 1 < kL) store_quads<HS>(SEQ_C(l, t), c, lane);
 #pragma unroll
@@ -256,6 +286,16 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) part += __shfl_xor(part, m);
     if (lane == 0) a.loss_part[wave] = part;
+#if FCR_STAMP
+    if (lane == 0) {
+        unsigned long long *o = a.stamp + (size_t)wave * 8;
+        o[0] = st_head;
+        o[1] = st_l0;
+        o[2] = st_fill;
+        o[3] = st_l12;
+        o[4] = fstamp() - st_k0;
+    }
+#endif
 }
 
 }  // namespace fcr

@@ -37,3 +37,11 @@ for k, nm in ((5, "window head (row grads, controller bwd)"), (6, "layer-2 image
     print(f"  {nm:40s} {np.mean(st[:, k]) / 10:9.0f} cycles/window")
 print(f"  cell total {np.mean((st[:, 0] + st[:, 1] + st[:, 2]) / cells):9.0f} cycles/cell;"
       f" kernel wave lifetime {np.mean(st[:, 4]):.3e} cycles, {np.mean(st[:, 4] / cells):.0f} per cell")
+
+nw_pad = (nw + 7) // 8 * 8
+fw = ws[off + nw_pad * 64: off + nw_pad * 64 + nw * 64].view(torch.int64).reshape(nw, 8).cpu().numpy().astype(np.float64)
+N = state["dims"].N
+tot = fw[:, 4].mean()
+print(f"forward: wave lifetime {tot:.3e} cycles; per window: head {fw[:, 0].mean() / N:.0f}, layer 0 "
+      f"{fw[:, 1].mean() / N:.0f}, fills+barriers {fw[:, 2].mean() / N:.0f}, layers 1-2 + readout "
+      f"{(tot - fw[:, 0].mean() - fw[:, 1].mean() - fw[:, 2].mean()) / N:.0f}")
