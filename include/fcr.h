@@ -47,7 +47,7 @@ typedef struct fcr_dims {
     int32_t B;           /* trajectories in the batch                         */
     int32_t N;           /* prediction horizon (MPCLoss.N)                    */
     int32_t L;           /* lookback rows of the LSTM window (must be 10)     */
-    int32_t H;           /* LSTM hidden size (built: 1..52)                   */
+    int32_t H;           /* LSTM hidden size: 1..52 fused kernels, 53..2048 per-cell GEMM path */
     int32_t layers;      /* LSTM layers (must be 3)                           */
     int32_t in_dim;      /* LSTM input features (must be 5)                   */
     int32_t out_dim;     /* LSTM outputs (must be 4)                          */
