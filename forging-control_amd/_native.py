@@ -18,7 +18,8 @@ ABI_VERSION = 1
 ERRORS = {-1: "FCR_EINVAL", -2: "FCR_EWORKSPACE", -3: "FCR_EHIP", -4: "FCR_EUNSUPPORTED"}
 
 # Every symbol include/fcr.h declares (tests check the .so exports exactly these).
-EXPORTS = ("fcr_workspace_size", "fcr_forward", "fcr_backward", "fcr_last_error", "fcr_abi_version")
+EXPORTS = ("fcr_workspace_size", "fcr_forward", "fcr_backward", "fcr_plant_rk4", "fcr_last_error",
+           "fcr_abi_version")
 
 
 class FcrDims(ctypes.Structure):
@@ -64,6 +65,8 @@ def load() -> ctypes.CDLL:
         lib.fcr_forward.restype = i32
         lib.fcr_backward.argtypes = [ctypes.POINTER(FcrDims), vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp]
         lib.fcr_backward.restype = i32
+        lib.fcr_plant_rk4.argtypes = [i32, i32, ctypes.c_double, i32, i32, vp, vp, vp, vp]
+        lib.fcr_plant_rk4.restype = i32
         lib.fcr_last_error.argtypes = []
         lib.fcr_last_error.restype = ctypes.c_char_p
         lib.fcr_abi_version.argtypes = []

@@ -15,6 +15,7 @@
 #include "fcr_fwd.h"
 #include "fcr_img.h"
 #include "fcr_pack.h"
+#include "fcr_plant.h"
 #include "fcr_wide.h"
 
 namespace fcr {
@@ -563,6 +564,27 @@ int fcr_backward(const fcr_dims *d, const float *X, const float *states, const f
     hipLaunchKernelGGL(grad_reduce_kernel, dim3(d->ctrl_hidden * 5), dim3(256), 0, s, (const float *)part,
                        L.ctrl_blocks, d->ctrl_hidden, g_w_inp, g_b_inp, g_w_out);
     return launch_check("grad_reduce_kernel");
+}
+
+int fcr_plant_rk4(int32_t B, int32_t S, double ts, int32_t substeps, int32_t smooth, const double *x0,
+                  const double *u, double *x, void *stream) {
+    if (B < 0 || S < 0) return fail(FCR_EINVAL, "fcr_plant_rk4: B=%d, S=%d must be >= 0", B, S);
+    if (substeps < 1 || substeps > 4096) return fail(FCR_EINVAL, "fcr_plant_rk4: substeps=%d must be 1..4096", substeps);
+    if (!(ts > 0.0) || ts > 1e6) return fail(FCR_EINVAL, "fcr_plant_rk4: ts=%g must be a positive time step", ts);
+    if (smooth != 0 && smooth != 1) return fail(FCR_EINVAL, "fcr_plant_rk4: smooth=%d must be 0 or 1", smooth);
+    if ((long long)B * (S + 1) * 5 > (1LL << 40)) return fail(FCR_EINVAL, "fcr_plant_rk4: B*(S+1) too large");
+    if (B == 0) return FCR_OK;
+    if (!x0 || !x || (S > 0 && !u)) return fail(FCR_EINVAL, "fcr_plant_rk4: a required pointer is NULL");
+    if ((((uintptr_t)x0) | ((uintptr_t)u) | ((uintptr_t)x)) & 7)
+        return fail(FCR_EINVAL, "fcr_plant_rk4: buffers must be 8-byte aligned (fp64)");
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 grid((B + plant::kPlantBlock - 1) / plant::kPlantBlock);
+    const double dt = ts / substeps;
+    if (smooth)
+        hipLaunchKernelGGL(plant::plant_rk4_kernel<true>, grid, dim3(plant::kPlantBlock), 0, s, B, S, dt, substeps, x0, u, x);
+    else
+        hipLaunchKernelGGL(plant::plant_rk4_kernel<false>, grid, dim3(plant::kPlantBlock), 0, s, B, S, dt, substeps, x0, u, x);
+    return launch_check("plant_rk4_kernel");
 }
 
 }  // extern "C"

@@ -103,6 +103,21 @@ int fcr_backward(const fcr_dims *dims,
                  float *g_u0, float *g_w_inp, float *g_b_inp, float *g_w_out,
                  void *ws, size_t ws_bytes, void *stream);
 
+/*
+ * Batched forging-press plant: the state update x_{t+1} = F(x_t, u_t) of
+ * FeasibilityRecovery.Ruge_Kuta (Functions.py:1743-1781) over the dynamics of forging_model
+ * (Functions.py:1615-1740; smooth = 1: template_model.py:19-149, pressures floored by smooth_relu),
+ * for B independent trajectories of S steps, in fp64.
+ *   x0 (B,5)       initial states [y, y_dot, p1, p2, z]
+ *   u  (B,S)       command held over each step
+ *   x  (B,S+1,5)   x[:,0] = x0, x[:,t+1] = F(x[:,t], u[:,t])
+ *   ts             step (the reference: TS = controller t_step = 0.001, template_mpc.py:23)
+ *   substeps       RK4 stages per step (the reference: M = 4, Functions.py:1760)
+ * B = 0 is a no-op. Buffers are fp64 device memory, 8-byte aligned.
+ */
+int fcr_plant_rk4(int32_t B, int32_t S, double ts, int32_t substeps, int32_t smooth,
+                  const double *x0, const double *u, double *x, void *stream);
+
 /* Thread-local description of the last error (never NULL). */
 const char *fcr_last_error(void);
 
