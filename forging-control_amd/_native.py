@@ -18,8 +18,8 @@ ABI_VERSION = 1
 ERRORS = {-1: "FCR_EINVAL", -2: "FCR_EWORKSPACE", -3: "FCR_EHIP", -4: "FCR_EUNSUPPORTED"}
 
 # Every symbol include/fcr.h declares (tests check the .so exports exactly these).
-EXPORTS = ("fcr_workspace_size", "fcr_forward", "fcr_backward", "fcr_plant_rk4", "fcr_last_error",
-           "fcr_abi_version")
+EXPORTS = ("fcr_workspace_size", "fcr_forward", "fcr_backward", "fcr_plant_rk4", "fcr_window_gather",
+           "fcr_last_error", "fcr_abi_version")
 
 
 class FcrDims(ctypes.Structure):
@@ -35,6 +35,14 @@ class FcrWeights(ctypes.Structure):
         ("ctrl_w_inp", ctypes.c_void_p), ("ctrl_b_inp", ctypes.c_void_p), ("ctrl_w_out", ctypes.c_void_p),
         ("w_ih", ctypes.c_void_p * 3), ("w_hh", ctypes.c_void_p * 3),
         ("fc_w", ctypes.c_void_p), ("fc_b", ctypes.c_void_p),
+    ]
+
+
+class FcrWindows(ctypes.Structure):
+    _fields_ = [
+        ("rows", ctypes.c_int64), ("traj_len", ctypes.c_int32), ("lookback", ctypes.c_int32),
+        ("nx", ctypes.c_int32), ("ny", ctypes.c_int32), ("nz", ctypes.c_int32),
+        ("X", ctypes.c_void_p), ("Y", ctypes.c_void_p), ("Z", ctypes.c_void_p),
     ]
 
 
@@ -67,6 +75,8 @@ def load() -> ctypes.CDLL:
         lib.fcr_backward.restype = i32
         lib.fcr_plant_rk4.argtypes = [i32, i32, ctypes.c_double, i32, i32, vp, vp, vp, vp]
         lib.fcr_plant_rk4.restype = i32
+        lib.fcr_window_gather.argtypes = [ctypes.POINTER(FcrWindows), i32, vp, vp, vp, vp, vp, vp]
+        lib.fcr_window_gather.restype = i32
         lib.fcr_last_error.argtypes = []
         lib.fcr_last_error.restype = ctypes.c_char_p
         lib.fcr_abi_version.argtypes = []

@@ -16,6 +16,7 @@
 #include "fcr_img.h"
 #include "fcr_pack.h"
 #include "fcr_plant.h"
+#include "fcr_window.h"
 #include "fcr_wide.h"
 
 namespace fcr {
@@ -585,6 +586,32 @@ int fcr_plant_rk4(int32_t B, int32_t S, double ts, int32_t substeps, int32_t smo
     else
         hipLaunchKernelGGL(plant::plant_rk4_kernel<false>, grid, dim3(plant::kPlantBlock), 0, s, B, S, dt, substeps, x0, u, x);
     return launch_check("plant_rk4_kernel");
+}
+
+int fcr_window_gather(const fcr_windows *t, int32_t B, const int64_t *idx, float *x, float *y, float *z,
+                      int32_t *bad, void *stream) {
+    if (!t) return fail(FCR_EINVAL, "fcr_window_gather: tables is NULL");
+    if (t->rows < 1 || t->traj_len < 1 || t->rows % t->traj_len)
+        return fail(FCR_EINVAL, "fcr_window_gather: rows=%lld must be a positive multiple of traj_len=%d",
+                    (long long)t->rows, t->traj_len);
+    if (t->lookback < 1 || t->lookback > 4096) return fail(FCR_EINVAL, "fcr_window_gather: lookback=%d must be 1..4096", t->lookback);
+    if (t->nx < 0 || t->ny < 0 || t->nz < 0 || t->nx > 4096 || t->ny > 4096 || t->nz > 4096)
+        return fail(FCR_EINVAL, "fcr_window_gather: feature counts %d/%d/%d must be 0..4096", t->nx, t->ny, t->nz);
+    if (B < 0) return fail(FCR_EINVAL, "fcr_window_gather: B=%d must be >= 0", B);
+    if ((t->nx && !t->X) || (t->ny && !t->Y) || (t->nz && !t->Z) || !bad ||
+        (B && (!idx || (t->nx && !x) || (t->ny && !y) || (t->nz && !z))))
+        return fail(FCR_EINVAL, "fcr_window_gather: a required pointer is NULL");
+    hipStream_t s = (hipStream_t)stream;
+    if (hipMemsetAsync(bad, 0, sizeof(int32_t), s) != hipSuccess) return fail(FCR_EHIP, "hipMemsetAsync failed");
+    const long long per = t->nx + t->ny + (long long)t->lookback * t->nz;
+    if (B == 0 || per == 0) return FCR_OK;
+    window::WinArgs a{t->X, t->Y, t->Z, (long long)t->rows, t->traj_len, t->lookback, t->nx, t->ny, t->nz,
+                      B, (const long long *)idx, x, y, z, bad};
+    const long long n = (long long)B * per;
+    if (n > (1LL << 40)) return fail(FCR_EINVAL, "fcr_window_gather: batch too large");
+    hipLaunchKernelGGL(window::window_gather_kernel, dim3((unsigned)((n + window::kWinBlock - 1) / window::kWinBlock)),
+                       dim3(window::kWinBlock), 0, s, a);
+    return launch_check("window_gather_kernel");
 }
 
 }  // extern "C"

@@ -118,6 +118,32 @@ int fcr_backward(const fcr_dims *dims,
 int fcr_plant_rk4(int32_t B, int32_t S, double ts, int32_t substeps, int32_t smooth,
                   const double *x0, const double *u, double *x, void *stream);
 
+/*
+ * Training-sample windows: the tables of the concatenated per-trajectory
+ * SequenceDatasets (Functions.py:92-132, built by Data.get_individual_dataset :479-516 and
+ * ConcatDataset, UL/Main.py:270-279), resident in device memory.
+ *   X (rows, nx) features [y_dot, z, ref]; Y (rows, ny) target; Z (rows, nz) recurrent features;
+ *   rows = trajectories · traj_len (T_TRAJ rows each); lookback = window rows (10, UL/Main.py:267).
+ */
+typedef struct fcr_windows {
+    int64_t rows;
+    int32_t traj_len;
+    int32_t lookback;
+    int32_t nx, ny, nz;
+    const float *X, *Y, *Z;
+} fcr_windows;
+
+/*
+ * Batch gather = SequenceDataset.__getitem__ (Functions.py:109-132) for every global index idx[b]
+ * (trajectory k = idx / traj_len, row i = idx % traj_len):
+ *   x[b] = X[i],  y[b] = Y[min(i+1, traj_len-1)],  z[b, j] = Z[max(i-lookback+1+j, 0)]   (rows of trajectory k)
+ * into x (B,nx), y (B,ny), z (B,lookback,nz). `bad` (device int32) receives the number of indices outside
+ * [0, rows) (their outputs are zero-filled) — the reference raises IndexError for them; the Python layer
+ * checks it. Stream-ordered; B = 0 only clears `bad`.
+ */
+int fcr_window_gather(const fcr_windows *tables, int32_t B, const int64_t *idx,
+                      float *x, float *y, float *z, int32_t *bad, void *stream);
+
 /* Thread-local description of the last error (never NULL). */
 const char *fcr_last_error(void);
 
