@@ -18,8 +18,8 @@ ABI_VERSION = 1
 ERRORS = {-1: "FCR_EINVAL", -2: "FCR_EWORKSPACE", -3: "FCR_EHIP", -4: "FCR_EUNSUPPORTED"}
 
 # Every symbol include/fcr.h declares (tests check the .so exports exactly these).
-EXPORTS = ("fcr_workspace_size", "fcr_forward", "fcr_backward", "fcr_plant_rk4", "fcr_window_gather",
-           "fcr_last_error", "fcr_abi_version")
+EXPORTS = ("fcr_workspace_size", "fcr_forward", "fcr_backward", "fcr_lstm_workspace_size", "fcr_lstm_forward",
+           "fcr_lstm_backward", "fcr_plant_rk4", "fcr_window_gather", "fcr_last_error", "fcr_abi_version")
 
 
 class FcrDims(ctypes.Structure):
@@ -75,6 +75,13 @@ def load() -> ctypes.CDLL:
         lib.fcr_backward.restype = i32
         lib.fcr_plant_rk4.argtypes = [i32, i32, ctypes.c_double, i32, i32, vp, vp, vp, vp]
         lib.fcr_plant_rk4.restype = i32
+        lib.fcr_lstm_workspace_size.argtypes = [ctypes.POINTER(FcrDims), i32, ctypes.POINTER(sz)]
+        lib.fcr_lstm_workspace_size.restype = i32
+        lib.fcr_lstm_forward.argtypes = [ctypes.POINTER(FcrDims), ctypes.POINTER(FcrWeights), vp, vp, i32, vp, sz, vp]
+        lib.fcr_lstm_forward.restype = i32
+        lib.fcr_lstm_backward.argtypes = [ctypes.POINTER(FcrDims), ctypes.POINTER(FcrWeights), vp,
+                                          ctypes.POINTER(vp), ctypes.POINTER(vp), vp, vp, vp, vp, sz, vp]
+        lib.fcr_lstm_backward.restype = i32
         lib.fcr_window_gather.argtypes = [ctypes.POINTER(FcrWindows), i32, vp, vp, vp, vp, vp, vp]
         lib.fcr_window_gather.restype = i32
         lib.fcr_last_error.argtypes = []

@@ -16,6 +16,7 @@
 #include "fcr_img.h"
 #include "fcr_pack.h"
 #include "fcr_plant.h"
+#include "fcr_surrogate.h"
 #include "fcr_window.h"
 #include "fcr_wide.h"
 
@@ -263,13 +264,14 @@ WideArgs wide_args(const fcr_dims *d, const WideLayout &L, char *base) {
 }
 
 // One window's cells, forward: 3 layers x 10 steps of [GEMM x_t W_ih^T, GEMM h_{t-1} W_hh^T, cell]
-int wide_cells(rocblas_handle h, const WideArgs &a, const WideLayout &L, char *base, bool keep_act, hipStream_t s) {
+int wide_cells(rocblas_handle h, const WideArgs &a, const float *const *w_ih, const float *const *w_hh, bool keep_act,
+               hipStream_t s) {
     const int B = a.B, H = a.H;
     const size_t cell = (size_t)B * H;
     const int nb = (int)((cell + 255) / 256);
     int rc;
     for (int l = 0; l < kLayers; ++l) {
-        const float *wih = (const float *)(base + L.wih[l]), *whh = (const float *)(base + L.whh[l]);
+        const float *wih = w_ih[l], *whh = w_hh[l];
         for (int t = 0; t < kL; ++t) {
             const float *x = l == 0 ? a.X0 + (size_t)t * B * kIn : a.Hs + ((size_t)(l - 1) * kL + t) * cell;
             if ((rc = gemm_xwt(h, B, 4 * H, l == 0 ? kIn : H, wih, x, 0.0f, a.G))) return rc;
@@ -325,11 +327,16 @@ int wide_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const 
     a.states = states;
     a.noise = noise;
     a.pred = prediction;
+    const float *wih[kLayers], *whh[kLayers];
+    for (int l = 0; l < kLayers; ++l) {
+        wih[l] = (const float *)(base + L.wih[l]);
+        whh[l] = (const float *)(base + L.whh[l]);
+    }
     const int nb = (d->B + 255) / 256;
     for (int j = 0; j < d->N; ++j) {
         hipLaunchKernelGGL(wide_window_kernel<true>, dim3(nb), dim3(256), 0, s, a, j);
         if ((rc = launch_check("wide_window_kernel"))) return rc;
-        if ((rc = wide_cells(h, a, L, base, false, s))) return rc;
+        if ((rc = wide_cells(h, a, wih, whh, false, s))) return rc;
         hipLaunchKernelGGL(wide_readout_kernel, dim3(nb), dim3(256), 0, s, a, j,
                            (const float *)(a.Hs + ((size_t)2 * kL + kL - 1) * d->B * H));
         if ((rc = launch_check("wide_readout_kernel"))) return rc;
@@ -356,6 +363,11 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
     a.pred = (float *)prediction;
     a.dloss = dloss;
     float *D[2] = {(float *)(base + L.D[0]), (float *)(base + L.D[1])};
+    const float *wih[kLayers], *whh[kLayers];
+    for (int l = 0; l < kLayers; ++l) {
+        wih[l] = (const float *)(base + L.wih[l]);
+        whh[l] = (const float *)(base + L.whh[l]);
+    }
     if (hipMemsetAsync(a.rowg, 0, sizeof(float) * (size_t)(d->N + kL - 1) * B * kIn, s) != hipSuccess)
         return fail(FCR_EHIP, "hipMemsetAsync failed");
     for (int j = d->N - 1; j >= 0; --j) {
@@ -363,9 +375,8 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
         if ((rc = launch_check("wide_head_kernel"))) return rc;
         hipLaunchKernelGGL(wide_window_kernel<false>, dim3(nb), dim3(256), 0, s, a, j);
         if ((rc = launch_check("wide_window_kernel"))) return rc;
-        if ((rc = wide_cells(h, a, L, base, true, s))) return rc;   // checkpoint: recompute the window
+        if ((rc = wide_cells(h, a, wih, whh, true, s))) return rc;   // checkpoint: recompute the window
         for (int l = kLayers - 1; l >= 0; --l) {
-            const float *wih = (const float *)(base + L.wih[l]), *whh = (const float *)(base + L.whh[l]);
             if (l < kLayers - 1 && hipMemsetAsync(a.dH, 0, sizeof(float) * cell, s) != hipSuccess)
                 return fail(FCR_EHIP, "hipMemsetAsync failed");
             if (hipMemsetAsync(a.dC, 0, sizeof(float) * cell, s) != hipSuccess) return fail(FCR_EHIP, "hipMemsetAsync failed");
@@ -377,11 +388,11 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
                                    a.dC, a.G, B, H);
                 if ((rc = launch_check("wide_cell_bwd_kernel"))) return rc;
                 if (l > 0) {
-                    if ((rc = gemm_gw(h, B, 4 * H, H, wih, a.G, 0.0f, D[l - 1] + (size_t)t * cell))) return rc;
+                    if ((rc = gemm_gw(h, B, 4 * H, H, wih[l], a.G, 0.0f, D[l - 1] + (size_t)t * cell))) return rc;
                 } else {   // layer 0: the window rows' gradients, row j + t
-                    if ((rc = gemm_gw(h, B, 4 * H, kIn, wih, a.G, 1.0f, a.rowg + (size_t)(j + t) * B * kIn))) return rc;
+                    if ((rc = gemm_gw(h, B, 4 * H, kIn, wih[l], a.G, 1.0f, a.rowg + (size_t)(j + t) * B * kIn))) return rc;
                 }
-                if (t > 0 && (rc = gemm_gw(h, B, 4 * H, H, whh, a.G, 0.0f, a.dH))) return rc;
+                if (t > 0 && (rc = gemm_gw(h, B, 4 * H, H, whh[l], a.G, 0.0f, a.dH))) return rc;
             }
         }
     }
@@ -394,6 +405,141 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
     hipLaunchKernelGGL(grad_reduce_kernel, dim3(d->ctrl_hidden * 5), dim3(256), 0, s, (const float *)part,
                        L.ctrl_blocks, d->ctrl_hidden, g_w_inp, g_b_inp, g_w_out);
     return launch_check("grad_reduce_kernel");
+}
+
+// ------------------------------------------------------------------------------------------------
+// LSTM surrogate training step: LSTMModel forward on a window batch and the
+// backward of ALL its weights (Model_NN/Functions.py:520-569), on the per-cell path.
+
+int check_lstm_dims(const fcr_dims *d) {
+    if (!d) return fail(FCR_EINVAL, "dims is NULL");
+    if (d->B < 1) return fail(FCR_EINVAL, "B=%d must be >= 1", d->B);
+    if (d->L != kL) return fail(FCR_EUNSUPPORTED, "L=%d: the window is fixed at 10 rows", d->L);
+    if (d->layers != kLayers) return fail(FCR_EUNSUPPORTED, "layers=%d: built for 3", d->layers);
+    if (d->in_dim != kIn || d->out_dim != kOut)
+        return fail(FCR_EUNSUPPORTED, "in/out = %d/%d: built for 5/4", d->in_dim, d->out_dim);
+    if (d->H < 1 || d->H > kMaxWideH) return fail(FCR_EUNSUPPORTED, "H=%d: built for 1..%d", d->H, kMaxWideH);
+    if ((long long)d->B * kL * 4 * d->H > (1LL << 40)) return fail(FCR_EINVAL, "B*H too large");
+    return FCR_OK;
+}
+
+// Split of the weight-gradient reduction: S chunks of `rows` rows each (S·rows >= n), S partial R x K products.
+// A single GEMM over n = 10·B rows has a tiny output (e.g. 200 x 50) and so only a handful of tiles: the
+// library runs the whole reduction on one or two workgroups. Chunking turns it into a strided-batched GEMM
+// with hundreds of independent tiles plus one fixed-order sum (deterministic).
+struct WgradSplit {
+    int S;
+    long long rows;
+};
+WgradSplit wgrad_split(long long n, int R, int K) {
+    const long long kPartFloats = 16LL << 20;                // 64 MiB of partials at most
+    long long S = n / 8192;                                  // >= 8192 rows per chunk, <= 64 chunks: the
+    S = S < 1 ? 1 : (S > 64 ? 64 : S);                       // fixed-order sum stays a small fraction
+    while (S > 1 && S * R * K > kPartFloats) S >>= 1;
+    const long long rows = (n + S - 1) / S;
+    return {(int)((n + rows - 1) / rows), rows};
+}
+size_t wgrad_part_floats(long long n, int R, int K) {
+    const WgradSplit w = wgrad_split(n, R, K);
+    return w.S > 1 ? (size_t)w.S * R * K : 0;
+}
+
+struct LstmLayout {
+    size_t X0, Hs, Cs, G, Act, dGs, dH, dC, D[2], gx, part, total;
+};
+
+LstmLayout make_lstm(const fcr_dims *d, int with_backward) {
+    LstmLayout L{};
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += align_up(bytes);
+        return o;
+    };
+    const size_t B = d->B, H = d->H, F = sizeof(float);
+    L.X0 = take(F * kL * B * kIn);
+    L.Hs = take(F * kLayers * kL * B * H);
+    L.Cs = take(F * kLayers * kL * B * H);
+    L.G = take(F * B * 4 * H);
+    if (with_backward) {
+        L.Act = take(F * kLayers * kL * B * 4 * H);
+        L.dGs = take(F * kL * B * 4 * H);
+        L.dH = take(F * B * H);
+        L.dC = take(F * B * H);
+        L.D[0] = take(F * kL * B * H);
+        L.D[1] = take(F * kL * B * H);
+        L.gx = take(F * kL * B * kIn);
+        size_t pf = wgrad_part_floats((long long)B, kOut, H);   // the largest split of any weight gradient
+        for (int K : {kIn, (int)H}) {
+            const size_t a = wgrad_part_floats((long long)kL * B, 4 * H, K);
+            pf = a > pf ? a : pf;
+        }
+        L.part = take(F * (pf ? pf : 1));
+    }
+    L.total = off;
+    return L;
+}
+
+__global__ void wgrad_sum_kernel(const float *__restrict__ part, int S, long long RK, float *__restrict__ dW) {
+    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= RK) return;
+    float acc = 0.0f;
+    for (int s = 0; s < S; ++s) acc += part[(long long)s * RK + e];
+    dW[e] = acc;
+}
+
+// dW (row-major R x K) = Σ_n dG[n][r] · X[n][k]: dG (n x R), X (n x K) row-major — the weight gradient of one
+// LSTM weight matrix with the reduction over n = (window step, sample) rows. `part` holds
+// wgrad_part_floats(n, R, K) floats (unused when the reduction is not split).
+int gemm_wgrad(rocblas_handle h, long long n, int R, int K, const float *dG, const float *X, float *part, float *dW,
+               hipStream_t s) {
+    const float one = 1.0f, zero = 0.0f;
+    const WgradSplit w = wgrad_split(n, R, K);
+    rocblas_status st;
+    if (w.S == 1) {
+        st = rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, K, R, (int)n, &one, X, K, dG, R,
+                           &zero, dW, K);
+    } else {
+        // full chunks as one strided-batched call, the ragged last chunk as its own GEMM
+        const int full = (int)(n / w.rows);
+        st = rocblas_sgemm_strided_batched(h, rocblas_operation_none, rocblas_operation_transpose, K, R, (int)w.rows,
+                                           &one, X, K, w.rows * K, dG, R, w.rows * R, &zero, part, K, (long long)R * K,
+                                           full);
+        if (st == rocblas_status_success && full < w.S) {
+            const long long r0 = (long long)full * w.rows;
+            st = rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, K, R, (int)(n - r0), &one,
+                               X + r0 * K, K, dG + r0 * R, R, &zero, part + (long long)full * R * K, K);
+        }
+        if (st == rocblas_status_success) {
+            const long long RK = (long long)R * K;
+            hipLaunchKernelGGL(wgrad_sum_kernel, dim3((unsigned)((RK + 255) / 256)), dim3(256), 0, s, (const float *)part,
+                               w.S, RK, dW);
+            if (hipGetLastError() != hipSuccess) return fail(FCR_EHIP, "launch of wgrad_sum_kernel failed");
+        }
+    }
+    return st == rocblas_status_success ? FCR_OK : fail(FCR_EHIP, "rocblas_sgemm (weight gradient) failed: %d", (int)st);
+}
+
+int lstm_weights_ok(const fcr_weights *w) {
+    if (!w || !w->fc_w || !w->fc_b) return 0;
+    for (int l = 0; l < kLayers; ++l)
+        if (!w->w_ih[l] || !w->w_hh[l]) return 0;
+    return 1;
+}
+
+WideArgs lstm_args(const fcr_dims *d, const LstmLayout &L, char *base) {
+    WideArgs a{};
+    a.B = d->B;
+    a.N = 1;
+    a.H = d->H;
+    a.X0 = (float *)(base + L.X0);
+    a.Hs = (float *)(base + L.Hs);
+    a.Cs = (float *)(base + L.Cs);
+    a.G = (float *)(base + L.G);
+    a.Act = L.Act ? (float *)(base + L.Act) : nullptr;
+    a.dH = L.dH ? (float *)(base + L.dH) : nullptr;
+    a.dC = L.dC ? (float *)(base + L.dC) : nullptr;
+    return a;
 }
 
 }  // namespace
@@ -612,6 +758,107 @@ int fcr_window_gather(const fcr_windows *t, int32_t B, const int64_t *idx, float
     hipLaunchKernelGGL(window::window_gather_kernel, dim3((unsigned)((n + window::kWinBlock - 1) / window::kWinBlock)),
                        dim3(window::kWinBlock), 0, s, a);
     return launch_check("window_gather_kernel");
+}
+
+int fcr_lstm_workspace_size(const fcr_dims *dims, int with_backward, size_t *bytes) {
+    int rc = check_lstm_dims(dims);
+    if (rc) return rc;
+    if (!bytes) return fail(FCR_EINVAL, "bytes is NULL");
+    *bytes = make_lstm(dims, with_backward).total;
+    return FCR_OK;
+}
+
+int fcr_lstm_forward(const fcr_dims *d, const fcr_weights *w, const float *x, float *y, int with_backward, void *ws,
+                     size_t ws_bytes, void *stream) {
+    int rc = check_lstm_dims(d);
+    if (rc) return rc;
+    if (!x || !y || !ws) return fail(FCR_EINVAL, "fcr_lstm_forward: a required pointer is NULL");
+    if (!lstm_weights_ok(w)) return fail(FCR_EINVAL, "fcr_lstm_forward: an LSTM/fc weight pointer is NULL");
+    if (((uintptr_t)ws) & 255) return fail(FCR_EINVAL, "fcr_lstm_forward: ws must be 256-byte aligned");
+    const LstmLayout L = make_lstm(d, with_backward);
+    if (ws_bytes < L.total) return fail(FCR_EWORKSPACE, "fcr_lstm_forward: ws has %zu bytes, needs %zu", ws_bytes, L.total);
+    hipStream_t s = (hipStream_t)stream;
+    char *base = (char *)ws;
+    const int B = d->B, H = d->H;
+    const long long nx = (long long)B * kL * kIn;
+    hipLaunchKernelGGL(surrogate::window_transpose_kernel, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, s, x,
+                       (float *)(base + L.X0), B, kIn, false);
+    if ((rc = launch_check("window_transpose_kernel"))) return rc;
+    rocblas_handle h = blas_on(s);
+    if (!h) return fail(FCR_EHIP, "rocblas_create_handle failed");
+    const WideArgs a = lstm_args(d, L, base);
+    if ((rc = wide_cells(h, a, w->w_ih, w->w_hh, with_backward != 0, s))) return rc;
+    hipLaunchKernelGGL(surrogate::readout_kernel, dim3((B + 255) / 256), dim3(256), 0, s,
+                       (const float *)(a.Hs + ((size_t)(kLayers - 1) * kL + kL - 1) * B * H), w->fc_w, w->fc_b, y, B, H);
+    return launch_check("readout_kernel");
+}
+
+int fcr_lstm_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, float *const *g_w_ih,
+                      float *const *g_w_hh, float *g_fc_w, float *g_fc_b, float *g_x, void *ws, size_t ws_bytes,
+                      void *stream) {
+    int rc = check_lstm_dims(d);
+    if (rc) return rc;
+    if (!dy || !ws || !g_w_ih || !g_w_hh || !g_fc_w || !g_fc_b)
+        return fail(FCR_EINVAL, "fcr_lstm_backward: a required pointer is NULL");
+    for (int l = 0; l < kLayers; ++l)
+        if (!g_w_ih[l] || !g_w_hh[l]) return fail(FCR_EINVAL, "fcr_lstm_backward: gradient of layer %d is NULL", l);
+    if (!lstm_weights_ok(w)) return fail(FCR_EINVAL, "fcr_lstm_backward: an LSTM/fc weight pointer is NULL");
+    if (((uintptr_t)ws) & 255) return fail(FCR_EINVAL, "fcr_lstm_backward: ws must be 256-byte aligned");
+    const LstmLayout L = make_lstm(d, 1);
+    if (ws_bytes < L.total) return fail(FCR_EWORKSPACE, "fcr_lstm_backward: ws has %zu bytes, needs %zu", ws_bytes, L.total);
+    hipStream_t s = (hipStream_t)stream;
+    char *base = (char *)ws;
+    const int B = d->B, H = d->H;
+    const size_t cell = (size_t)B * H, gcell = (size_t)B * 4 * H;
+    const int nc = (int)((cell + 255) / 256);
+    rocblas_handle h = blas_on(s);
+    if (!h) return fail(FCR_EHIP, "rocblas_create_handle failed");
+    const WideArgs a = lstm_args(d, L, base);
+    float *dGs = (float *)(base + L.dGs);
+    float *D[2] = {(float *)(base + L.D[0]), (float *)(base + L.D[1])};
+    float *gx = (float *)(base + L.gx);
+    const float *htop = a.Hs + ((size_t)(kLayers - 1) * kL + kL - 1) * cell;
+    // readout: d fc.W = dy^T h_9, d fc.b = Σ dy, dh_9 = dy fc.W
+    float *part = (float *)(base + L.part);
+    if ((rc = gemm_wgrad(h, B, kOut, H, dy, htop, part, g_fc_w, s))) return rc;
+    hipLaunchKernelGGL(surrogate::bias_grad_kernel, dim3(kOut), dim3(surrogate::kSurBlock), 0, s, dy, g_fc_b, B);
+    if ((rc = launch_check("bias_grad_kernel"))) return rc;
+    hipLaunchKernelGGL(surrogate::readout_bwd_kernel, dim3(nc), dim3(256), 0, s, dy, w->fc_w, a.dH, B, H);
+    if ((rc = launch_check("readout_bwd_kernel"))) return rc;
+    for (int l = kLayers - 1; l >= 0; --l) {
+        const int K = l == 0 ? kIn : H;
+        if (l < kLayers - 1 && hipMemsetAsync(a.dH, 0, sizeof(float) * cell, s) != hipSuccess)
+            return fail(FCR_EHIP, "hipMemsetAsync failed");
+        if (hipMemsetAsync(a.dC, 0, sizeof(float) * cell, s) != hipSuccess) return fail(FCR_EHIP, "hipMemsetAsync failed");
+        for (int t = kL - 1; t >= 0; --t) {
+            const size_t c_off = ((size_t)l * kL + t) * cell;
+            float *dG = dGs + (size_t)t * gcell;
+            hipLaunchKernelGGL(wide_cell_bwd_kernel, dim3(nc), dim3(256), 0, s, (const float *)(a.Act + c_off * 4),
+                               (const float *)(a.Cs + c_off), t > 0 ? (const float *)(a.Cs + c_off - cell) : nullptr,
+                               (const float *)a.dH, l < kLayers - 1 ? (const float *)(D[l] + (size_t)t * cell) : nullptr,
+                               a.dC, dG, B, H);
+            if ((rc = launch_check("wide_cell_bwd_kernel"))) return rc;
+            if (l > 0) {
+                if ((rc = gemm_gw(h, B, 4 * H, H, w->w_ih[l], dG, 0.0f, D[l - 1] + (size_t)t * cell))) return rc;
+            } else if (g_x) {
+                if ((rc = gemm_gw(h, B, 4 * H, kIn, w->w_ih[0], dG, 0.0f, gx + (size_t)t * B * kIn))) return rc;
+            }
+            if (t > 0 && (rc = gemm_gw(h, B, 4 * H, H, w->w_hh[l], dG, 0.0f, a.dH))) return rc;
+        }
+        // the layer's weight gradients: one GEMM each over all (step, sample) rows
+        const float *xin = l == 0 ? a.X0 : a.Hs + (size_t)(l - 1) * kL * cell;
+        if ((rc = gemm_wgrad(h, (long long)kL * B, 4 * H, K, dGs, xin, part, g_w_ih[l], s))) return rc;
+        if ((rc = gemm_wgrad(h, (long long)(kL - 1) * B, 4 * H, H, dGs + gcell, a.Hs + (size_t)l * kL * cell, part,
+                             g_w_hh[l], s)))
+            return rc;
+    }
+    if (g_x) {
+        const long long nx = (long long)B * kL * kIn;
+        hipLaunchKernelGGL(surrogate::window_transpose_kernel, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, s,
+                           (const float *)gx, g_x, B, kIn, true);
+        if ((rc = launch_check("window_transpose_kernel"))) return rc;
+    }
+    return FCR_OK;
 }
 
 }  // extern "C"

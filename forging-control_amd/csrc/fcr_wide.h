@@ -79,17 +79,19 @@ __global__ void wide_window_kernel(WideArgs a, int j) {
 }
 
 // Cell update from the gate pre-activations G [B][4H] (torch gate order i|f|g|o): c, h; and, for the
-// backward's recompute, the activations.
+// backward's recompute, the activations. tanh is the library's (a few ulp RELATIVE to tanh): these
+// memory-bound kernels can afford it, and the weight gradients of the surrogate step need it when the
+// hidden states are small (1 - 2/(1 + e^{2x}) is only accurate to ~1e-7 absolute).
 __global__ void wide_cell_kernel(const float *__restrict__ G, const float *__restrict__ c_prev, float *c_out,
                                  float *h_out, float *act, int B, int H) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (size_t)B * H) return;
     const size_t b = idx / H, u = idx % H;
     const float *g4 = G + b * 4 * H + u;
-    const float i = sigm(g4[0]), f = sigm(g4[H]), g = tanh_f(g4[2 * H]), o = sigm(g4[3 * H]);
+    const float i = sigm(g4[0]), f = sigm(g4[H]), g = tanhf(g4[2 * H]), o = sigm(g4[3 * H]);
     const float c = (c_prev ? f * c_prev[idx] : 0.0f) + i * g;
     c_out[idx] = c;
-    h_out[idx] = o * tanh_f(c);
+    h_out[idx] = o * tanhf(c);
     if (act) {
         float *a4 = act + b * 4 * H + u;
         a4[0] = i;
@@ -182,7 +184,7 @@ __global__ void wide_cell_bwd_kernel(const float *__restrict__ act, const float 
     const size_t b = idx / H, u = idx % H;
     const float *a4 = act + b * 4 * H + u;
     const float i = a4[0], f = a4[H], g = a4[2 * H], o = a4[3 * H];
-    const float tc = tanh_f(c[idx]);
+    const float tc = tanhf(c[idx]);
     const float cp = c_prev ? c_prev[idx] : 0.0f;
     const float dh = dH[idx] + (din ? din[idx] : 0.0f);
     const float dct = dC[idx] + dh * o * (1.0f - tc * tc);

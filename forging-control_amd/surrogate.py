@@ -1,0 +1,104 @@
+"""LSTM surrogate training on the gfx950 path.
+
+The reference trains the plant surrogate ``LSTMModel(5, 50, 4, 3)`` with ``nn.MSELoss`` and AdamW
+(Model_NN/Main.py:218-242) through ``NeuralNetwork.train_model`` (Model_NN/Functions.py:520-569), i.e.
+``output = model(X, device); loss = loss_function(output, y.squeeze()); loss.backward();
+optimizer.step()`` per batch. Here ``LSTMModel.forward`` on a ROCm device runs :class:`LSTMFunction`:
+``fcr_lstm_forward`` (per-cell rocBLAS gate GEMMs + HIP cell kernels, every cell's state kept) and, on
+``backward``, ``fcr_lstm_backward`` (dgates per cell, then ONE weight-gradient GEMM per weight matrix
+over all 10·B (step, sample) rows). Every LSTM weight, the readout and — when it requires grad — the
+input window receive gradients, so the reference's loop and optimizer run unchanged.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _native
+from .rollout import WINDOW_ROWS, make_dims
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _weights(w_ih, w_hh, fc_w, fc_b):
+    w = _native.FcrWeights()
+    w.w_ih = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in w_ih])
+    w.w_hh = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in w_hh])
+    w.fc_w, w.fc_b = fc_w.data_ptr(), fc_b.data_ptr()
+    return w
+
+
+class LSTMFunction(torch.autograd.Function):
+    """y = LSTMModel(x) with gradients for x and every weight (fcr_lstm_forward / fcr_lstm_backward)."""
+
+    @staticmethod
+    def forward(ctx, x, w_ih0, w_ih1, w_ih2, w_hh0, w_hh1, w_hh2, fc_w, fc_b):
+        dev = x.device
+        B, H = x.shape[0], w_hh0.shape[1]
+        dims = make_dims(B, 1, H, 3, 1, 0.0)
+        ts = [t.detach().to(torch.float32).contiguous() for t in (x, w_ih0, w_ih1, w_ih2, w_hh0, w_hh1, w_hh2, fc_w, fc_b)]
+        xc, w_ih, w_hh, fcw, fcb = ts[0], ts[1:4], ts[4:7], ts[7], ts[8]
+        w = _weights(w_ih, w_hh, fcw, fcb)
+        need_grad = any(ctx.needs_input_grad)
+        lib = _native.load()
+        nbytes = ctypes.c_size_t(0)
+        _native.check(lib.fcr_lstm_workspace_size(ctypes.byref(dims), int(need_grad), ctypes.byref(nbytes)),
+                      "fcr_lstm_workspace_size")
+        ws = torch.empty(nbytes.value, dtype=torch.uint8, device=dev)
+        y = torch.empty(B, 4, dtype=torch.float32, device=dev)
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        _native.check(lib.fcr_lstm_forward(ctypes.byref(dims), ctypes.byref(w), _p(xc), _p(y), int(need_grad),
+                                           _p(ws), ws.numel(), stream), "fcr_lstm_forward")
+        if need_grad:
+            ctx.dims, ctx.ws, ctx.tensors = dims, ws, ts
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        ts = ctx.tensors
+        xc, w_ih, w_hh, fcw, fcb = ts[0], ts[1:4], ts[4:7], ts[7], ts[8]
+        dev = xc.device
+        g = [torch.empty_like(t) for t in ts]
+        w = _weights(w_ih, w_hh, fcw, fcb)
+        g_ih = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in g[1:4]])
+        g_hh = (ctypes.c_void_p * 3)(*[t.data_ptr() for t in g[4:7]])
+        dyc = dy.to(torch.float32).contiguous()
+        lib = _native.load()
+        _native.check(lib.fcr_lstm_backward(ctypes.byref(ctx.dims), ctypes.byref(w), _p(dyc), g_ih, g_hh, _p(g[7]),
+                                            _p(g[8]), _p(g[0]) if ctx.needs_input_grad[0] else None, _p(ctx.ws),
+                                            ctx.ws.numel(), ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
+                      "fcr_lstm_backward")
+        return tuple(gi if need else None for gi, need in zip(g, ctx.needs_input_grad))
+
+
+def lstm_apply(model, x: torch.Tensor) -> torch.Tensor:
+    """LSTMModel forward on the HIP path (x (B, 10, 5) on a ROCm device)."""
+    lstm = model.lstm
+    if x.device.type != "cuda":
+        raise RuntimeError(f"LSTMModel runs on a ROCm device only (got {x.device}); move the model and the "
+                           "windows to the GPU — there is no CPU path")
+    if lstm.bias or lstm.num_layers != 3 or lstm.input_size != 5 or model.fc.out_features != 4:
+        raise RuntimeError("the gfx950 LSTM path is built for LSTMModel(5, H, 4, 3) without LSTM bias "
+                           "(Model_NN/Main.py:225, UL/Main.py:144-154)")
+    if x.dim() != 3 or x.shape[1:] != (WINDOW_ROWS, 5):
+        raise ValueError(f"x must be (B, 10, 5), got {tuple(x.shape)}")
+    p = [getattr(lstm, f"weight_ih_l{k}") for k in range(3)] + [getattr(lstm, f"weight_hh_l{k}") for k in range(3)]
+    return LSTMFunction.apply(x, *p, model.fc.weight, model.fc.bias)
+
+
+def train_model(data_loader, model, loss_function, optimizer, device):
+    """Model_NN/Functions.py:520-569 with the same arguments and return value (average batch loss)."""
+    model.train()
+    total = 0.0
+    for X, y in data_loader:
+        X, y = X.to(device), y.to(device)
+        optimizer.zero_grad()
+        output = model(X, device)
+        loss = loss_function(output, y.squeeze())
+        loss.backward()
+        optimizer.step()
+        total += loss.item()
+    return total / len(data_loader)

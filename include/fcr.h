@@ -144,6 +144,28 @@ typedef struct fcr_windows {
 int fcr_window_gather(const fcr_windows *tables, int32_t B, const int64_t *idx,
                       float *x, float *y, float *z, int32_t *bad, void *stream);
 
+/*
+ * LSTM surrogate training step: what one iteration of
+ * NeuralNetwork.train_model (Model_NN/Functions.py:520-569) asks of LSTMModel (Model_NN/Functions.py:
+ * 255-330, trained by Model_NN/Main.py:218-242): the forward on a window batch and loss.backward() into
+ * every weight. `dims` uses B, H, L (=10), layers (=3), in_dim (=5), out_dim (=4); the controller fields
+ * are ignored. Weights: fcr_weights' w_ih/w_hh/fc_w/fc_b (the controller pointers are ignored).
+ *   x  (B,10,5)  windows          y (B,4) = fc(h_9 of the top layer) + b
+ * with_backward != 0 keeps every cell's state in `ws` for fcr_lstm_backward.
+ */
+int fcr_lstm_workspace_size(const fcr_dims *dims, int with_backward, size_t *bytes);
+int fcr_lstm_forward(const fcr_dims *dims, const fcr_weights *w, const float *x, float *y,
+                     int with_backward, void *ws, size_t ws_bytes, void *stream);
+
+/*
+ * Backward of the last fcr_lstm_forward(with_backward=1) on the same `ws` and weights, given dy = dL/dy
+ * (B,4): gradients of weight_ih_l{0,1,2} (4H,5|H), weight_hh_l{0,1,2} (4H,H), fc.weight (4,H), fc.bias (4),
+ * OVERWRITTEN, fixed reduction order; g_x (B,10,5) = dL/dx, or NULL to skip it.
+ */
+int fcr_lstm_backward(const fcr_dims *dims, const fcr_weights *w, const float *dy,
+                      float *const *g_w_ih, float *const *g_w_hh, float *g_fc_w, float *g_fc_b, float *g_x,
+                      void *ws, size_t ws_bytes, void *stream);
+
 /* Thread-local description of the last error (never NULL). */
 const char *fcr_last_error(void);
 

@@ -1,0 +1,163 @@
+"""LSTM surrogate training step: fcr_lstm_forward/backward vs the fp64 torch
+restatement of Model_NN's train_model body (every weight gradient, the input gradient, AdamW steps)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import forging_control_amd as fca
+from conftest import GOLDEN, relerr
+from oracle import surrogate_torch as S
+from tests.golden.make_golden import synth_params
+
+TOL = 1e-5
+
+
+def ref_params():
+    w = dict(np.load(os.path.join(GOLDEN, "weights_ref.npz")))
+    return {"Wih": [w[f"Wih{k}"].astype(np.float64) for k in range(3)],
+            "Whh": [w[f"Whh{k}"].astype(np.float64) for k in range(3)],
+            "fcW": w["fcW"].astype(np.float64), "fcb": w["fcb"].astype(np.float64)}
+
+
+def params_for(H, seed=0):
+    if H == 50:
+        return ref_params()
+    p = synth_params(H, seed)
+    return {"Wih": [np.asarray(a, np.float64) for a in p["Wih"]], "Whh": [np.asarray(a, np.float64) for a in p["Whh"]],
+            "fcW": np.asarray(p["fcW"], np.float64), "fcb": np.asarray(p["fcb"], np.float64)}
+
+
+def batch(B, seed):
+    rng = np.random.default_rng(seed)
+    x = rng.uniform(-1, 1, (B, 10, 5))
+    x[..., 1:3] = rng.uniform(0, 1.1, (B, 10, 2))      # pressures, as the rollout's windows
+    return x, rng.uniform(-1, 1, (B, 4))
+
+
+# ------------------------------------------------------------------------------------------------ CPU
+
+def test_oracle_gradients_match_finite_differences():
+    p = params_for(3, seed=1)
+    x, target = batch(2, 0)
+    _, loss, g = S.step_grads(p, x, target)
+    rng = np.random.default_rng(0)
+    for key, k in (("Wih", 0), ("Whh", 2), ("Wih", 1)):
+        W = p[key][k]
+        for _ in range(3):
+            i = tuple(rng.integers(0, s) for s in W.shape)
+            eps = 1e-6
+            W[i] += eps
+            lp = S.step_grads(p, x, target)[1]
+            W[i] -= 2 * eps
+            lm = S.step_grads(p, x, target)[1]
+            W[i] += eps
+            assert (lp - lm) / (2 * eps) == pytest.approx(g[key][k][i], rel=1e-6, abs=1e-10)
+
+
+def test_lstm_model_refuses_cpu_tensors():
+    m = fca.LSTMModel(5, 50, 4, 3)
+    with pytest.raises(RuntimeError, match="ROCm device only"):
+        m(torch.zeros(2, 10, 5), "cpu")
+
+
+def test_abi_validates_before_any_device_call():
+    lib = fca._native.load()
+    d = fca.rollout.make_dims(16, 1, 50, 3, 1, 0.0)
+    out = ctypes.c_size_t(0)
+    assert lib.fcr_lstm_workspace_size(ctypes.byref(d), 1, ctypes.byref(out)) == 0
+    fwd_only = ctypes.c_size_t(0)
+    assert lib.fcr_lstm_workspace_size(ctypes.byref(d), 0, ctypes.byref(fwd_only)) == 0
+    assert 0 < fwd_only.value < out.value
+    bad = fca.rollout.make_dims(16, 1, 50, 2, 1, 0.0)
+    assert lib.fcr_lstm_workspace_size(ctypes.byref(bad), 1, ctypes.byref(out)) == -4
+    w = fca._native.FcrWeights()
+    assert lib.fcr_lstm_forward(ctypes.byref(d), ctypes.byref(w), None, None, 1, None, 0, None) == -1
+    assert "NULL" in lib.fcr_last_error().decode()
+    assert lib.fcr_lstm_backward(ctypes.byref(d), ctypes.byref(w), None, None, None, None, None, None, None, 0,
+                                 None) == -1
+
+
+# ------------------------------------------------------------------------------------------------ GPU
+
+def model_for(p, dev="cuda:0"):
+    H = p["Whh"][0].shape[1]
+    m = fca.LSTMModel(5, H, 4, 3).to(dev)
+    t = lambda a: torch.as_tensor(np.asarray(a, np.float32))
+    with torch.no_grad():
+        for k in range(3):
+            getattr(m.lstm, f"weight_ih_l{k}").copy_(t(p["Wih"][k]))
+            getattr(m.lstm, f"weight_hh_l{k}").copy_(t(p["Whh"][k]))
+        m.fc.weight.copy_(t(p["fcW"]))
+        m.fc.bias.copy_(t(p["fcb"]))
+    return m
+
+
+def grads_of(m):
+    return {"Wih": [getattr(m.lstm, f"weight_ih_l{k}").grad.cpu().numpy() for k in range(3)],
+            "Whh": [getattr(m.lstm, f"weight_hh_l{k}").grad.cpu().numpy() for k in range(3)],
+            "fcW": m.fc.weight.grad.cpu().numpy(), "fcb": m.fc.bias.grad.cpu().numpy()}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,B", [(50, 256), (50, 1), (50, 4099), (7, 33), (64, 100), (256, 64)])
+def test_gpu_training_step_matches_oracle(H, B):
+    p = params_for(H, seed=H)
+    x, target = batch(B, seed=B + H)
+    y_ref, loss_ref, g_ref = S.step_grads(p, x, target)
+    m = model_for(p)
+    xt = torch.tensor(x, dtype=torch.float32, device="cuda:0", requires_grad=True)
+    y = m(xt, "cuda:0")
+    loss = torch.nn.functional.mse_loss(y, torch.tensor(target, dtype=torch.float32, device="cuda:0"))
+    loss.backward()
+    assert relerr(y.detach().cpu().numpy(), y_ref) < TOL
+    assert abs(float(loss) - loss_ref) <= TOL * abs(loss_ref)
+    g = grads_of(m)
+    for key in ("Wih", "Whh"):
+        for k in range(3):
+            assert relerr(g[key][k], g_ref[key][k]) < TOL, (key, k, relerr(g[key][k], g_ref[key][k]))
+    assert relerr(g["fcW"], g_ref["fcW"]) < TOL and relerr(g["fcb"], g_ref["fcb"]) < TOL
+    assert relerr(xt.grad.cpu().numpy(), g_ref["x"]) < TOL
+
+
+@pytest.mark.gpu
+def test_gpu_adamw_trajectory_matches_oracle():
+    """Five train_model iterations (MSE + AdamW lr 1e-3, wd 0; Model_NN/Main.py:229-232) on fixed batches:
+    the parameters after the last step agree with the fp64 restatement."""
+    p = ref_params()
+    batches = [batch(256, seed=s) for s in range(5)]
+    ref, ref_losses = S.train_steps(p, batches, lr=1e-3)
+    m = model_for(p)
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=0.0)
+    loader = [(torch.tensor(x, dtype=torch.float32), torch.tensor(t, dtype=torch.float32)) for x, t in batches]
+    losses = []
+    for X, Y in loader:           # fca.surrogate.train_model's body, losses kept per step
+        X, Y = X.to("cuda:0"), Y.to("cuda:0")
+        opt.zero_grad()
+        loss = torch.nn.functional.mse_loss(m(X, "cuda:0"), Y.squeeze())
+        loss.backward()
+        opt.step()
+        losses.append(float(loss))
+    assert np.allclose(losses, ref_losses, rtol=TOL)
+    got = {"Wih": [getattr(m.lstm, f"weight_ih_l{k}").detach().cpu().numpy() for k in range(3)],
+           "Whh": [getattr(m.lstm, f"weight_hh_l{k}").detach().cpu().numpy() for k in range(3)]}
+    for key in ("Wih", "Whh"):
+        for k in range(3):
+            assert relerr(got[key][k], ref[key][k]) < TOL
+    avg = fca.surrogate.train_model(loader, m, torch.nn.MSELoss(), opt, "cuda:0")
+    assert np.isfinite(avg)
+
+
+@pytest.mark.gpu
+def test_gpu_forward_matches_rollout_kernel_one_step():
+    """The surrogate forward and the rollout's first LSTM call (fused kernel, N = 1) agree on a window."""
+    p = ref_params()
+    x, _ = batch(512, seed=3)
+    m = model_for(p)
+    xt = torch.tensor(x, dtype=torch.float32, device="cuda:0")
+    with torch.no_grad():
+        y = m(xt, "cuda:0")
+    y2 = fca.simulate_step(m, xt)
+    assert relerr(y.cpu().numpy(), y2.cpu().numpy()) < 2 * TOL
