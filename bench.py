@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 import forging_control_amd as fca  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3          # MI355X dense FP32 (vector = MFMA), MI355X_MICROARCH.md
+F16_PEAK_TFLOPS = 2500.0          # MI355X dense FP16/BF16 MFMA (no sparsity), MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0             # MI355X HBM3E spec
 ALPHA = 20.0                      # UL/Main.py:192
 
@@ -139,6 +140,8 @@ def main():
     ap.add_argument("--hidden", type=int, default=50)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--precision", choices=("fp32", "f16"), default="fp32",
+                    help="fp32: reference-accurate (default, config 2); f16: config 3's reduced-precision mode")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -154,7 +157,7 @@ def main():
     if world > 1:
         fca.distributed.broadcast_params(ctrl)
     opt = torch.optim.AdamW(ctrl.parameters(), lr=1e-4)     # UL/Main.py:195
-    loss_fn = fca.MPCLoss(prediction_horizon=N, alpha=ALPHA)
+    loss_fn = fca.MPCLoss(prediction_horizon=N, alpha=ALPHA, precision=args.precision)
     sync = fca.distributed.GradAllReduce() if world > 1 else None
     X, S = synth_batch(B, dev, 1000 + rank)
 
@@ -212,17 +215,19 @@ def main():
         dom = ("bwd", b_ms) if b_ms >= f_ms else ("fwd", f_ms)
         achieved = B * N * fl[dom[0]] / (dom[1] * 1e-3) / 1e12
         hbm_roof = HBM_PEAK_GBS * 1e9 / hbm_bytes_per_rollout_step(N)
-        traffic, traffic_src = pmc_traffic(f"fcr_{dom[0]}_kernel") if (B, N, H) == (65536, 10, 50) else (None, None)
+        default_cfg = (B, N, H, args.precision) == (65536, 10, 50, "fp32")
+        traffic, traffic_src = pmc_traffic(f"fcr_{dom[0]}_kernel") if default_cfg else (None, None)
+        peak = FP32_PEAK_TFLOPS if args.precision == "fp32" else F16_PEAK_TFLOPS
         line = {
             "metric": "rollout-steps/s (batch x horizon), fwd+bwd+AdamW step",
             "value": value, "unit": "rollout-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f32", "data": "synthetic (SURVEY §8d distribution); reference-trained LSTM/controller weights",
+            "dtype": "f32" if args.precision == "fp32" else "f16", "data": "synthetic (SURVEY §8d distribution); reference-trained LSTM/controller weights",
             "config": {"workload": f"unsupervised-MPC rollout train step, B={B}/GPU, N={N}, H={H}, 3-layer LSTM, "
-                                   f"ctrl 3-50-1, fp32", "batch_per_gpu": B, "global_batch": B * world, "horizon": N,
+                                   f"ctrl 3-50-1, {args.precision}", "batch_per_gpu": B, "global_batch": B * world, "horizon": N,
                        "hidden": H, "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "kernel": f"fcr_{dom[0]}_kernel", "achieved": achieved,
-                         "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
+                         "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
                          "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src},
             "kernels_ms": {"fwd": f_ms, "bwd": b_ms},
             # the design's own HBM traffic (activation records and hand-off slabs, PMC-measured) against

@@ -14,7 +14,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", _LIB_NAME)
 
 FCR_OK = 0
-ABI_VERSION = 1
+ABI_VERSION = 2
+PRECISION_FP32, PRECISION_F16 = 0, 1
 ERRORS = {-1: "FCR_EINVAL", -2: "FCR_EWORKSPACE", -3: "FCR_EHIP", -4: "FCR_EUNSUPPORTED"}
 
 # Every symbol include/fcr.h declares (tests check the .so exports exactly these).
@@ -27,6 +28,7 @@ class FcrDims(ctypes.Structure):
         ("B", ctypes.c_int32), ("N", ctypes.c_int32), ("L", ctypes.c_int32), ("H", ctypes.c_int32),
         ("layers", ctypes.c_int32), ("in_dim", ctypes.c_int32), ("out_dim", ctypes.c_int32),
         ("ctrl_in", ctypes.c_int32), ("ctrl_hidden", ctypes.c_int32), ("alpha", ctypes.c_float),
+        ("precision", ctypes.c_int32),
     ]
 
 

@@ -64,6 +64,10 @@ int check_dims(const fcr_dims *d) {
     if (d->H < 1 || d->H > kMaxWideH)
         return fail(FCR_EUNSUPPORTED, "H=%d: built for 1..%d", d->H, kMaxWideH);
     if ((long long)d->B * d->N > (1LL << 31)) return fail(FCR_EINVAL, "B*N too large");
+    if (d->precision != FCR_PRECISION_FP32 && d->precision != FCR_PRECISION_F16)
+        return fail(FCR_EINVAL, "precision=%d: FCR_PRECISION_FP32 (0) or FCR_PRECISION_F16 (1)", d->precision);
+    if (d->precision == FCR_PRECISION_F16 && is_wide(d))
+        return fail(FCR_EUNSUPPORTED, "precision=f16 is built for H <= %d (the fused kernels)", 4 * kMaxSlots);
     return FCR_OK;
 }
 
@@ -126,38 +130,44 @@ int launch_check(const char *what) {
     return FCR_OK;
 }
 
-template <int HS, bool STORE>
+template <int HS, bool STORE, bool LP>
 int launch_fwd_t(const FwdArgs &fa, const Layout &L, hipStream_t s) {
     const int lds = Geo16<HS>::LDS_FWD;
     static bool attr_set = false;
     if (!attr_set) {
-        const hipError_t e = hipFuncSetAttribute((const void *)fcr_fwd_kernel<HS, STORE>,
+        const hipError_t e = hipFuncSetAttribute((const void *)fcr_fwd_kernel<HS, STORE, LP>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(fwd): %s", hipGetErrorString(e));
         attr_set = true;
     }
-    hipLaunchKernelGGL((fcr_fwd_kernel<HS, STORE>), dim3(L.nw_pad / kFwdWaves), dim3(kFwdWaves * kWave),
+    hipLaunchKernelGGL((fcr_fwd_kernel<HS, STORE, LP>), dim3(L.nw_pad / kFwdWaves), dim3(kFwdWaves * kWave),
                        lds, s, fa);
     return launch_check("fcr_fwd_kernel");
 }
 
 template <int HS>
-int launch_fwd(const FwdArgs &fa, const Layout &L, hipStream_t s) {
-    return fa.cseq ? launch_fwd_t<HS, true>(fa, L, s) : launch_fwd_t<HS, false>(fa, L, s);
+int launch_fwd(const FwdArgs &fa, const Layout &L, bool lp, hipStream_t s) {
+    if (lp) return fa.cseq ? launch_fwd_t<HS, true, true>(fa, L, s) : launch_fwd_t<HS, false, true>(fa, L, s);
+    return fa.cseq ? launch_fwd_t<HS, true, false>(fa, L, s) : launch_fwd_t<HS, false, false>(fa, L, s);
 }
 
-template <int HS>
-int launch_bwd(const BwdArgs &ba, const Layout &L, hipStream_t s) {
+template <int HS, bool LP>
+int launch_bwd_t(const BwdArgs &ba, const Layout &L, hipStream_t s) {
     const int lds = BwdLds<HS>::BYTES;
     static bool attr_set = false;
     if (!attr_set) {
-        const hipError_t e = hipFuncSetAttribute((const void *)fcr_bwd_kernel<HS>,
+        const hipError_t e = hipFuncSetAttribute((const void *)fcr_bwd_kernel<HS, LP>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(bwd): %s", hipGetErrorString(e));
         attr_set = true;
     }
-    hipLaunchKernelGGL(fcr_bwd_kernel<HS>, dim3(L.nw_pad / kBwdWaves), dim3(kBwdWaves * kWave), lds, s, ba);
+    hipLaunchKernelGGL((fcr_bwd_kernel<HS, LP>), dim3(L.nw_pad / kBwdWaves), dim3(kBwdWaves * kWave), lds, s, ba);
     return launch_check("fcr_bwd_kernel");
+}
+
+template <int HS>
+int launch_bwd(const BwdArgs &ba, const Layout &L, bool lp, hipStream_t s) {
+    return lp ? launch_bwd_t<HS, true>(ba, L, s) : launch_bwd_t<HS, false>(ba, L, s);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -646,9 +656,9 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
     fa.stamp = (unsigned long long *)(base + L.stamp) + (size_t)L.nw_pad * 8;
 #endif
     switch (L.HS) {
-        case 4: rc = launch_fwd<4>(fa, L, s); break;
-        case 8: rc = launch_fwd<8>(fa, L, s); break;
-        case 13: rc = launch_fwd<13>(fa, L, s); break;
+        case 4: rc = launch_fwd<4>(fa, L, d->precision == FCR_PRECISION_F16, s); break;
+        case 8: rc = launch_fwd<8>(fa, L, d->precision == FCR_PRECISION_F16, s); break;
+        case 13: rc = launch_fwd<13>(fa, L, d->precision == FCR_PRECISION_F16, s); break;
         default: rc = fail(FCR_EUNSUPPORTED, "H=%d", d->H);
     }
     if (rc) return rc;
@@ -698,9 +708,9 @@ int fcr_backward(const fcr_dims *d, const float *X, const float *states, const f
 #endif
     ba.p = packed_ptrs(L, base);
     switch (L.HS) {
-        case 4: rc = launch_bwd<4>(ba, L, s); break;
-        case 8: rc = launch_bwd<8>(ba, L, s); break;
-        case 13: rc = launch_bwd<13>(ba, L, s); break;
+        case 4: rc = launch_bwd<4>(ba, L, d->precision == FCR_PRECISION_F16, s); break;
+        case 8: rc = launch_bwd<8>(ba, L, d->precision == FCR_PRECISION_F16, s); break;
+        case 13: rc = launch_bwd<13>(ba, L, d->precision == FCR_PRECISION_F16, s); break;
         default: rc = fail(FCR_EUNSUPPORTED, "H=%d", d->H);
     }
     if (rc) return rc;

@@ -102,7 +102,7 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 #endif
 }
 
-template <int HS, bool L0, bool DIN, bool FIRST, bool NX_L0, bool NX_HC, bool NX_DIN>
+template <int HS, bool L0, bool DIN, bool FIRST, bool NX_L0, bool NX_HC, bool NX_DIN, bool LP>
 __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, const float (&ext)[HS],
                                          float (&dh)[HS], float (&dc)[HS], float (&dxo)[HS], float &dxq,
                                          float &dx4, CellIn<HS> &ci, const NextIn &nx, Stamps &sp) {
@@ -136,7 +136,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     const float sg0 = up * kInvNegLog2e;   // dgate scale (the g row's -0.5 is applied per slot)
 
     // ---- the recomputation's B operands (this cell's x_t and h_{t-1}) ----
-    f16x8 bh[KB], bl[KB];
+    f16x8 bh[KB], bl[KB] = {};
     {
         float xv[HS], hv[HS];
 #pragma unroll
@@ -146,7 +146,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
         }
         const float x0 = ci.x[0][0], x1 = ci.x[0][1];
 #pragma unroll
-        for (int kb = KLO; kb < KHI; ++kb) fwd_operand<HS, L0, FIRST>(kb, x0, x1, xv, hv, bh[kb], bl[kb]);
+        for (int kb = KLO; kb < KHI; ++kb) fwd_operand<HS, L0, FIRST, LP>(kb, x0, x1, xv, hv, bh[kb], bl[kb]);
     }
     load_xhd<HS, NX_L0, NX_HC, NX_DIN>(ci, nx, lane);   // x, h, din of this cell are consumed
 
@@ -163,18 +163,23 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
         for (int kb = KLO; kb < KHI; ++kb) {
             const uint32_t a0 = (fb ^ (8u * (8 * kb))) + r * TILE, a1 = (fb ^ (8u * (8 * kb + 1))) + r * TILE;
             const uint32_t b0 = (fbl ^ (8u * (8 * kb))) + r * TILE, b1 = (fbl ^ (8u * (8 * kb + 1))) + r * TILE;
-            f16x8 ah, al;
+            f16x8 ah, al = {};
             const f16x4 h0 = lds_b64_f16(a0), h1 = lds_b64_f16(a1);
-            const f16x4 l0 = lds_b64_f16(b0), l1 = lds_b64_f16(b1);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 ah[k] = h0[k];
                 ah[4 + k] = h1[k];
-                al[k] = l0[k];
-                al[4 + k] = l1[k];
             }
-            if (((kb - KLO) & 1) == 0) a = mma3(ah, al, bh[kb], bl[kb], a);
-            else a2 = mma3(ah, al, bh[kb], bl[kb], a2);
+            if (!LP) {
+                const f16x4 l0 = lds_b64_f16(b0), l1 = lds_b64_f16(b1);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    al[k] = l0[k];
+                    al[4 + k] = l1[k];
+                }
+            }
+            if (((kb - KLO) & 1) == 0) a = mma_p<LP>(ah, al, bh[kb], bl[kb], a);
+            else a2 = mma_p<LP>(ah, al, bh[kb], bl[kb], a2);
         }
         if (KHI - KLO > 1) a += a2;
     };
@@ -213,7 +218,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
                 v[4 * u] = v[4 * u + 1] = v[4 * u + 2] = v[4 * u + 3] = 0.0f;
             }
         }
-        split8s(v, sg0, gh, gl);
+        split_p<LP>(v, sg0, gh, gl);
     };
 
     // Pipeline: region kbb issues the forward MFMAs of pair kbb+2, the transposed products of dgate
@@ -222,7 +227,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
 #pragma unroll
     for (int k = 0; k < NB; ++k) acc[k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     f32x4 fa[3][2];
-    f16x8 gh[2], gl[2];
+    f16x8 gh[2], gl[2] = {};
     fwd_pair(0, fa[0]);
     if (KBB > 1) fwd_pair(1, fa[1]);
     dgate_block(0, fa[0], gh[0], gl[0]);
@@ -241,11 +246,11 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
         for (int tau = 0; tau < NB; ++tau) {
             const uint32_t at = (tb ^ (8u * (8 * (tau >> 1) + (tau & 1)))) + 2 * kbb * TILE;
             f16x8 ah, al;
-            const f16x4 h0 = lds_tr_f16(at), l0 = lds_tr_f16(at + LO);
+            const f16x4 h0 = lds_tr_f16(at), l0 = LP ? f16x4{0, 0, 0, 0} : lds_tr_f16(at + LO);
             f16x4 h1 = {0, 0, 0, 0}, l1 = {0, 0, 0, 0};
             if (two) {
                 h1 = lds_tr_f16(at + TILE);
-                l1 = lds_tr_f16(at + TILE + LO);
+                if (!LP) l1 = lds_tr_f16(at + TILE + LO);
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -258,7 +263,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
             // of the cell (all fragments live at once); naming the accumulator keeps block kb-1's
             // MFMAs ahead of this point (issued ~NB*3 MFMAs ago: no hazard wait)
             if (kbb > 0) asm volatile("" : "+v"(acc[tau]));
-            acc[tau] = mma3(ah, al, gh[cu], gl[cu], acc[tau]);
+            acc[tau] = mma_p<LP>(ah, al, gh[cu], gl[cu], acc[tau]);
         }
         if (kbb + 1 < KBB) dgate_block(kbb + 1, fa[(kbb + 1) % 3], gh[nu], gl[nu]);
     }
@@ -293,7 +298,7 @@ struct BwdLds {
     static_assert(BYTES <= 163840, "weight images exceed the 160 KiB LDS");
 };
 
-template <int HS>
+template <int HS, bool LP>
 __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kernel(BwdArgs a) {
     using LD = BwdLds<HS>;
     using I1 = Img<HS, false>;
@@ -435,16 +440,16 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         for (int t = kL - 1; t >= 2; --t) {
 #pragma unroll
             for (int r = 0; r < HS; ++r) dab[r] = (t == kL - 1) ? dh_out[r] : 0.0f;
-            bwd_cell<HS, false, false, false, false, true, false>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
+            bwd_cell<HS, false, false, false, false, true, false, LP>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
                                                                 unused1, ci, next_of(j, 2, t), sp);
             store_quads<HS>(dseq_w + doff(j, 2, t), dxo, lane);
         }
 #pragma unroll
         for (int r = 0; r < HS; ++r) dab[r] = 0.0f;
-        bwd_cell<HS, false, false, false, false, false, false>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
+        bwd_cell<HS, false, false, false, false, false, false, LP>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
                                                              unused1, ci, next_of(j, 2, 1), sp);
         store_quads<HS>(dseq_w + doff(j, 2, 1), dxo, lane);
-        bwd_cell<HS, false, false, true, false, true, true>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
+        bwd_cell<HS, false, false, true, false, true, true, LP>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
                                                           unused1, ci, next_of(j, 2, 0), sp);
         store_quads<HS>(dseq_w + doff(j, 2, 0), dxo, lane);
         // ---- layer 1 ----
@@ -455,14 +460,14 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
 #pragma unroll
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
         for (int t = kL - 1; t >= 2; --t) {
-            bwd_cell<HS, false, true, false, false, true, true>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
+            bwd_cell<HS, false, true, false, false, true, true, LP>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
                                                               unused1, ci, next_of(j, 1, t), sp);
             store_quads<HS>(dseq_w + doff(j, 1, t), dxo, lane);
         }
-        bwd_cell<HS, false, true, false, false, false, true>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
+        bwd_cell<HS, false, true, false, false, false, true, LP>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
                                                            unused1, ci, next_of(j, 1, 1), sp);
         store_quads<HS>(dseq_w + doff(j, 1, 1), dxo, lane);
-        bwd_cell<HS, false, true, true, true, true, true>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
+        bwd_cell<HS, false, true, true, true, true, true, LP>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
                                                         unused1, ci, next_of(j, 1, 0), sp);
         store_quads<HS>(dseq_w + doff(j, 1, 0), dxo, lane);
         // ---- layer 0: dx -> window-row gradients ----
@@ -470,16 +475,16 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
         for (int t = kL - 1; t >= 2; --t) {
             float dxq, dx4;
-            bwd_cell<HS, true, true, false, true, true, true>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
+            bwd_cell<HS, true, true, false, true, true, true, LP>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
                                                             next_of(j, 0, t), sp);
             buf_st2(rr, lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{dxq, dx4});   // row j+t
         }
         {
             float dxq, dx4;
-            bwd_cell<HS, true, true, false, true, false, true>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
+            bwd_cell<HS, true, true, false, true, false, true, LP>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
                                                              next_of(j, 0, 1), sp);
             buf_st2(rr, lane * 8, (uint32_t)((j * kL + 1) * kWave * 8), f32x2{dxq, dx4});   // row j+1
-            bwd_cell<HS, true, true, true, false, true, false>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
+            bwd_cell<HS, true, true, true, false, true, false, LP>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
                                                              next_of(j, 0, 0), sp);
             buf_st2(rr, lane * 8, (uint32_t)((j * kL) * kWave * 8), f32x2{dxq, dx4});   // row j
         }

@@ -81,16 +81,44 @@ __device__ __forceinline__ void split8s(const float (&v)[8], float s, f16x8 &hi,
     lo = __builtin_bit_cast(f16x8, l);
 }
 
+// s·v -> hi = f16(s·v) only: the reduced-precision mode's operand (one product, no lo half)
+__device__ __forceinline__ void cvt8s(const float (&v)[8], float s, f16x8 &hi) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 h;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        unsigned hp;
+        asm("v_fma_mixlo_f16 %0, %1, %2, 0\n\t"
+            "v_fma_mixhi_f16 %0, %3, %2, 0"
+            : "=&v"(hp) : "v"(v[2 * p]), "v"(s), "v"(v[2 * p + 1]));
+        h[p] = hp;
+    }
+    hi = __builtin_bit_cast(f16x8, h);
+}
+
+// Precision modes (fcr_dims.precision): LP = false — fp32-accurate split products (three MFMAs);
+// LP = true — config 3's reduced-precision mode: f16 operands, ONE MFMA per product, fp32 accumulate
+template <bool LP>
+__device__ __forceinline__ void split_p(const float (&v)[8], float s, f16x8 &hi, f16x8 &lo) {
+    if (LP) cvt8s(v, s, hi);
+    else split8s(v, s, hi, lo);
+}
+
 // a·b with a = (ah, al), b = (bh, bl): small terms first, then the leading product
 __device__ __forceinline__ f32x4 mma3(f16x8 ah, f16x8 al, f16x8 bh, f16x8 bl, f32x4 acc) {
     acc = mfma16(al, bh, acc);
     acc = mfma16(ah, bl, acc);
     return mfma16(ah, bh, acc);
 }
+template <bool LP>
+__device__ __forceinline__ f32x4 mma_p(f16x8 ah, f16x8 al, f16x8 bh, f16x8 bl, f32x4 acc) {
+    if (LP) return mfma16(ah, bh, acc);
+    return mma3(ah, al, bh, bl, acc);
+}
 
 // B operand (8 combined slots of k-block kb) of a forward cell, from the lane's own registers.
 // FIRST: h_{t-1} = 0. Identical in the forward kernel and the backward's recomputation.
-template <int HS, bool L0, bool FIRST>
+template <int HS, bool L0, bool FIRST, bool LP>
 __device__ __forceinline__ void fwd_operand(int kb, float x0, float x1, const float (&x)[HS],
                                             const float (&hp)[HS], f16x8 &bh, f16x8 &bl) {
     float v[8];
@@ -108,7 +136,7 @@ __device__ __forceinline__ void fwd_operand(int kb, float x0, float x1, const fl
         }
         v[j] = e;
     }
-    split8s(v, 1.0f, bh, bl);
+    split_p<LP>(v, 1.0f, bh, bl);
 }
 
 // Cell update of one unit slot from its pre-activations a = (i, f, g, o), pre-scaled for exp2 (the

@@ -30,7 +30,7 @@ __device__ __forceinline__ void rot_left(float (&w)[kL]) {
 #ifndef FCR_FWD_PRIO
 #define FCR_FWD_PRIO 1
 #endif
-template <int HS, bool L0, bool FIRST>
+template <int HS, bool L0, bool FIRST, bool LP>
 __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lane, float x0, float x1,
                                            const float (&x)[HS], const float (&hp)[HS], float (&c)[HS],
                                            float (&hout)[HS], unsigned &turn) {
@@ -45,15 +45,15 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
     constexpr int KLO = (L0 && FIRST) ? G::XBLK : 0;
     constexpr int KHI = FIRST ? (L0 ? G::XBLK + 1 : G::KX1) : KB;
     constexpr int NP = (HS + 1) / 2;   // tile pairs
-    f16x8 bh[KB], bl[KB];
+    f16x8 bh[KB], bl[KB] = {};
 #pragma unroll
-    for (int kb = KLO; kb < KHI; ++kb) fwd_operand<HS, L0, FIRST>(kb, x0, x1, x, hp, bh[kb], bl[kb]);
+    for (int kb = KLO; kb < KHI; ++kb) fwd_operand<HS, L0, FIRST, LP>(kb, x0, x1, x, hp, bh[kb], bl[kb]);
     // fragment reads of (tile r, block kb): hi, lo
     auto rd = [&](int r, int kb, f16x8 &h, f16x8 &l) {
         h = lds_frag16(lw, (r * KB + kb) * 2, lane);
-        l = lds_frag16(lw, (r * KB + kb) * 2 + 1, lane);
+        if (!LP) l = lds_frag16(lw, (r * KB + kb) * 2 + 1, lane);
     };
-    f16x8 ah[2], al[2];
+    f16x8 ah[2], al[2] = {};
     rd(0, KLO, ah[0], al[0]);
     if (HS > 1) rd(1, KLO, ah[1], al[1]);
     f32x4 prev[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
@@ -77,8 +77,8 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
                 if (r1 + 2 < HS) rd(r1 + 2, KLO, nh[1], nl[1]);
             }
             const int ch = (kb - KLO) & 1;
-            acc[0][ch] = mma3(ah[0], al[0], bh[kb], bl[kb], acc[0][ch]);
-            if (two) acc[1][ch] = mma3(ah[1], al[1], bh[kb], bl[kb], acc[1][ch]);
+            acc[0][ch] = mma_p<LP>(ah[0], al[0], bh[kb], bl[kb], acc[0][ch]);
+            if (two) acc[1][ch] = mma_p<LP>(ah[1], al[1], bh[kb], bl[kb], acc[1][ch]);
             if (kb == KLO && p > 0) {
                 lstm_point<FIRST>(prev[0], c[r0 - 2], c[r0 - 2], hout[r0 - 2]);
                 lstm_point<FIRST>(prev[1], c[r1 - 2], c[r1 - 2], hout[r1 - 2]);
@@ -108,7 +108,7 @@ __device__ __forceinline__ unsigned long long fstamp() {
 #endif
 }
 
-template <int HS, bool STORE>
+template <int HS, bool STORE, bool LP>
 __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kernel(FwdArgs a) {
     using G = Geo16<HS>;
     extern __shared__ __attribute__((aligned(16))) float lw[];
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             const float x0 = w0[0], x1 = w1[0];
             rot_left(w0);
             rot_left(w1);
-            fwd16_cell<HS, true, true>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
+            fwd16_cell<HS, true, true, LP>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
             store_quads<HS>(SEQ_H(0, 0), hout, lane);
             if (STORE) {
                 xw_wave[(size_t)j * kL * kWave + lane] = f32x2{x0, x1};
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             const float x0 = w0[0], x1 = w1[0];
             rot_left(w0);
             rot_left(w1);
-            fwd16_cell<HS, true, false>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
+            fwd16_cell<HS, true, false, LP>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
             store_quads<HS>(SEQ_H(0, t), hout, lane);
             if (STORE) {
                 xw_wave[((size_t)j * kL + t) * kWave + lane] = f32x2{x0, x1};
@@ -224,7 +224,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             stagger();
             load_quads<HS>(xc, SEQ_H(l - 1, 0), lane);
             load_quads<HS>(xn, SEQ_H(l - 1, 1), lane);
-            fwd16_cell<HS, false, true>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
+            fwd16_cell<HS, false, true, LP>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
             if (keep_h) store_quads<HS>(SEQ_H(l, 0), hout, lane);
             if (STORE) store_quads<HS>(SEQ_C(l, 0), c, lane);
 #pragma unroll
@@ -234,7 +234,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             }
             for (int t = 1; t < kL; ++t) {
                 load_quads<HS>(xn, SEQ_H(l - 1, t + 1 < kL ? t + 1 : t), lane);
-                fwd16_cell<HS, false, false>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
+                fwd16_cell<HS, false, false, LP>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
                 if (keep_h && !(l == 2 && t + 1 == kL)) store_quads<HS>(SEQ_H(l, t), hout, lane);
                 if (STORE && t + 1 < kL) store_quads<HS>(SEQ_C(l, t), c, lane);
 #pragma unroll

@@ -105,10 +105,11 @@ class MPCLoss(nn.Module):
     passed instead. After each call ``self.last_trajectory`` holds the (B, N, 4) LSTM predictions.
     """
 
-    def __init__(self, prediction_horizon=10, alpha=0.1):
+    def __init__(self, prediction_horizon=10, alpha=0.1, precision="fp32"):
         super().__init__()
         self.N = prediction_horizon
         self.alpha = alpha
+        self.precision = precision     # "fp32" (reference-accurate) or "f16" (config 3, include/fcr.h)
         self.activation = nn.ReLU()
         self.last_trajectory = None
 
@@ -126,7 +127,7 @@ class MPCLoss(nn.Module):
             noise = None
         loss, cost, command, error, prediction, xhat = rollout(
             X, output_controller, states, _controller_params(controller), _simulator_params(simulator),
-            self.N, self.alpha, noise)
+            self.N, self.alpha, noise, self.precision)
         self.last_trajectory = xhat
         return loss, {"loss": cost, "command": command, "error": error, "prediction": prediction}
 

@@ -25,8 +25,8 @@ def _stream(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
-def make_dims(B, N, H, layers, ctrl_hidden, alpha, in_dim=5, out_dim=4, ctrl_in=3, L=WINDOW_ROWS):
-    return _native.FcrDims(B, N, L, H, layers, in_dim, out_dim, ctrl_in, ctrl_hidden, float(alpha))
+def make_dims(B, N, H, layers, ctrl_hidden, alpha, in_dim=5, out_dim=4, ctrl_in=3, L=WINDOW_ROWS, precision=0):
+    return _native.FcrDims(B, N, L, H, layers, in_dim, out_dim, ctrl_in, ctrl_hidden, float(alpha), int(precision))
 
 
 def _dev_f32(t, name):
@@ -42,12 +42,12 @@ class RolloutFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, X, u0, states, noise, W_inp, b_inp, W_out, w_ih0, w_ih1, w_ih2, w_hh0, w_hh1,
-                w_hh2, fc_w, fc_b, N, alpha):
+                w_hh2, fc_w, fc_b, N, alpha, precision=0):
         lib = _native.load()
         dev = X.device
         B = X.shape[0]
         H = w_hh0.shape[1]
-        dims = make_dims(B, N, H, 3, W_inp.shape[0], alpha)
+        dims = make_dims(B, N, H, 3, W_inp.shape[0], alpha, precision=precision)
         need_grad = any(ctx.needs_input_grad[i] for i in (1, 4, 5, 6))
         ws = torch.empty(_native.workspace_bytes(dims, need_grad), dtype=torch.uint8, device=dev)
         f32 = dict(dtype=torch.float32, device=dev)
@@ -96,11 +96,18 @@ class RolloutFn(torch.autograd.Function):
                                        _ptr(g_u0), _ptr(g_wi), _ptr(g_bi), _ptr(g_wo), _ptr(ctx.ws),
                                        ctx.ws.numel(), _stream(dev)), "fcr_backward")
         ctx.ws = None   # release the activation slab as early as autograd lets us
-        return (None, g_u0, None, None, g_wi, g_bi, g_wo) + (None,) * 10
+        return (None, g_u0, None, None, g_wi, g_bi, g_wo) + (None,) * 11
 
 
-def rollout(X, u0, states, ctrl_params, lstm_params, N, alpha, noise=None):
-    """Functional entry: ctrl_params = (W_inp, b_inp, W_out), lstm_params = (w_ih[3], w_hh[3], fc_w, fc_b)."""
+PRECISIONS = {"fp32": _native.PRECISION_FP32, "f16": _native.PRECISION_F16}
+
+
+def rollout(X, u0, states, ctrl_params, lstm_params, N, alpha, noise=None, precision="fp32"):
+    """Functional entry: ctrl_params = (W_inp, b_inp, W_out), lstm_params = (w_ih[3], w_hh[3], fc_w, fc_b).
+    precision: "fp32" (fp32-accurate, the default) or "f16" (config 3's reduced-precision gate products,
+    include/fcr.h FCR_PRECISION_F16)."""
+    if precision not in PRECISIONS:
+        raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {precision!r}")
     w_ih, w_hh, fc_w, fc_b = lstm_params
     dev = X.device
     if dev.type != "cuda":
@@ -122,4 +129,4 @@ def rollout(X, u0, states, ctrl_params, lstm_params, N, alpha, noise=None):
                            None if noise is None else _dev_f32(noise, "noise"),
                            *[_dev_f32(t, "controller param") for t in ctrl_params],
                            *[_dev_f32(t, "lstm weight") for t in list(w_ih) + list(w_hh) + [fc_w, fc_b]],
-                           int(N), float(alpha))
+                           int(N), float(alpha), PRECISIONS[precision])

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define FCR_ABI_VERSION 1
+#define FCR_ABI_VERSION 2
 
 enum {
     FCR_OK = 0,
@@ -54,7 +54,18 @@ typedef struct fcr_dims {
     int32_t ctrl_in;     /* controller inputs (must be 3)                     */
     int32_t ctrl_hidden; /* controller hidden units (<= 52)                   */
     float alpha;         /* MPCLoss.alpha, command-variation weight            */
+    int32_t precision;   /* FCR_PRECISION_FP32 (0) or FCR_PRECISION_F16 (1), below */
 } fcr_dims;
+
+/* Arithmetic of the gate products (fcr_forward/fcr_backward; fcr_lstm_* ignore it and run fp32):
+ *   FCR_PRECISION_FP32 — fp32-accurate: each operand split into two f16 halves, three f16 MFMAs per
+ *                        product, fp32 accumulate (results within 1e-5 of an fp64 evaluation);
+ *   FCR_PRECISION_F16  — config 3's reduced-precision mode ("bf16 storage/MFMA fwd"):
+ *                        f16 operands (11-bit significand, more than bf16's 8; the backward's per-trajectory
+ *                        power-of-two scaling keeps them in range), one MFMA per product, fp32 accumulate;
+ *                        H <= 52 only. Both calls of one step must use the same precision. */
+#define FCR_PRECISION_FP32 0
+#define FCR_PRECISION_F16 1
 
 /* Weights, torch layouts (row-major, as state_dict holds them). */
 typedef struct fcr_weights {

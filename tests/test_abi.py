@@ -41,9 +41,10 @@ def test_abi_version():
 
 
 def dims(**kw):
-    base = dict(B=65536, N=10, H=50, layers=3, ctrl_hidden=50, alpha=20.0)
+    base = dict(B=65536, N=10, H=50, layers=3, ctrl_hidden=50, alpha=20.0, precision=0)
     base.update(kw)
-    return fca.rollout.make_dims(base["B"], base["N"], base["H"], base["layers"], base["ctrl_hidden"], base["alpha"])
+    return fca.rollout.make_dims(base["B"], base["N"], base["H"], base["layers"], base["ctrl_hidden"], base["alpha"],
+                                 precision=base["precision"])
 
 
 def test_workspace_size_scales_with_batch_and_backward():
@@ -58,6 +59,7 @@ def test_workspace_size_scales_with_batch_and_backward():
 
 @pytest.mark.parametrize("kw,code", [
     (dict(B=0), -1), (dict(N=0), -1), (dict(H=4096), -4), (dict(H=0), -4), (dict(layers=2), -4), (dict(ctrl_hidden=80), -4),
+    (dict(precision=2), -1), (dict(precision=1, H=64), -4),
 ])
 def test_invalid_dims_rejected_with_message(kw, code):
     lib = fca._native.load()
