@@ -51,7 +51,9 @@ def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
     (profiles/r*_pmc.json, collected by scripts/profile.sh on this workload), or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    import re
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json"))
+                   if re.fullmatch(r"r\d+_pmc\.json", os.path.basename(f)))   # the rollout's, not the plant's
     if not files:
         return None, None
     d = json.load(open(files[-1]))
