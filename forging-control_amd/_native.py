@@ -20,7 +20,7 @@ ERRORS = {-1: "FCR_EINVAL", -2: "FCR_EWORKSPACE", -3: "FCR_EHIP", -4: "FCR_EUNSU
 
 # Every symbol include/fcr.h declares (tests check the .so exports exactly these).
 EXPORTS = ("fcr_workspace_size", "fcr_forward", "fcr_backward", "fcr_lstm_workspace_size", "fcr_lstm_forward",
-           "fcr_lstm_backward", "fcr_plant_rk4", "fcr_window_gather", "fcr_last_error", "fcr_abi_version")
+           "fcr_lstm_backward", "fcr_plant_rk4", "fcr_closed_loop_run", "fcr_window_gather", "fcr_last_error", "fcr_abi_version")
 
 
 class FcrDims(ctypes.Structure):
@@ -45,6 +45,18 @@ class FcrWindows(ctypes.Structure):
         ("rows", ctypes.c_int64), ("traj_len", ctypes.c_int32), ("lookback", ctypes.c_int32),
         ("nx", ctypes.c_int32), ("ny", ctypes.c_int32), ("nz", ctypes.c_int32),
         ("X", ctypes.c_void_p), ("Y", ctypes.c_void_p), ("Z", ctypes.c_void_p),
+    ]
+
+
+class FcrClosedLoop(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int32), ("T", ctypes.c_int32), ("ts", ctypes.c_double),
+        ("substeps", ctypes.c_int32), ("smooth", ctypes.c_int32),
+        ("x0", ctypes.c_void_p), ("ref", ctypes.c_void_p),
+        ("ctrl_w_inp", ctypes.c_void_p), ("ctrl_b_inp", ctypes.c_void_p), ("ctrl_w_out", ctypes.c_void_p),
+        ("ctrl_hidden", ctypes.c_int32), ("in_scale", ctypes.c_double * 2),
+        ("ref_scale", ctypes.c_double), ("out_scale", ctypes.c_double),
+        ("x", ctypes.c_void_p), ("u", ctypes.c_void_p),
     ]
 
 
@@ -84,6 +96,8 @@ def load() -> ctypes.CDLL:
         lib.fcr_lstm_backward.argtypes = [ctypes.POINTER(FcrDims), ctypes.POINTER(FcrWeights), vp,
                                           ctypes.POINTER(vp), ctypes.POINTER(vp), vp, vp, vp, vp, sz, vp]
         lib.fcr_lstm_backward.restype = i32
+        lib.fcr_closed_loop_run.argtypes = [ctypes.POINTER(FcrClosedLoop), vp]
+        lib.fcr_closed_loop_run.restype = i32
         lib.fcr_window_gather.argtypes = [ctypes.POINTER(FcrWindows), i32, vp, vp, vp, vp, vp, vp]
         lib.fcr_window_gather.restype = i32
         lib.fcr_last_error.argtypes = []

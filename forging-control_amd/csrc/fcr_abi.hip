@@ -16,6 +16,7 @@
 #include "fcr_img.h"
 #include "fcr_pack.h"
 #include "fcr_plant.h"
+#include "fcr_closed_loop.h"
 #include "fcr_surrogate.h"
 #include "fcr_window.h"
 #include "fcr_wide.h"
@@ -869,6 +870,34 @@ int fcr_lstm_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, 
         if ((rc = launch_check("window_transpose_kernel"))) return rc;
     }
     return FCR_OK;
+}
+
+int fcr_closed_loop_run(const fcr_closed_loop *c, void *stream) {
+    if (!c) return fail(FCR_EINVAL, "fcr_closed_loop_run: args is NULL");
+    if (c->B < 0 || c->T < 0) return fail(FCR_EINVAL, "fcr_closed_loop_run: B=%d, T=%d must be >= 0", c->B, c->T);
+    if (c->substeps < 1 || c->substeps > 4096) return fail(FCR_EINVAL, "fcr_closed_loop_run: substeps=%d must be 1..4096", c->substeps);
+    if (!(c->ts > 0.0) || c->ts > 1e6) return fail(FCR_EINVAL, "fcr_closed_loop_run: ts=%g must be a positive time step", c->ts);
+    if (c->smooth != 0 && c->smooth != 1) return fail(FCR_EINVAL, "fcr_closed_loop_run: smooth=%d must be 0 or 1", c->smooth);
+    if (c->ctrl_hidden < 1 || c->ctrl_hidden > closed_loop::kClMaxHidden)
+        return fail(FCR_EUNSUPPORTED, "fcr_closed_loop_run: ctrl_hidden=%d: built for 1..%d", c->ctrl_hidden,
+                    closed_loop::kClMaxHidden);
+    if (!(c->in_scale[0] > 0.0) || !(c->in_scale[1] > 0.0) || !(c->ref_scale > 0.0) || !(c->out_scale > 0.0))
+        return fail(FCR_EINVAL, "fcr_closed_loop_run: scaler scales must be positive");
+    if (c->B == 0) return FCR_OK;
+    if (!c->x0 || !c->x || !c->ctrl_w_inp || !c->ctrl_b_inp || !c->ctrl_w_out || (c->T > 0 && (!c->ref || !c->u)))
+        return fail(FCR_EINVAL, "fcr_closed_loop_run: a required pointer is NULL");
+    if ((((uintptr_t)c->x0) | ((uintptr_t)c->ref) | ((uintptr_t)c->x) | ((uintptr_t)c->u)) & 7)
+        return fail(FCR_EINVAL, "fcr_closed_loop_run: fp64 buffers must be 8-byte aligned");
+    closed_loop::ClArgs a{c->B, c->T, c->substeps, c->ctrl_hidden, c->ts / c->substeps, c->x0, c->ref,
+                          c->ctrl_w_inp, c->ctrl_b_inp, c->ctrl_w_out, c->in_scale[0], c->in_scale[1],
+                          c->ref_scale, c->out_scale, c->x, c->u};
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 grid((c->B + closed_loop::kClBlock - 1) / closed_loop::kClBlock);
+    if (c->smooth)
+        hipLaunchKernelGGL(closed_loop::closed_loop_kernel<true>, grid, dim3(closed_loop::kClBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL(closed_loop::closed_loop_kernel<false>, grid, dim3(closed_loop::kClBlock), 0, s, a);
+    return launch_check("closed_loop_kernel");
 }
 
 }  // extern "C"

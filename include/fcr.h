@@ -130,6 +130,30 @@ int fcr_plant_rk4(int32_t B, int32_t S, double ts, int32_t substeps, int32_t smo
                   const double *x0, const double *u, double *x, void *stream);
 
 /*
+ * Batched closed-loop evaluation (SURVEY.md §8(f) ranks 1 + 2): NeuralNetwork.loop (Functions.py:
+ * 1075-1240) without feasibility recovery — per step the FNN controller on the MaxAbs-scaled
+ * [y_dot, z, ref] (NN_make_step, :1560-1613; fp32 like torch) and the press advanced by the RK4
+ * integrator of fcr_plant_rk4 (in place of do-mpc's CVODES) — for B trajectories × T steps, one launch.
+ *   x0 (B,5), ref (B,T) unscaled speed references (NeuralNetwork.tvp_fun, :926-966, computed by the
+ *   caller); controller weights as fcr_weights; in_scale = scalers['input'].scale_[0:2] (y_dot, z),
+ *   ref_scale = scalers['y_dot'].scale_, out_scale = scalers['output'].scale_ (UL/Main.py:237-256);
+ *   outputs x (B,T+1,5) with x[:,0] = x0 and u (B,T) the commands applied. fp64 buffers, fp32 weights.
+ */
+typedef struct fcr_closed_loop {
+    int32_t B, T;
+    double ts;
+    int32_t substeps, smooth;
+    const double *x0, *ref;
+    const float *ctrl_w_inp, *ctrl_b_inp, *ctrl_w_out;
+    int32_t ctrl_hidden;
+    double in_scale[2];
+    double ref_scale, out_scale;
+    double *x, *u;
+} fcr_closed_loop;
+
+int fcr_closed_loop_run(const fcr_closed_loop *args, void *stream);
+
+/*
  * Training-sample windows: the tables of the concatenated per-trajectory
  * SequenceDatasets (Functions.py:92-132, built by Data.get_individual_dataset :479-516 and
  * ConcatDataset, UL/Main.py:270-279), resident in device memory.
