@@ -122,18 +122,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     constexpr int KLO = (L0 && FIRST) ? G::XBLK : 0;
     constexpr int KHI = FIRST ? (L0 ? G::XBLK + 1 : G::KX1) : KB;
 
-    // ---- incoming dh, and the trajectory's power-of-two scale ----
-    float m = 0.0f;
-#pragma unroll
-    for (int r = 0; r < HS; ++r) {
-        dh[r] += DIN ? ci.d[r >> 2][r & 3] : ext[r];
-        m = fmaxf(m, fabsf(dh[r]) + fabsf(dc[r]));
-    }
-    m = fmaxf(m, __shfl_xor(m, 16));
-    m = fmaxf(m, __shfl_xor(m, 32));
-    const int e = max(__builtin_amdgcn_frexp_expf(m), -100);   // m < 2^e; all-zero -> e = 0
-    const float up = __builtin_amdgcn_ldexpf(1.0f, 13 - e), down = __builtin_amdgcn_ldexpf(1.0f, e - 13);
-    const float sg0 = up * kInvNegLog2e;   // dgate scale (the g row's -0.5 is applied per slot)
+    float up, down, sg0;   // the trajectory's power-of-two scale, set once the incoming dh is in
 
     // ---- the recomputation's B operands (this cell's x_t and h_{t-1}) ----
     f16x8 bh[KB], bl[KB] = {};
@@ -148,7 +137,6 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
 #pragma unroll
         for (int kb = KLO; kb < KHI; ++kb) fwd_operand<HS, L0, FIRST, LP>(kb, x0, x1, xv, hv, bh[kb], bl[kb]);
     }
-    load_xhd<HS, NX_L0, NX_HC, NX_DIN>(ci, nx, lane);   // x, h, din of this cell are consumed
 
     // Recomputed forward tile r: its MFMA chain, issued two regions before its result is used (two
     // accumulators over alternate k-blocks halve the dependent-MFMA chain).
@@ -230,6 +218,23 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     f16x8 gh[2], gl[2] = {};
     fwd_pair(0, fa[0]);
     if (KBB > 1) fwd_pair(1, fa[1]);
+    // ---- incoming dh, and the trajectory's power-of-two scale: issued behind the first forward MFMAs,
+    // which only need this cell's (prefetched) inputs, so the previous cell's tail overlaps them ----
+    {
+        float m = 0.0f;
+#pragma unroll
+        for (int r = 0; r < HS; ++r) {
+            dh[r] += DIN ? ci.d[r >> 2][r & 3] : ext[r];
+            m = fmaxf(m, fabsf(dh[r]) + fabsf(dc[r]));
+        }
+        m = fmaxf(m, __shfl_xor(m, 16));
+        m = fmaxf(m, __shfl_xor(m, 32));
+        const int e = max(__builtin_amdgcn_frexp_expf(m), -100);   // m < 2^e; all-zero -> e = 0
+        up = __builtin_amdgcn_ldexpf(1.0f, 13 - e);
+        down = __builtin_amdgcn_ldexpf(1.0f, e - 13);
+        sg0 = up * kInvNegLog2e;   // dgate scale (the g row's -0.5 is applied per slot)
+    }
+    load_xhd<HS, NX_L0, NX_HC, NX_DIN>(ci, nx, lane);   // x, h, din of this cell are consumed
     dgate_block(0, fa[0], gh[0], gl[0]);
     const unsigned long long t1 = stamp_now();
 #pragma unroll
