@@ -133,7 +133,7 @@ int launch_check(const char *what) {
 
 template <int HS, bool STORE, bool LP>
 int launch_fwd_t(const FwdArgs &fa, const Layout &L, hipStream_t s) {
-    const int lds = Geo16<HS>::LDS_FWD;
+    const int lds = LP ? Geo16<HS>::LDS_FWD_LP : Geo16<HS>::LDS_FWD;
     static bool attr_set = false;
     if (!attr_set) {
         const hipError_t e = hipFuncSetAttribute((const void *)fcr_fwd_kernel<HS, STORE, LP>,
@@ -154,7 +154,7 @@ int launch_fwd(const FwdArgs &fa, const Layout &L, bool lp, hipStream_t s) {
 
 template <int HS, bool LP>
 int launch_bwd_t(const BwdArgs &ba, const Layout &L, hipStream_t s) {
-    const int lds = BwdLds<HS>::BYTES;
+    const int lds = BwdLds<HS, LP>::BYTES;
     static bool attr_set = false;
     if (!attr_set) {
         const hipError_t e = hipFuncSetAttribute((const void *)fcr_bwd_kernel<HS, LP>,

@@ -295,23 +295,32 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     }
 }
 
-template <int HS>
+// fp32 mode: [layer 2|1 image (hi, lo), refilled per phase | layer-0 image | misc];
+// f16 mode:  [layer 2 hi | layer 1 hi | layer 0 hi | misc], all resident (no refills)
+template <int HS, bool LP>
 struct BwdLds {
-    static constexpr int IMG1 = Img<HS, false>::BYTES, IMG0 = Img<HS, true>::BYTES;
+    static constexpr int IMG1 = LP ? Img<HS, false>::BYTES / 2 : Img<HS, false>::BYTES;
+    static constexpr int IMG0 = LP ? Img<HS, true>::BYTES / 2 : Img<HS, true>::BYTES;
+    static constexpr int NIMG1 = LP ? 2 : 1;
     static constexpr int FNP = kMS * 4 * kFnpStride, FCP = kOut * HS * 4;
-    static constexpr int BYTES = IMG1 + IMG0 + (FNP + FCP) * 4;
+    static constexpr int BYTES = NIMG1 * IMG1 + IMG0 + (FNP + FCP) * 4;
     static_assert(BYTES <= 163840, "weight images exceed the 160 KiB LDS");
 };
 
 template <int HS, bool LP>
 __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kernel(BwdArgs a) {
-    using LD = BwdLds<HS>;
+    using LD = BwdLds<HS, LP>;
     using I1 = Img<HS, false>;
     using I0 = Img<HS, true>;
     extern __shared__ __attribute__((aligned(16))) float lw[];
-    float *lw0 = lw + LD::IMG1 / 4;             // resident layer-0 image
+    float *lw1 = lw + (LP ? LD::IMG1 / 4 : 0);  // layer-1 image (f16 mode: resident beside layer 2's)
+    float *lw0 = lw + LD::NIMG1 * LD::IMG1 / 4; // resident layer-0 image
     float *lfnp = lw0 + LD::IMG0 / 4;           // resident controller records
     float *lfcp = lfnp + LD::FNP;               // resident fc.weight (lane layout)
+    if (LP) {
+        lds_copy(lw, a.p.img[2], LD::IMG1 / 4);     // hi images only: the first half of each
+        lds_copy(lw1, a.p.img[1], LD::IMG1 / 4);
+    }
     lds_copy(lw0, a.p.img[0], LD::IMG0 / 4);
     lds_copy(lfnp, a.p.fnp, LD::FNP);
     lds_copy(lfcp, a.p.fcp, LD::FCP);
@@ -330,7 +339,8 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
     const float s84 = a.states[(size_t)bc * kL * kIn + (kL - 2) * kIn + 4];
     const float *pred = a.prediction + (size_t)bc * N;
     const float *xh = a.xhat + (size_t)bc * N * kOut;
-    const ImgLane<I1::RB> L1 = img_lane<I1::RB>(lds_offset(lw), lane);
+    const ImgLane<I1::RB> L1 = img_lane<I1::RB>(lds_offset(lw), lane);      // layer 2 (fp32: layers 2, 1)
+    const ImgLane<I1::RB> L1b = img_lane<I1::RB>(lds_offset(lw1), lane);    // layer 1
     const ImgLane<I0::RB> L0 = img_lane<I0::RB>(lds_offset(lw0), lane);
 
     // window-row gradients dx(w, t) (lane group q: column q; lane group 0 also column 4) go to a
@@ -431,8 +441,10 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         }
         float unused0, unused1;
         const unsigned long long tw1 = stamp_now();
-        lds_fill<LD::IMG1, kBwdWaves>(lw, a.p.img[2]);
-        stagger();
+        if (!LP) {
+            lds_fill<LD::IMG1, kBwdWaves>(lw, a.p.img[2]);
+            stagger();
+        }
         if (FCR_STAMP) {
             const unsigned long long tw2 = stamp_now();
             sp.t[5] += tw1 - tw0;
@@ -459,20 +471,22 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         store_quads<HS>(dseq_w + doff(j, 2, 0), dxo, lane);
         // ---- layer 1 ----
         const unsigned long long tw3 = stamp_now();
-        lds_fill<LD::IMG1, kBwdWaves>(lw, a.p.img[1]);
-        stagger();
+        if (!LP) {
+            lds_fill<LD::IMG1, kBwdWaves>(lw, a.p.img[1]);
+            stagger();
+        }
         if (FCR_STAMP) sp.t[7] += stamp_now() - tw3;
 #pragma unroll
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
         for (int t = kL - 1; t >= 2; --t) {
-            bwd_cell<HS, false, true, false, false, true, true, LP>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
+            bwd_cell<HS, false, true, false, false, true, true, LP>(L1b.fb, L1b.tb, lane, dab, dh, dc, dxo, unused0,
                                                               unused1, ci, next_of(j, 1, t), sp);
             store_quads<HS>(dseq_w + doff(j, 1, t), dxo, lane);
         }
-        bwd_cell<HS, false, true, false, false, false, true, LP>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
+        bwd_cell<HS, false, true, false, false, false, true, LP>(L1b.fb, L1b.tb, lane, dab, dh, dc, dxo, unused0,
                                                            unused1, ci, next_of(j, 1, 1), sp);
         store_quads<HS>(dseq_w + doff(j, 1, 1), dxo, lane);
-        bwd_cell<HS, false, true, true, true, true, true, LP>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
+        bwd_cell<HS, false, true, true, true, true, true, LP>(L1b.fb, L1b.tb, lane, dab, dh, dc, dxo, unused0,
                                                         unused1, ci, next_of(j, 1, 0), sp);
         store_quads<HS>(dseq_w + doff(j, 1, 0), dxo, lane);
         // ---- layer 0: dx -> window-row gradients ----

@@ -36,7 +36,9 @@ struct Geo16 {
     static constexpr int FCP = kOut * HS * 4;
     static constexpr int MISC = FNP + FCP + 4;
     static constexpr int LDS_FWD = (FA1 + FA0 + MISC) * 4;   // bytes
-    static_assert(LDS_FWD <= 163840, "fragments exceed the 160 KiB LDS");
+    // f16 mode: the hi fragments of all three layers stay resident (no per-phase refills)
+    static constexpr int LDS_FWD_LP = (FA1 + FA0 / 2 + MISC) * 4;
+    static_assert(LDS_FWD <= 163840 && LDS_FWD_LP <= 163840, "fragments exceed the 160 KiB LDS");
     static_assert((HS & 7) + 1 < 8, "window columns must share one k-block");
 };
 
@@ -175,7 +177,7 @@ inline size_t f16_fwd_bytes(int HS, int l) {
     return (size_t)HS * KB * 2 * kWave * 16;
 }
 
-// Forward fragments, f16 split: element (r, kb, split, lane, j) = hi|lo of A[rho][k] with rho = lane&15
+// Forward fragments, f16 split: element (split, r, kb, lane, j) = hi|lo of A[rho][k] with rho = lane&15
 // -> unit 4r+(rho>>2), gate rho&3 (torch row gate*H + unit), k = combined slot 8kb+j of lane group
 // lane>>4 (see the header). Scaled for exp2 as the pointwise expects.
 __global__ void pack_fwd16_kernel(PackArgs a, int l, _Float16 *dst) {
@@ -212,9 +214,10 @@ __global__ void pack_fwd16_kernel(PackArgs a, int l, _Float16 *dst) {
     v *= (gate == 2 ? kTwoLog2e : kNegLog2e);
     const _Float16 hi = (_Float16)v;
     const _Float16 lo = (_Float16)(v - (float)hi);
-    const size_t frag = (size_t)rk * 2;
-    dst[(frag * kWave + lane) * 8 + j] = hi;
-    dst[((frag + 1) * kWave + lane) * 8 + j] = lo;
+    // split-major: every hi fragment of the layer, then every lo one (the f16 mode reads the first half)
+    const size_t nq = (size_t)HS * KB;
+    dst[((size_t)rk * kWave + lane) * 8 + j] = hi;
+    dst[((nq + rk) * kWave + lane) * 8 + j] = lo;
 }
 
 }  // namespace fcr

@@ -49,9 +49,9 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
 #pragma unroll
     for (int kb = KLO; kb < KHI; ++kb) fwd_operand<HS, L0, FIRST, LP>(kb, x0, x1, x, hp, bh[kb], bl[kb]);
     // fragment reads of (tile r, block kb): hi, lo
-    auto rd = [&](int r, int kb, f16x8 &h, f16x8 &l) {
-        h = lds_frag16(lw, (r * KB + kb) * 2, lane);
-        if (!LP) l = lds_frag16(lw, (r * KB + kb) * 2 + 1, lane);
+    auto rd = [&](int r, int kb, f16x8 &h, f16x8 &l) {   // split-major fragments (pack_fwd16_kernel)
+        h = lds_frag16(lw, r * KB + kb, lane);
+        if (!LP) l = lds_frag16(lw, HS * KB + r * KB + kb, lane);
     };
     f16x8 ah[2], al[2] = {};
     rd(0, KLO, ah[0], al[0]);
@@ -112,11 +112,19 @@ template <int HS, bool STORE, bool LP>
 __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kernel(FwdArgs a) {
     using G = Geo16<HS>;
     extern __shared__ __attribute__((aligned(16))) float lw[];
+    // fp32 mode: [layer 1|2 fragments, refilled per phase | layer 0 | misc];
+    // f16 mode:  [layer 1 hi | layer 2 hi | layer 0 hi | misc], all resident
+    constexpr int F0 = LP ? G::FA0 / 2 : G::FA0;
     float *lw0 = lw + G::FA1;                   // resident layer-0 fragments
-    float *lfnp = lw0 + G::FA0;                 // resident controller records
+    float *lfnp = lw0 + F0;                     // resident controller records
     float *lfcp = lfnp + G::FNP;                // resident fc.weight (lane layout) and fc.bias
     float *lfcb = lfcp + G::FCP;
-    lds_copy(lw0, a.p.fa[0], G::FA0);
+    float *lwl[3] = {lw0, lw, lw + G::FA1 / 2};
+    if (LP) {
+        lds_copy(lwl[1], a.p.fa[1], G::FA1 / 2);
+        lds_copy(lwl[2], a.p.fa[2], G::FA1 / 2);
+    }
+    lds_copy(lw0, a.p.fa[0], F0);
     lds_copy(lfnp, a.p.fnp, G::FNP);
     lds_copy(lfcp, a.p.fcp, G::FCP);
     lds_copy(lfcb, a.p.fcb, 4);
@@ -184,8 +192,10 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
         const unsigned long long st_w1 = fstamp();
         st_head += st_w1 - st_w0;
         // ---- layer 0 over the window (Functions.py:374) ----
-        __syncthreads();   // resident blocks are in place (first window) — no refill for layer 0
-        stagger();
+        if (j == 0) {
+            __syncthreads();   // resident blocks are in place — layer 0 (and in f16 mode every layer) never refills
+            stagger();
+        }
         {
             const float x0 = w0[0], x1 = w1[0];
             rot_left(w0);
@@ -218,13 +228,16 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             const bool keep_h = l == 1 || STORE;   // layer 2's h_t is only the backward's h_{t-1}
             const unsigned long long st_f0 = fstamp();
             if (l == 1) st_l0 += st_f0 - st_w1;
-            lds_fill<G::FA1 * 4, kFwdWaves>(lw, a.p.fa[l]);
+            if (!LP) {
+                lds_fill<G::FA1 * 4, kFwdWaves>(lw, a.p.fa[l]);
+                stagger();
+            }
+            const float *lwc = LP ? lwl[l] : lw;
             const unsigned long long st_f1 = fstamp();
             st_fill += st_f1 - st_f0;
-            stagger();
             load_quads<HS>(xc, SEQ_H(l - 1, 0), lane);
             load_quads<HS>(xn, SEQ_H(l - 1, 1), lane);
-            fwd16_cell<HS, false, true, LP>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
+            fwd16_cell<HS, false, true, LP>(lwc, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
             if (keep_h) store_quads<HS>(SEQ_H(l, 0), hout, lane);
             if (STORE) store_quads<HS>(SEQ_C(l, 0), c, lane);
 #pragma unroll
@@ -234,7 +247,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             }
             for (int t = 1; t < kL; ++t) {
                 load_quads<HS>(xn, SEQ_H(l - 1, t + 1 < kL ? t + 1 : t), lane);
-                fwd16_cell<HS, false, false, LP>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
+                fwd16_cell<HS, false, false, LP>(lwc, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
                 if (keep_h && !(l == 2 && t + 1 == kL)) store_quads<HS>(SEQ_H(l, t), hout, lane);
                 if (STORE && t + 1 < kL) store_quads<HS>(SEQ_C(l, t), c, lane);
 #pragma unroll
