@@ -95,6 +95,50 @@ def test_grad_allreduce_equals_global_mean_gloo_world2():
         assert abs(res[r][1] - loss.item()) < 1e-6
 
 
+def _dp_adamw_worker(rank, world, port, out):
+    """Three optimizer steps exactly as bench.py / train_model(grad_sync=...) run them per rank."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(rank + 7)                       # ranks start from different weights ...
+    model = fca.FNNModel(3, 50, 1, 1)
+    fca.distributed.broadcast_params(model)           # ... until rank 0's are broadcast
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-2)
+    sync = fca.distributed.GradAllReduce()
+    B_global = 10
+    lo, hi = fca.distributed.shard_range(B_global, rank, world)
+    for step in range(3):
+        X = torch.randn(B_global, 3, generator=torch.Generator().manual_seed(100 + step))
+        opt.zero_grad()
+        loss = (model(X[lo:hi]) - 0.3).pow(2).mean()
+        loss.backward()
+        sync(model, hi - lo, B_global, loss)
+        opt.step()
+    out[rank] = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).numpy()
+    dist.destroy_process_group()
+
+
+def test_dp_adamw_steps_equal_full_batch_gloo_world3():
+    """World size 3 with ragged shards (4/3/3): after three AdamW steps every rank holds the parameters
+    of one process training on the whole batch (the reduction order differs, hence allclose)."""
+    port = 30500 + os.getpid() % 1000
+    with mp.Manager() as m:
+        out = m.dict()
+        mp.spawn(_dp_adamw_worker, args=(3, port, out), nprocs=3, join=True)
+        res = dict(out)
+    torch.manual_seed(0 + 7)
+    model = fca.FNNModel(3, 50, 1, 1)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-2)
+    for step in range(3):
+        X = torch.randn(10, 3, generator=torch.Generator().manual_seed(100 + step))
+        opt.zero_grad()
+        (model(X) - 0.3).pow(2).mean().backward()
+        opt.step()
+    ref = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).numpy()
+    for r in range(3):
+        assert np.allclose(res[r], ref, atol=1e-6), r
+    assert np.array_equal(res[0], res[1]) and np.array_equal(res[1], res[2])
+
+
 def test_inference_refuses_cpu_tensors():
     """No CPU fallback: the product path needs the ROCm device (the oracle is test infrastructure)."""
     import pytest
