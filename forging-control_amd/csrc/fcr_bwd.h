@@ -166,8 +166,13 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
                     al[4 + k] = l1[k];
                 }
             }
+#if FCR_ABLATE == 1
+            if (((kb - KLO) & 1) == 0) a[0] += (float)ah[0] + (float)bh[kb][0];
+            else a2[0] += (float)ah[1] + (float)bh[kb][1];
+#else
             if (((kb - KLO) & 1) == 0) a = mma_p<LP>(ah, al, bh[kb], bl[kb], a);
             else a2 = mma_p<LP>(ah, al, bh[kb], bl[kb], a2);
+#endif
         }
         if (KHI - KLO > 1) a += a2;
     };
@@ -268,7 +273,11 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
             // of the cell (all fragments live at once); naming the accumulator keeps block kb-1's
             // MFMAs ahead of this point (issued ~NB*3 MFMAs ago: no hazard wait)
             if (kbb > 0) asm volatile("" : "+v"(acc[tau]));
+#if FCR_ABLATE == 1
+            acc[tau][0] += (float)ah[0] + (float)gh[cu][0];
+#else
             acc[tau] = mma_p<LP>(ah, al, gh[cu], gl[cu], acc[tau]);
+#endif
         }
         if (kbb + 1 < KBB) dgate_block(kbb + 1, fa[(kbb + 1) % 3], gh[nu], gl[nu]);
     }

@@ -22,6 +22,9 @@ constexpr int kOut = 4;          // [y_dot, p1, p2, z]
 constexpr int kCtrlIn = 3;       // [y_dot, z, ref]
 constexpr int kMS = 13;          // controller hidden slots (units 4m+q), hidden <= 52
 constexpr int kFnpStride = 8;    // floats per (m, q) controller record: W0 W1 W2 b wout 0 0 0
+#ifndef FCR_ABLATE
+#define FCR_ABLATE 0   // diagnostic builds only (scripts/ablate.sh): 1 = no MFMAs, 2 = no cell pointwise
+#endif
 #ifndef FCR_FWD_WAVES
 #define FCR_FWD_WAVES 8
 #endif

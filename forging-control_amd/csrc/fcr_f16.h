@@ -147,6 +147,11 @@ __device__ __forceinline__ void fwd_operand(int kb, float x0, float x1, const fl
 // P = (dh/dc, dh/do, dc/di, dc/df) and Q = (dc/dg, f), each one fma from products the cell has.
 template <bool FIRST>
 __device__ __forceinline__ void lstm_point(f32x4 a, float c_prev, float &c, float &h) {
+#if FCR_ABLATE == 2   // diagnostic: the cell pointwise goes
+    c = a[0] + c_prev;
+    h = a[1];
+    return;
+#endif
     const float i = sigm_pre(a[0]);
     const float f = sigm_pre(a[1]);
     const float g = tanh_pre(a[2]);
@@ -158,6 +163,11 @@ __device__ __forceinline__ void lstm_point(f32x4 a, float c_prev, float &c, floa
 }
 template <bool FIRST>
 __device__ __forceinline__ void lstm_point_grad(f32x4 a, float c_prev, f32x4 &P, f32x2 &Q) {
+#if FCR_ABLATE == 2
+    P = a;
+    Q = f32x2{c_prev, a[0]};
+    return;
+#endif
     const float i = sigm_pre(a[0]);
     const float f = sigm_pre(a[1]);
     const float g = tanh_pre(a[2]);

@@ -30,6 +30,7 @@ __device__ __forceinline__ void rot_left(float (&w)[kL]) {
 #ifndef FCR_FWD_PRIO
 #define FCR_FWD_PRIO 1
 #endif
+
 template <int HS, bool L0, bool FIRST, bool LP>
 __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lane, float x0, float x1,
                                            const float (&x)[HS], const float (&hp)[HS], float (&c)[HS],
@@ -77,8 +78,13 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
                 if (r1 + 2 < HS) rd(r1 + 2, KLO, nh[1], nl[1]);
             }
             const int ch = (kb - KLO) & 1;
+#if FCR_ABLATE == 1   // diagnostic: the fragment reads and operands stay, the MFMAs go
+            acc[0][ch][0] += (float)ah[0][0] + (float)bh[kb][0];
+            if (two) acc[1][ch][0] += (float)ah[1][0] + (float)bh[kb][1];
+#else
             acc[0][ch] = mma_p<LP>(ah[0], al[0], bh[kb], bl[kb], acc[0][ch]);
             if (two) acc[1][ch] = mma_p<LP>(ah[1], al[1], bh[kb], bl[kb], acc[1][ch]);
+#endif
             if (kb == KLO && p > 0) {
                 lstm_point<FIRST>(prev[0], c[r0 - 2], c[r0 - 2], hout[r0 - 2]);
                 lstm_point<FIRST>(prev[1], c[r1 - 2], c[r1 - 2], hout[r1 - 2]);
