@@ -14,13 +14,14 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", _LIB_NAME)
 
 FCR_OK = 0
-ABI_VERSION = 2
+ABI_VERSION = 3
 PRECISION_FP32, PRECISION_F16 = 0, 1
 ERRORS = {-1: "FCR_EINVAL", -2: "FCR_EWORKSPACE", -3: "FCR_EHIP", -4: "FCR_EUNSUPPORTED"}
 
 # Every symbol include/fcr.h declares (tests check the .so exports exactly these).
 EXPORTS = ("fcr_workspace_size", "fcr_forward", "fcr_backward", "fcr_lstm_workspace_size", "fcr_lstm_forward",
-           "fcr_lstm_backward", "fcr_plant_rk4", "fcr_closed_loop_run", "fcr_window_gather", "fcr_last_error", "fcr_abi_version")
+           "fcr_lstm_backward", "fcr_plant_rk4", "fcr_closed_loop_run", "fcr_window_gather", "fcr_fnn_workspace_size",
+           "fcr_fnn_forward", "fcr_fnn_backward", "fcr_last_error", "fcr_abi_version")
 
 
 class FcrDims(ctypes.Structure):
@@ -100,6 +101,12 @@ def load() -> ctypes.CDLL:
         lib.fcr_closed_loop_run.restype = i32
         lib.fcr_window_gather.argtypes = [ctypes.POINTER(FcrWindows), i32, vp, vp, vp, vp, vp, vp]
         lib.fcr_window_gather.restype = i32
+        lib.fcr_fnn_workspace_size.argtypes = [i32, i32, ctypes.POINTER(sz)]
+        lib.fcr_fnn_workspace_size.restype = i32
+        lib.fcr_fnn_forward.argtypes = [i32, i32, i32, vp, vp, vp, vp, vp, vp]
+        lib.fcr_fnn_forward.restype = i32
+        lib.fcr_fnn_backward.argtypes = [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp]
+        lib.fcr_fnn_backward.restype = i32
         lib.fcr_last_error.argtypes = []
         lib.fcr_last_error.restype = ctypes.c_char_p
         lib.fcr_abi_version.argtypes = []

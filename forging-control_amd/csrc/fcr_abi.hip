@@ -14,6 +14,7 @@
 #include "fcr.h"
 #include "fcr_bwd.h"
 #include "fcr_common.h"
+#include "fcr_fnn.h"
 #include "fcr_fwd.h"
 #include "fcr_img.h"
 #include "fcr_pack.h"
@@ -823,6 +824,56 @@ int fcr_lstm_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, 
         if ((rc = launch_check("window_transpose_kernel"))) return rc;
     }
     return FCR_OK;
+}
+
+int fcr_fnn_workspace_size(int32_t B, int32_t hidden, size_t *bytes) {
+    if (B < 0 || hidden < 1 || hidden > fnn::kFnnMaxHidden)
+        return fail(FCR_EINVAL, "fcr_fnn_workspace_size: B=%d, hidden=%d (1..%d)", B, hidden, fnn::kFnnMaxHidden);
+    if (!bytes) return fail(FCR_EINVAL, "bytes is NULL");
+    const size_t blocks = ((size_t)B + fnn::kFnnItems - 1) / fnn::kFnnItems;
+    *bytes = blocks * (size_t)hidden * 5 * sizeof(float);
+    return FCR_OK;
+}
+
+static int fnn_check(const char *what, int32_t B, int32_t in_dim, int32_t hidden) {
+    if (B < 0) return fail(FCR_EINVAL, "%s: B=%d must be >= 0", what, B);
+    if (in_dim != kCtrlIn) return fail(FCR_EUNSUPPORTED, "%s: in_dim=%d: built for %d (UL/Main.py:188)", what, in_dim, kCtrlIn);
+    if (hidden < 1 || hidden > fnn::kFnnMaxHidden)
+        return fail(FCR_EUNSUPPORTED, "%s: hidden=%d: built for 1..%d", what, hidden, fnn::kFnnMaxHidden);
+    return FCR_OK;
+}
+
+int fcr_fnn_forward(int32_t B, int32_t in_dim, int32_t hidden, const float *X, const float *w_inp,
+                    const float *b_inp, const float *w_out, float *u, void *stream) {
+    int rc = fnn_check("fcr_fnn_forward", B, in_dim, hidden);
+    if (rc) return rc;
+    if (B == 0) return FCR_OK;
+    if (!X || !w_inp || !b_inp || !w_out || !u) return fail(FCR_EINVAL, "fcr_fnn_forward: a required pointer is NULL");
+    hipLaunchKernelGGL(fnn::fnn_fwd_kernel, dim3((B + fnn::kFnnBlock - 1) / fnn::kFnnBlock), dim3(fnn::kFnnBlock), 0,
+                       (hipStream_t)stream, B, hidden, X, w_inp, b_inp, w_out, u);
+    return launch_check("fnn_fwd_kernel");
+}
+
+int fcr_fnn_backward(int32_t B, int32_t in_dim, int32_t hidden, const float *X, const float *w_inp,
+                     const float *b_inp, const float *w_out, const float *g_u, float *g_x, float *g_w_inp,
+                     float *g_b_inp, float *g_w_out, void *ws, size_t ws_bytes, void *stream) {
+    int rc = fnn_check("fcr_fnn_backward", B, in_dim, hidden);
+    if (rc) return rc;
+    if (!w_inp || !b_inp || !w_out || !g_w_inp || !g_b_inp || !g_w_out || (B && (!X || !g_u || !ws)))
+        return fail(FCR_EINVAL, "fcr_fnn_backward: a required pointer is NULL");
+    size_t need = 0;
+    if ((rc = fcr_fnn_workspace_size(B, hidden, &need))) return rc;
+    if (ws_bytes < need) return fail(FCR_EWORKSPACE, "fcr_fnn_backward: ws has %zu bytes, needs %zu", ws_bytes, need);
+    hipStream_t s = (hipStream_t)stream;
+    const int blocks = (int)((B + fnn::kFnnItems - 1) / fnn::kFnnItems);
+    if (blocks) {
+        hipLaunchKernelGGL(fnn::fnn_bwd_kernel, dim3(blocks), dim3(fnn::kFnnBlock), 0, s, B, hidden, X, w_inp, b_inp,
+                           w_out, g_u, g_x, (float *)ws);
+        if ((rc = launch_check("fnn_bwd_kernel"))) return rc;
+    }
+    hipLaunchKernelGGL(grad_reduce_kernel, dim3(hidden * 5), dim3(256), 0, s, (const float *)ws, blocks, hidden,
+                       g_w_inp, g_b_inp, g_w_out);
+    return launch_check("grad_reduce_kernel");
 }
 
 }  // extern "C"

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define FCR_ABI_VERSION 2
+#define FCR_ABI_VERSION 3
 
 enum {
     FCR_OK = 0,
@@ -113,6 +113,22 @@ int fcr_backward(const fcr_dims *dims,
                  const float *dloss,
                  float *g_u0, float *g_w_inp, float *g_b_inp, float *g_w_out,
                  void *ws, size_t ws_bytes, void *stream);
+
+/*
+ * The caller's controller call `output = model(X)` (Functions.py:643): FNNModel.forward
+ * (Functions.py:261-289) at the reference's shape — Linear(in_dim=3 -> hidden) + ReLU,
+ * Linear(hidden -> 1, no bias) + Hardtanh (UL/Main.py:188, width_dim = 1); hidden <= 64.
+ *   X (B,3), w_inp (hidden,3), b_inp (hidden), w_out (1,hidden) -> u (B,1)
+ * fcr_fnn_backward is its autograd backward for g_u = dL/du (B,1): the parameter gradients
+ * (OVERWRITTEN, fixed reduction order) and g_x = dL/dX (B,3), or NULL to skip it. Hardtanh'(±1) = 0,
+ * ReLU'(0) = 0 (torch). Scratch: fcr_fnn_workspace_size bytes.
+ */
+int fcr_fnn_workspace_size(int32_t B, int32_t hidden, size_t *bytes);
+int fcr_fnn_forward(int32_t B, int32_t in_dim, int32_t hidden, const float *X, const float *w_inp,
+                    const float *b_inp, const float *w_out, float *u, void *stream);
+int fcr_fnn_backward(int32_t B, int32_t in_dim, int32_t hidden, const float *X, const float *w_inp,
+                     const float *b_inp, const float *w_out, const float *g_u, float *g_x, float *g_w_inp,
+                     float *g_b_inp, float *g_w_out, void *ws, size_t ws_bytes, void *stream);
 
 /*
  * Batched forging-press plant: the state update x_{t+1} = F(x_t, u_t) of

@@ -78,3 +78,29 @@ def test_null_pointers_rejected_before_any_device_call():
     assert rc == -1 and "NULL" in lib.fcr_last_error().decode()
     rc = lib.fcr_backward(ctypes.byref(d), *([None] * 8), None, 0, None)
     assert rc == -1
+
+
+def test_fnn_entry_points_validate_before_any_device_call():
+    lib = fca._native.load()
+    out = ctypes.c_size_t(0)
+    assert lib.fcr_fnn_workspace_size(65536, 50, ctypes.byref(out)) == 0
+    assert out.value == 256 * 50 * 5 * 4          # one partial record per 256-sample block
+    assert lib.fcr_fnn_workspace_size(65536, 65, ctypes.byref(out)) == -1
+    assert lib.fcr_fnn_forward(16, 4, 50, *([None] * 5), None) == -4      # in_dim != 3
+    assert "in_dim" in lib.fcr_last_error().decode()
+    assert lib.fcr_fnn_forward(16, 3, 80, *([None] * 5), None) == -4      # hidden > 64
+    assert lib.fcr_fnn_forward(16, 3, 50, *([None] * 5), None) == -1      # NULL
+    assert lib.fcr_fnn_forward(0, 3, 50, *([None] * 5), None) == 0        # empty batch: no launch
+    assert lib.fcr_fnn_backward(-1, 3, 50, *([None] * 10), 0, None) == -1
+    assert lib.fcr_fnn_backward(16, 3, 50, *([None] * 10), 0, None) == -1
+
+
+def test_fnn_model_on_cpu_is_the_torch_module():
+    """CPU tensors never reach the HIP path (it is selected for ROCm tensors of the reference's shape)."""
+    import torch
+    m = fca.FNNModel(3, 50, 1, 1)
+    x = torch.randn(7, 3)
+    from forging_control_amd.controller import hip_shape_ok
+    assert not hip_shape_ok(m, x)
+    ref = torch.nn.functional.hardtanh(m.fc_out(torch.relu(m.fc_inp(x))))
+    assert torch.equal(m(x), ref)
