@@ -105,12 +105,12 @@ Layout make_layout(const fcr_dims *d, int with_backward) {
     L.fnn_part = take(sizeof(float) * (size_t)L.ctrl_blocks * d->ctrl_hidden * 5);
     // sequence slabs (fcr_common.h): h of every cell always (layers 0, 1 are the next phase's input);
     // c, the window rows and the backward's dx / window-row-gradient slabs only with a backward
-    const size_t qcells = (size_t)L.nw_pad * d->N * kLayers * kL * ((HS + 3) / 4) * kWave;
+    const size_t qcells = (size_t)L.nw_pad * d->N * kLayers * kL * HS * 16;   // Geo<HS>::QC per cell
     L.hseq = take(sizeof(f32x4) * qcells);
     if (with_backward) {
         L.cseq = take(sizeof(f32x4) * qcells);
         L.xw = take(sizeof(f32x2) * (size_t)L.nw_pad * d->N * kL * kWave);
-        L.dseq = take(sizeof(f32x4) * (size_t)L.nw_pad * d->N * 2 * kL * ((HS + 3) / 4) * kWave);
+        L.dseq = take(sizeof(f32x4) * (size_t)L.nw_pad * d->N * 2 * kL * HS * 16);
         L.dxrow = take(sizeof(f32x2) * (size_t)L.nw_pad * d->N * kL * kWave);
     }
 #if FCR_STAMP

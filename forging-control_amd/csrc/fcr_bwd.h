@@ -51,7 +51,7 @@ struct NextIn {
 template <int HS, int k = 0>
 __device__ __forceinline__ void ld_quads(f32x4 (&dst)[Geo<HS>::HQ], __amdgpu_buffer_rsrc_t r, uint32_t off, int lane) {
     if constexpr (k < Geo<HS>::HQ) {
-        dst[k] = buf_ldq<quad_n<HS, k>()>(r, lane * 16, off + k * kWave * 16);
+        dst[k] = buf_ldq<quad_n<HS, k>()>(r, quad_voff<HS, k>(lane), off + quad_soff<HS, k>());
         ld_quads<HS, k + 1>(dst, r, off, lane);
     }
 }
@@ -191,7 +191,8 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
         if (NX_HC && (r & 3) == 3)
             ci.c[r >> 2] = buf_ld4(nx.rc, lane * 16, nx.c + (r >> 2) * kWave * 16);
         if (NX_HC && r == HS - 1 && (r & 3) != 3)
-            ci.c[r >> 2] = buf_ldq<quad_n<HS, (HS - 1) / 4>()>(nx.rc, lane * 16, nx.c + (r >> 2) * kWave * 16);
+            ci.c[r >> 2] = buf_ldq<quad_n<HS, (HS - 1) / 4>()>(nx.rc, quad_voff<HS, (HS - 1) / 4>(lane),
+                                                              nx.c + quad_soff<HS, (HS - 1) / 4>());
     };
     // forward MFMAs of slot pair kbb into fa[.][0..1]
     auto fwd_pair = [&](int kbb, f32x4 (&fp)[2]) {
@@ -365,7 +366,7 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
     float dh[HS], dc[HS], dxo[HS], dab[HS];
 
     // this wave's slab regions
-    const size_t qcell = (size_t)Geo<HS>::HQ * kWave;   // one cell of a sequence slab, in quads
+    const size_t qcell = (size_t)Geo<HS>::QC;   // one cell of a sequence slab, in 16-B units
     const size_t seq_sz = (size_t)N * kLayers * kL * qcell;
     const size_t dseq_sz = (size_t)N * 2 * kL * qcell;
     NextIn nb;

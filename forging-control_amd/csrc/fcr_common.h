@@ -23,7 +23,8 @@ constexpr int kCtrlIn = 3;       // [y_dot, z, ref]
 constexpr int kMS = 13;          // controller hidden slots (units 4m+q), hidden <= 52
 constexpr int kFnpStride = 8;    // floats per (m, q) controller record: W0 W1 W2 b wout 0 0 0
 #ifndef FCR_ABLATE
-#define FCR_ABLATE 0   // diagnostic builds only (scripts/ablate.sh): 1 = no MFMAs, 2 = no cell pointwise
+#define FCR_ABLATE 0   // diagnostic builds only (scripts/ablate.sh): 1 = no MFMAs, 2 = no cell pointwise,
+                       // 3 = no slab traffic (sequence loads return opaque registers, stores go)
 #endif
 #ifndef FCR_FWD_WAVES
 #define FCR_FWD_WAVES 8
@@ -38,7 +39,8 @@ constexpr float kP2Max = 1.036233f;  // Functions.py:1411 (32e6 / p2 max_abs_)
 
 template <int HS>
 struct Geo {
-    static constexpr int HQ = (HS + 3) / 4;   // 16-B quads per unit-slot vector (sequence slabs)
+    static constexpr int HQ = (HS + 3) / 4;   // registers (f32x4) per unit-slot vector
+    static constexpr int QC = HS * 16;        // 16-B units per cell record of a sequence slab (64 lanes x 4·HS B)
 };
 
 struct Packed {                    // device pointers into the workspace
@@ -50,9 +52,9 @@ struct Packed {                    // device pointers into the workspace
 };
 
 // Sequence slabs (per wave, each address written once per call):
-//   hseq, cseq [wave][j][layer][t][quad][64]  h_t and c_t of every cell, 4 unit slots per 16-B quad
+//   hseq, cseq [wave][j][layer][t][record]     h_t and c_t of every cell (compact records: store_quads)
 //   xw         [wave][j][t][64]               layer-0 window row t of window j (col q, col 4)
-//   dseq       [wave][j][2][t][quad][64]      backward dx of layers 2, 1 (inputs of layers 1, 0)
+//   dseq       [wave][j][2][t][record]         backward dx of layers 2, 1 (inputs of layers 1, 0)
 //   dxrow      [wave][j][t][64]               backward window-row gradients (col q, col 4)
 struct FwdArgs {
     int B, N;
@@ -148,15 +150,28 @@ __device__ __forceinline__ f32x4 lds_quad(const float *lw, int idx, int lane) {
     return *reinterpret_cast<const f32x4 *>(hi + (byte - kSplit));
 }
 
+// FCR_ABLATE == 3: a register the compiler cannot see through, in place of a load
+__device__ __forceinline__ float ablate_val(uint32_t seed) {
+    float v;   // values in [-1, 1) like the h and c they replace (operand-dependent MFMA power)
+    asm volatile("v_cvt_f32_ubyte0 %0, %1" : "=v"(v) : "v"(seed * 2654435761u));
+    return fmaf(v, 1.0f / 128.0f, -1.0f);
+}
+
 // Raw buffer loads through a wave-uniform descriptor (base and size from SGPR values only, so no
 // waterfall loop): the per-lane part is a 32-bit voffset, the rest an SGPR soffset.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void *base, size_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)(uint32_t)bytes, 0x00020000);
 }
 __device__ __forceinline__ f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+#if FCR_ABLATE == 3
+    return f32x4{ablate_val(voff), ablate_val(voff + soff), ablate_val(voff ^ soff), ablate_val(voff - soff)};
+#endif
     return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
 }
 __device__ __forceinline__ f32x2 buf_ld2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+#if FCR_ABLATE == 3
+    return f32x2{ablate_val(voff), ablate_val(voff + soff)};
+#endif
     return __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0));
 }
 // Quad k of a unit-slot vector with only its first n (1..4) slots loaded: a padding lane of a partial
@@ -164,6 +179,9 @@ __device__ __forceinline__ f32x2 buf_ld2(__amdgpu_buffer_rsrc_t r, uint32_t voff
 template <int n>
 __device__ __forceinline__ f32x4 buf_ldq(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     f32x4 q = {0.0f, 0.0f, 0.0f, 0.0f};
+#if FCR_ABLATE == 3
+    return buf_ld4(r, voff, soff);
+#endif
     if (n == 4) {
         q = buf_ld4(r, voff, soff);
     } else if (n == 3) {
@@ -183,8 +201,17 @@ __device__ __forceinline__ f32x4 buf_ldq(__amdgpu_buffer_rsrc_t r, uint32_t voff
 }
 template <int HS, int k>
 constexpr int quad_n() { return HS - 4 * k >= 4 ? 4 : HS - 4 * k; }
+// per-lane byte offset and cell-relative byte offset of record quad k (the tail is packed, store_quads)
+template <int HS, int k>
+__device__ __forceinline__ uint32_t quad_voff(int lane) { return (uint32_t)lane * (quad_n<HS, k>() == 4 ? 16u : 4u * quad_n<HS, k>()); }
+template <int HS, int k>
+constexpr uint32_t quad_soff() { return (uint32_t)k * kWave * 16; }
 
 __device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, f32x2 v) {
+#if FCR_ABLATE == 3
+    asm volatile("" ::"v"(v[0]), "v"(v[1]));
+    return;
+#endif
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int, v), r,
                                           (int)voff, (int)soff, 0);
 }
@@ -212,33 +239,47 @@ __device__ __forceinline__ void lds_fill(float *lw, const float *__restrict__ sr
     __syncthreads();
 }
 
-// Unit-slot vectors <-> 16-B quads (slots 4k..4k+3 of one lane in one record): sequence hand-offs
-// cost ceil(HS/4) memory instructions per cell instead of HS (vmcnt holds at most 63 per wave).
+// Unit-slot vectors <-> a compact cell record: HS/4 full 16-B quads [k][64 lanes] (slots 4k..4k+3),
+// then the HS%4 tail slots packed per lane [64 lanes][HS%4] — 4·HS bytes per lane, no padding slots
+// (a padded last quad cost 3/16 of the slab traffic at HS = 13, and the HBM traffic sets the clock
+// the chip holds). A cell is Geo<HS>::QC quads; ceil(HS/4) memory instructions per cell.
 template <int HS>
 __device__ __forceinline__ void store_quads(f32x4 *dst, const float (&v)[HS], int lane) {
+#if FCR_ABLATE == 3
+    for (int k = 0; k < HS; ++k) asm volatile("" ::"v"(v[k]));
+    return;
+#endif
+    constexpr int FQ = HS / 4, TS = HS % 4;
 #pragma unroll
-    for (int k = 0; k < (HS + 3) / 4; ++k) {
-        f32x4 q;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) q[e] = (4 * k + e < HS) ? v[4 * k + e < HS ? 4 * k + e : 0] : 0.0f;
-        dst[k * kWave + lane] = q;
+    for (int k = 0; k < FQ; ++k) dst[k * kWave + lane] = f32x4{v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]};
+    if constexpr (TS > 0) {
+        float *t = reinterpret_cast<float *>(dst + FQ * kWave) + lane * TS;
+        if constexpr (TS == 1) {
+            t[0] = v[4 * FQ];
+        } else if constexpr (TS == 2) {
+            *reinterpret_cast<f32x2 *>(t) = f32x2{v[4 * FQ], v[4 * FQ + 1]};
+        } else {
+            typedef float f32x3 __attribute__((ext_vector_type(3)));
+            *reinterpret_cast<f32x3 *>(t) = f32x3{v[4 * FQ], v[4 * FQ + 1], v[4 * FQ + 2]};
+        }
     }
 }
 template <int HS>
 __device__ __forceinline__ void load_quads(float (&v)[HS], const f32x4 *src, int lane) {
+#if FCR_ABLATE == 3
+    for (int k = 0; k < HS; ++k) v[k] = ablate_val(lane + 64 * k + (uint32_t)(uintptr_t)src);
+    return;
+#endif
+    constexpr int FQ = HS / 4, TS = HS % 4;
 #pragma unroll
-    for (int k = 0; k < (HS + 3) / 4; ++k) {
-        const float *p = reinterpret_cast<const float *>(src + k * kWave + lane);
-        if (4 * k + 4 <= HS) {   // full quad
-            const f32x4 q = src[k * kWave + lane];
+    for (int k = 0; k < FQ; ++k) {
+        const f32x4 q = src[k * kWave + lane];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[4 * k + e] = q[e];
-        } else {                 // partial last quad: only the slots that exist (see buf_ldq)
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (4 * k + e < HS) v[4 * k + e] = p[e];
-        }
+        for (int e = 0; e < 4; ++e) v[4 * k + e] = q[e];
     }
+    const float *t = reinterpret_cast<const float *>(src + FQ * kWave) + lane * TS;
+#pragma unroll
+    for (int e = 0; e < TS; ++e) v[4 * FQ + e] = t[e];
 }
 
 // Controller pre-activation (FNNModel.forward, Functions.py:261-289): lane group q evaluates hidden

@@ -162,7 +162,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
     float c[HS], hout[HS], hp[HS], xc[HS], xn[HS];
     // sequence slabs [wave][j][layer][t][quad][64]: h of every cell (layers 0, 1: the next phase's
     // input; with STORE also layer 2) and, with STORE, c; plus the window rows [wave][j][t][64]
-    const size_t qcell = (size_t)Geo<HS>::HQ * kWave;    // one cell of a sequence slab, in quads
+    const size_t qcell = (size_t)Geo<HS>::QC;    // one cell of a sequence slab, in 16-B units
     const size_t wseq = (size_t)wave * N * kLayers * kL * qcell;
     f32x4 *hs_wave = a.hseq + wseq;
     f32x4 *cs_wave = a.cseq + wseq;
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             fwd16_cell<HS, true, true, LP>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
             store_quads<HS>(SEQ_H(0, 0), hout, lane);
             if (STORE) {
-                xw_wave[(size_t)j * kL * kWave + lane] = f32x2{x0, x1};
+                if (FCR_ABLATE != 3) xw_wave[(size_t)j * kL * kWave + lane] = f32x2{x0, x1};
                 store_quads<HS>(SEQ_C(0, 0), c, lane);
             }
 #pragma unroll
@@ -222,7 +222,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             fwd16_cell<HS, true, false, LP>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
             store_quads<HS>(SEQ_H(0, t), hout, lane);
             if (STORE) {
-                xw_wave[((size_t)j * kL + t) * kWave + lane] = f32x2{x0, x1};
+                if (FCR_ABLATE != 3) xw_wave[((size_t)j * kL + t) * kWave + lane] = f32x2{x0, x1};
                 if (t + 1 < kL) store_quads<HS>(SEQ_C(0, t), c, lane);   // c_9 is never a c_{t-1}
             }
 #pragma unroll
