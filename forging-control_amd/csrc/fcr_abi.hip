@@ -621,7 +621,7 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
     pa.fcbo = (float *)(base + L.fcb);
     pa.fnp = (float *)(base + L.fnp);
     for (int l = 0; l < kLayers; ++l) {
-        const int nf = (int)(f16_fwd_bytes(L.HS, l) / 4);   // one thread per (hi, lo) pair
+        const int nf = L.HS * (l == 0 ? (L.HS + 2 + 7) / 8 : (2 * L.HS + 7) / 8) * kWave * 8;   // per (tile, block, lane, k)
         hipLaunchKernelGGL(pack_fwd16_kernel, dim3((nf + 255) / 256), dim3(256), 0, s, pa, l,
                            (_Float16 *)(base + L.fa[l]));
         if ((rc = launch_check("pack_fwd16_kernel"))) return rc;

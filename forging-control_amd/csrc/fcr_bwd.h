@@ -124,6 +124,8 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
 
     float up, down, sg0;   // the trajectory's power-of-two scale, set once the incoming dh is in
 
+    // packed tail block (fcr_f16.h, fcr_img.h): its hi-image row read is the packed fragment
+    constexpr bool TAIL = !L0 && G::TAIL1;
     // ---- the recomputation's B operands (this cell's x_t and h_{t-1}) ----
     f16x8 bh[KB], bl[KB] = {};
     {
@@ -136,6 +138,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
         const float x0 = ci.x[0][0], x1 = ci.x[0][1];
 #pragma unroll
         for (int kb = KLO; kb < KHI; ++kb) fwd_operand<HS, L0, FIRST, LP>(kb, x0, x1, xv, hv, bh[kb], bl[kb]);
+        if (TAIL && KHI == KB) bh[KB - 1] = tail_operand<LP>(bh[KB - 1], bl[KB - 1]);
     }
 
     // Recomputed forward tile r: its MFMA chain, issued two regions before its result is used (two
@@ -158,7 +161,8 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
                 ah[k] = h0[k];
                 ah[4 + k] = h1[k];
             }
-            if (!LP) {
+            const bool tail = TAIL && kb == KB - 1;
+            if (!LP && !tail) {
                 const f16x4 l0 = lds_b64_f16(b0), l1 = lds_b64_f16(b1);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
@@ -170,8 +174,14 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
             if (((kb - KLO) & 1) == 0) a[0] += (float)ah[0] + (float)bh[kb][0];
             else a2[0] += (float)ah[1] + (float)bh[kb][1];
 #else
-            if (((kb - KLO) & 1) == 0) a = mma_p<LP>(ah, al, bh[kb], bl[kb], a);
-            else a2 = mma_p<LP>(ah, al, bh[kb], bl[kb], a2);
+            if (tail) {
+                if (((kb - KLO) & 1) == 0) a = mfma16(ah, bh[kb], a);
+                else a2 = mfma16(ah, bh[kb], a2);
+            } else if (((kb - KLO) & 1) == 0) {
+                a = mma_p<LP>(ah, al, bh[kb], bl[kb], a);
+            } else {
+                a2 = mma_p<LP>(ah, al, bh[kb], bl[kb], a2);
+            }
 #endif
         }
         if (KHI - KLO > 1) a += a2;

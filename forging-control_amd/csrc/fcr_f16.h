@@ -23,24 +23,42 @@ namespace fcr {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
+// Packed tail block (layers >= 1 when 2·HS = 8·(KB1-1) + 2, i.e. HS = 13): the last k-block holds
+// only combined slots 2HS-2, 2HS-1 (6 of its 8 k are zero padding), so its three split products go
+// into ONE MFMA over k = [A_hi B_hi | A_hi B_lo | A_lo B_hi | 0 0]: the A fragment carries
+// (hi σ0, hi σ1, hi σ0, hi σ1, lo σ0, lo σ1, 0, 0) and the B operand (hi, hi, lo, lo, hi, hi, 0, 0)
+// of the two slots. 10 instead of 12 MFMAs per tile and 13 % less fragment LDS at H = 50.
+__host__ __device__ constexpr bool tail_packed(int HS) { return 2 * HS - 8 * ((2 * HS + 7) / 8 - 1) == 2; }
+
 template <int HS>
 struct Geo16 {
     static constexpr int KB0 = (HS + 2 + 7) / 8;                    // layer-0 k-blocks
     static constexpr int XBLK = HS >> 3;                            // layer-0 block holding the columns
     static constexpr int KB1 = (2 * HS + 7) / 8;                    // layers >= 1
     static constexpr int KX1 = (HS + 7) / 8;                        // layers >= 1: blocks holding x slots
+    static constexpr bool TAIL1 = tail_packed(HS);                  // layers >= 1: packed last block
     static constexpr int QF0 = HS * KB0 * 2;                        // fragment quads (64 lanes x 16 B)
-    static constexpr int QF1 = HS * KB1 * 2;
-    static constexpr int FA0 = QF0 * kWave * 4, FA1 = QF1 * kWave * 4;   // floats
+    static constexpr int QH1 = HS * KB1;                            // layers >= 1: hi quads (tail included)
+    static constexpr int QF1 = QH1 + HS * (KB1 - (TAIL1 ? 1 : 0));  //   + lo quads
+    static constexpr int FA0 = QF0 * kWave * 4, FA1 = QF1 * kWave * 4, FH1 = QH1 * kWave * 4;   // floats
     static constexpr int FNP = kMS * 4 * kFnpStride;
     static constexpr int FCP = kOut * HS * 4;
     static constexpr int MISC = FNP + FCP + 4;
     static constexpr int LDS_FWD = (FA1 + FA0 + MISC) * 4;   // bytes
     // f16 mode: the hi fragments of all three layers stay resident (no per-phase refills)
-    static constexpr int LDS_FWD_LP = (FA1 + FA0 / 2 + MISC) * 4;
+    static constexpr int LDS_FWD_LP = (2 * FH1 + FA0 / 2 + MISC) * 4;
     static_assert(LDS_FWD <= 163840 && LDS_FWD_LP <= 163840, "fragments exceed the 160 KiB LDS");
     static_assert((HS & 7) + 1 < 8, "window columns must share one k-block");
 };
+
+// B operand of the packed tail block from the block's split halves (elements 0, 1 are the two real
+// slots): (hi, hi, lo, lo, hi, hi, 0, 0); the f16 mode keeps only the hi·hi part.
+template <bool LP>
+__device__ __forceinline__ f16x8 tail_operand(f16x8 bh, f16x8 bl) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 h = __builtin_bit_cast(u32x4, bh), l = __builtin_bit_cast(u32x4, bl);
+    return __builtin_bit_cast(f16x8, LP ? u32x4{h[0], 0u, 0u, 0u} : u32x4{h[0], l[0], h[0], 0u});
+}
 
 __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
@@ -184,23 +202,13 @@ __device__ __forceinline__ void lstm_point_grad(f32x4 a, float c_prev, f32x4 &P,
 // host-side geometry of the forward fragment blocks (bytes), matching Geo16
 inline size_t f16_fwd_bytes(int HS, int l) {
     const int KB = l == 0 ? (HS + 2 + 7) / 8 : (2 * HS + 7) / 8;
-    return (size_t)HS * KB * 2 * kWave * 16;
+    const int lo_blocks = (l > 0 && tail_packed(HS)) ? KB - 1 : KB;
+    return (size_t)HS * (KB + lo_blocks) * kWave * 16;
 }
 
-// Forward fragments, f16 split: element (split, r, kb, lane, j) = hi|lo of A[rho][k] with rho = lane&15
-// -> unit 4r+(rho>>2), gate rho&3 (torch row gate*H + unit), k = combined slot 8kb+j of lane group
-// lane>>4 (see the header). Scaled for exp2 as the pointwise expects.
-__global__ void pack_fwd16_kernel(PackArgs a, int l, _Float16 *dst) {
+// Scaled weight of the forward product: gate row (unit, gate) x combined slot s of lane group kq.
+__device__ __forceinline__ float fwd16_weight(const PackArgs &a, int l, int unit, int gate, int s, int kq) {
     const int H = a.H, HS = a.HS;
-    const int KB = l == 0 ? (HS + 2 + 7) / 8 : (2 * HS + 7) / 8;
-    const int n = HS * KB * kWave * 8;
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= n) return;
-    const int j = idx & 7, lane = (idx >> 3) & 63, rk = idx >> 9;
-    const int kb = rk % KB, r = rk / KB;
-    const int rho = lane & 15, kq = lane >> 4;
-    const int unit = 4 * r + (rho >> 2), gate = rho & 3;
-    const int s = 8 * kb + j;
     float v = 0.0f;
     if (unit < H) {
         const int grow = gate * H + unit;
@@ -221,13 +229,42 @@ __global__ void pack_fwd16_kernel(PackArgs a, int l, _Float16 *dst) {
             if (u < H) v = a.whh[l][grow * H + u];
         }
     }
-    v *= (gate == 2 ? kTwoLog2e : kNegLog2e);
+    return v * (gate == 2 ? kTwoLog2e : kNegLog2e);
+}
+
+// Forward fragments, f16 split: element (split, r, kb, lane, j) = hi|lo of A[rho][k] with rho = lane&15
+// -> unit 4r+(rho>>2), gate rho&3 (torch row gate*H + unit), k = combined slot 8kb+j of lane group
+// lane>>4 (see the header). Scaled for exp2 as the pointwise expects. Split-major: every hi fragment of
+// the layer [r][kb], then every lo one [r][kb] (the f16 mode reads the first part); with a packed tail
+// (tail_packed) the hi part's last block of each tile is the packed tail fragment and it has no lo.
+__global__ void pack_fwd16_kernel(PackArgs a, int l, _Float16 *dst) {
+    const int HS = a.HS;
+    const int KB = l == 0 ? (HS + 2 + 7) / 8 : (2 * HS + 7) / 8;
+    const bool tail = l > 0 && tail_packed(HS);
+    const int KL = tail ? KB - 1 : KB;   // lo blocks per tile
+    const int n = HS * KB * kWave * 8;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n) return;
+    const int j = idx & 7, lane = (idx >> 3) & 63, rk = idx >> 9;
+    const int kb = rk % KB, r = rk / KB;
+    const int rho = lane & 15, kq = lane >> 4;
+    const int unit = 4 * r + (rho >> 2), gate = rho & 3;
+    if (tail && kb == KB - 1) {   // packed tail: (hi s0, hi s1, hi s0, hi s1, lo s0, lo s1, 0, 0)
+        _Float16 out = (_Float16)0.0f;
+        if (j < 6) {
+            const float v = fwd16_weight(a, l, unit, gate, 8 * kb + (j & 1), kq);
+            const _Float16 hi = (_Float16)v;
+            out = j < 4 ? hi : (_Float16)(v - (float)hi);
+        }
+        dst[((size_t)rk * kWave + lane) * 8 + j] = out;
+        return;
+    }
+    const float v = fwd16_weight(a, l, unit, gate, 8 * kb + j, kq);
     const _Float16 hi = (_Float16)v;
     const _Float16 lo = (_Float16)(v - (float)hi);
-    // split-major: every hi fragment of the layer, then every lo one (the f16 mode reads the first half)
     const size_t nq = (size_t)HS * KB;
     dst[((size_t)rk * kWave + lane) * 8 + j] = hi;
-    dst[((nq + rk) * kWave + lane) * 8 + j] = lo;
+    dst[((nq + (size_t)r * KL + kb) * kWave + lane) * 8 + j] = lo;
 }
 
 }  // namespace fcr

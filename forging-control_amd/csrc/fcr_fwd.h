@@ -46,13 +46,17 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
     constexpr int KLO = (L0 && FIRST) ? G::XBLK : 0;
     constexpr int KHI = FIRST ? (L0 ? G::XBLK + 1 : G::KX1) : KB;
     constexpr int NP = (HS + 1) / 2;   // tile pairs
+    // packed tail block (fcr_f16.h): one MFMA on the tail fragment, no lo fragment
+    constexpr bool TAIL = !L0 && G::TAIL1;
+    constexpr int KT = TAIL ? KB - 1 : KB;   // lo fragments per tile
     f16x8 bh[KB], bl[KB] = {};
 #pragma unroll
     for (int kb = KLO; kb < KHI; ++kb) fwd_operand<HS, L0, FIRST, LP>(kb, x0, x1, x, hp, bh[kb], bl[kb]);
+    if (TAIL && KHI == KB) bh[KB - 1] = tail_operand<LP>(bh[KB - 1], bl[KB - 1]);
     // fragment reads of (tile r, block kb): hi, lo
     auto rd = [&](int r, int kb, f16x8 &h, f16x8 &l) {   // split-major fragments (pack_fwd16_kernel)
         h = lds_frag16(lw, r * KB + kb, lane);
-        if (!LP) l = lds_frag16(lw, HS * KB + r * KB + kb, lane);
+        if (!LP && !(TAIL && kb == KB - 1)) l = lds_frag16(lw, HS * KB + r * KT + kb, lane);
     };
     f16x8 ah[2], al[2] = {};
     rd(0, KLO, ah[0], al[0]);
@@ -82,8 +86,13 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
             acc[0][ch][0] += (float)ah[0][0] + (float)bh[kb][0];
             if (two) acc[1][ch][0] += (float)ah[1][0] + (float)bh[kb][1];
 #else
-            acc[0][ch] = mma_p<LP>(ah[0], al[0], bh[kb], bl[kb], acc[0][ch]);
-            if (two) acc[1][ch] = mma_p<LP>(ah[1], al[1], bh[kb], bl[kb], acc[1][ch]);
+            if (TAIL && kb == KB - 1) {
+                acc[0][ch] = mfma16(ah[0], bh[kb], acc[0][ch]);
+                if (two) acc[1][ch] = mfma16(ah[1], bh[kb], acc[1][ch]);
+            } else {
+                acc[0][ch] = mma_p<LP>(ah[0], al[0], bh[kb], bl[kb], acc[0][ch]);
+                if (two) acc[1][ch] = mma_p<LP>(ah[1], al[1], bh[kb], bl[kb], acc[1][ch]);
+            }
 #endif
             if (kb == KLO && p > 0) {
                 lstm_point<FIRST>(prev[0], c[r0 - 2], c[r0 - 2], hout[r0 - 2]);
@@ -121,14 +130,14 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
     // fp32 mode: [layer 1|2 fragments, refilled per phase | layer 0 | misc];
     // f16 mode:  [layer 1 hi | layer 2 hi | layer 0 hi | misc], all resident
     constexpr int F0 = LP ? G::FA0 / 2 : G::FA0;
-    float *lw0 = lw + G::FA1;                   // resident layer-0 fragments
+    float *lw0 = lw + (LP ? 2 * G::FH1 : G::FA1);   // resident layer-0 fragments
     float *lfnp = lw0 + F0;                     // resident controller records
     float *lfcp = lfnp + G::FNP;                // resident fc.weight (lane layout) and fc.bias
     float *lfcb = lfcp + G::FCP;
-    float *lwl[3] = {lw0, lw, lw + G::FA1 / 2};
+    float *lwl[3] = {lw0, lw, lw + G::FH1};
     if (LP) {
-        lds_copy(lwl[1], a.p.fa[1], G::FA1 / 2);
-        lds_copy(lwl[2], a.p.fa[2], G::FA1 / 2);
+        lds_copy(lwl[1], a.p.fa[1], G::FH1);
+        lds_copy(lwl[2], a.p.fa[2], G::FH1);
     }
     lds_copy(lw0, a.p.fa[0], F0);
     lds_copy(lfnp, a.p.fnp, G::FNP);

@@ -20,6 +20,7 @@
 // exhaustively for H = 16, 32, 50 by scripts/img_swizzle_check.py.
 #pragma once
 #include "fcr_common.h"
+#include "fcr_f16.h"
 #include "fcr_pack.h"
 
 namespace fcr {
@@ -49,7 +50,11 @@ inline size_t img_bytes(int HS, int l) {
 }
 
 // One thread per (image row, column): value W[gate*H + unit][input of (σ, grp)], pre-scaled for exp2
-// like the forward fragments (the backward divides its dgates by the same per-gate factor).
+// like the forward fragments (the backward divides its dgates by the same per-gate factor). With a
+// packed tail (tail_packed, fcr_f16.h) the hi image's last k-block carries, in its padding columns
+// σ = 2HS .. 2HS+3, the copies (hi σ0, hi σ1, lo σ0, lo σ1) of its two real slots, so the recompute's
+// row read of that block IS the packed tail fragment; the transposed product never reads those
+// columns as anything but unused output rows, and the lo image keeps zeros there.
 __global__ void pack_img_kernel(PackArgs a, int l, _Float16 *dst) {
     const int H = a.H, HS = a.HS;
     const int nsl = l == 0 ? HS + 2 : 2 * HS;
@@ -62,29 +67,41 @@ __global__ void pack_img_kernel(PackArgs a, int l, _Float16 *dst) {
     const int slot = R >> 4, m = R & 15;
     const int unit = 4 * slot + (m >> 2), gate = m & 3;
     const int sg = (col >> 5) * 8 + (col & 7), grp = (col >> 3) & 3;   // combined slot, lane group
-    float v = 0.0f;
-    if (unit < H && sg < nsl) {
-        const int grow = gate * H + unit;
-        if (l == 0) {
-            if (sg < HS) {
-                const int u = 4 * sg + grp;
-                if (u < H) v = a.whh[0][grow * H + u];
-            } else if (sg == HS) {
-                v = a.wih[0][grow * kIn + grp];
-            } else if (grp == 0) {   // sg == HS + 1
-                v = a.wih[0][grow * kIn + 4];
+    auto weight = [&](int s) {
+        float v = 0.0f;
+        if (unit < H && s < nsl) {
+            const int grow = gate * H + unit;
+            if (l == 0) {
+                if (s < HS) {
+                    const int u = 4 * s + grp;
+                    if (u < H) v = a.whh[0][grow * H + u];
+                } else if (s == HS) {
+                    v = a.wih[0][grow * kIn + grp];
+                } else if (grp == 0) {   // s == HS + 1
+                    v = a.wih[0][grow * kIn + 4];
+                }
+            } else if (s < HS) {
+                const int u = 4 * s + grp;
+                if (u < H) v = a.wih[l][grow * H + u];
+            } else {
+                const int u = 4 * (s - HS) + grp;
+                if (u < H) v = a.whh[l][grow * H + u];
             }
-        } else if (sg < HS) {
-            const int u = 4 * sg + grp;
-            if (u < H) v = a.wih[l][grow * H + u];
-        } else {
-            const int u = 4 * (sg - HS) + grp;
-            if (u < H) v = a.whh[l][grow * H + u];
         }
+        return v * (gate == 2 ? kTwoLog2e : kNegLog2e);
+    };
+    _Float16 hi, lo;
+    const int jt = sg - 8 * (kbn - 1);   // position inside the last k-block
+    if (l > 0 && tail_packed(HS) && jt >= 2 && jt < 6) {
+        const float v = weight(8 * (kbn - 1) + (jt & 1));
+        const _Float16 vh = (_Float16)v;
+        hi = jt < 4 ? vh : (_Float16)(v - (float)vh);
+        lo = (_Float16)0.0f;
+    } else {
+        const float v = weight(sg);
+        hi = (_Float16)v;
+        lo = (_Float16)(v - (float)hi);
     }
-    v *= (gate == 2 ? kTwoLog2e : kNegLog2e);
-    const _Float16 hi = (_Float16)v;
-    const _Float16 lo = (_Float16)(v - (float)hi);
     const int w = (col >> 2) ^ img_swz(m, RB);
     const size_t off = (size_t)R * (RB / 2) + w * 4 + (col & 3);   // in halves
     dst[off] = hi;
