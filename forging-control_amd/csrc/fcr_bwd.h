@@ -175,16 +175,16 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
             else a2[0] += (float)ah[1] + (float)bh[kb][1];
 #else
             if (tail) {
-                if (((kb - KLO) & 1) == 0) a = mfma16(ah, bh[kb], a);
+                if (kOneAcc || ((kb - KLO) & 1) == 0) a = mfma16(ah, bh[kb], a);
                 else a2 = mfma16(ah, bh[kb], a2);
-            } else if (((kb - KLO) & 1) == 0) {
+            } else if (kOneAcc || ((kb - KLO) & 1) == 0) {
                 a = mma_p<LP>(ah, al, bh[kb], bl[kb], a);
             } else {
                 a2 = mma_p<LP>(ah, al, bh[kb], bl[kb], a2);
             }
 #endif
         }
-        if (KHI - KLO > 1) a += a2;
+        if (!kOneAcc && KHI - KLO > 1) a += a2;
     };
     // pointwise + cell gradient of slot r from its pre-activations -> 4 scaled dgates
     auto slot_grad = [&](int r, f32x4 a, float *v) {

@@ -31,16 +31,41 @@ __device__ __forceinline__ void rot_left(float (&w)[kL]) {
 #define FCR_FWD_PRIO 1
 #endif
 
+// Issue-priority pacing of the two waves that share a SIMD (waves w and w+4 of the workgroup).
+//   FCR_FWD_PRIO 1: alternate the higher priority cell by cell;
+//   FCR_FWD_PRIO 2: the younger wave always has it;
+//   FCR_FWD_PRIO 3: the wave that is AHEAD of its partner (cells done, published in LDS) yields it.
+// Every layer phase ends at a workgroup barrier (the fragment refill), so a wave that runs ahead only
+// waits there while its partner runs alone on the SIMD.
+struct Pace {
+    unsigned turn;
+    volatile int *prog;   // [8] per-wave cell counters (FCR_FWD_PRIO 3)
+    int me, cnt, other;
+};
+__device__ __forceinline__ void pace_cell(Pace &p) {
+#if FCR_FWD_PRIO == 1
+    if (p.turn & 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+    p.turn ^= 1;
+#elif FCR_FWD_PRIO == 2
+    if (p.me >= 4) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+#elif FCR_FWD_PRIO == 3
+    ++p.cnt;
+    if (p.cnt > p.other) __builtin_amdgcn_s_setprio(0);
+    else __builtin_amdgcn_s_setprio(1);
+    p.prog[p.me] = p.cnt;
+    p.other = __builtin_amdgcn_readfirstlane(p.prog[p.me ^ 4]);   // used at the next cell
+#else
+    (void)p;
+#endif
+}
+
 template <int HS, bool L0, bool FIRST, bool LP>
 __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lane, float x0, float x1,
                                            const float (&x)[HS], const float (&hp)[HS], float (&c)[HS],
-                                           float (&hout)[HS], unsigned &turn) {
-#if FCR_FWD_PRIO
-    // the two waves of a SIMD take turns at the higher issue priority, cell by cell (fcr_bwd.h)
-    if (turn & 1) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
-    turn ^= 1;
-#endif
+                                           float (&hout)[HS], Pace &turn) {
+    pace_cell(turn);
     using G = Geo16<HS>;
     constexpr int KB = L0 ? G::KB0 : G::KB1;
     constexpr int KLO = (L0 && FIRST) ? G::XBLK : 0;
@@ -81,7 +106,7 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
                 rd(r0 + 2, KLO, nh[0], nl[0]);
                 if (r1 + 2 < HS) rd(r1 + 2, KLO, nh[1], nl[1]);
             }
-            const int ch = (kb - KLO) & 1;
+            const int ch = kOneAcc ? 0 : (kb - KLO) & 1;
 #if FCR_ABLATE == 1   // diagnostic: the fragment reads and operands stay, the MFMAs go
             acc[0][ch][0] += (float)ah[0][0] + (float)bh[kb][0];
             if (two) acc[1][ch][0] += (float)ah[1][0] + (float)bh[kb][1];
@@ -104,8 +129,8 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
                 al[u] = nl[u];
             }
         }
-        prev[0] = acc[0][0] + acc[0][1];
-        prev[1] = acc[1][0] + acc[1][1];
+        prev[0] = kOneAcc ? acc[0][0] : acc[0][0] + acc[0][1];
+        prev[1] = kOneAcc ? acc[1][0] : acc[1][0] + acc[1][1];
     }
     sched_fence();
     lstm_point<FIRST>(prev[0], c[2 * NP - 2], c[2 * NP - 2], hout[2 * NP - 2]);
@@ -177,8 +202,14 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
     f32x4 *cs_wave = a.cseq + wseq;
     f32x2 *xw_wave = a.xw + (size_t)wave * N * kL * kWave;
 
-    unsigned long long st_fill = 0, st_l0 = 0, st_l12 = 0, st_head = 0;
-    unsigned turn = (threadIdx.x >> 8) & 1;   // waves w and w+4 share a SIMD: start out of phase
+    unsigned long long st_fill = 0, st_l0 = 0, st_l12 = 0, st_head = 0, st_drain = 0, st_skew1 = 0, st_dma = 0;
+    __shared__ int prog[kFwdWaves];
+    Pace turn;
+    turn.turn = (threadIdx.x >> 8) & 1;   // waves w and w+4 share a SIMD: start out of phase
+    turn.prog = prog;
+    turn.me = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    turn.cnt = turn.other = 0;
+    if (lane == 0) prog[turn.me] = 0;
     const unsigned long long st_k0 = fstamp();
     for (int j = 0; j < N; ++j) {
         const unsigned long long st_w0 = fstamp();
@@ -244,7 +275,28 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             const unsigned long long st_f0 = fstamp();
             if (l == 1) st_l0 += st_f0 - st_w1;
             if (!LP) {
+#if FCR_STAMP   // diagnostic: split the refill into store drain, barrier skew, DMA, barrier skew
+                const unsigned long long s0 = fstamp();
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const unsigned long long s1 = fstamp();
+                __builtin_amdgcn_s_barrier();
+                const unsigned long long s2 = fstamp();
+                {
+                    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+                    for (int c = wv; c < G::FA1 * 4 / 1024; c += kFwdWaves)
+                        __builtin_amdgcn_global_load_lds(
+                            (const __attribute__((address_space(1))) void *)((const char *)a.p.fa[l] + c * 1024 + lane * 16),
+                            (__attribute__((address_space(3))) void *)((__attribute__((address_space(3))) char *)lw + c * 1024), 16, 0, 0);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const unsigned long long s3 = fstamp();
+                __builtin_amdgcn_s_barrier();
+                st_drain += s1 - s0;
+                st_skew1 += s2 - s1;
+                st_dma += s3 - s2;
+#else
                 lds_fill<G::FA1 * 4, kFwdWaves>(lw, a.p.fa[l]);
+#endif
                 stagger();
             }
             const float *lwc = LP ? lwl[l] : lw;
@@ -322,6 +374,9 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
         o[2] = st_fill;
         o[3] = st_l12;
         o[4] = fstamp() - st_k0;
+        o[5] = st_drain;
+        o[6] = st_skew1;
+        o[7] = st_dma;
     }
 #endif
 }

@@ -45,3 +45,11 @@ tot = fw[:, 4].mean()
 print(f"forward: wave lifetime {tot:.3e} cycles; per window: head {fw[:, 0].mean() / N:.0f}, layer 0 "
       f"{fw[:, 1].mean() / N:.0f}, fills+barriers {fw[:, 2].mean() / N:.0f}, layers 1-2 + readout "
       f"{(tot - fw[:, 0].mean() - fw[:, 1].mean() - fw[:, 2].mean()) / N:.0f}")
+print(f"forward refills per window: store drain {fw[:, 5].mean() / N:.0f}, barrier-1 skew {fw[:, 6].mean() / N:.0f}, "
+      f"DMA {fw[:, 7].mean() / N:.0f}, barrier 2 {(fw[:, 2] - fw[:, 5] - fw[:, 6] - fw[:, 7]).mean() / N:.0f} cycles")
+sk = fw[:, 6] / N
+print("forward barrier-1 skew per window by wave slot in the workgroup:",
+      " ".join(f"{sk[i::8].mean():.0f}" for i in range(8)))
+l12 = (fw[:, 4] - fw[:, 0] - fw[:, 1] - fw[:, 2]) / N
+print("forward layers 1-2 cycles per window by wave slot:", " ".join(f"{l12[i::8].mean():.0f}" for i in range(8)))
+print("forward layer 0 cycles per window by wave slot:", " ".join(f"{(fw[:, 1] / N)[i::8].mean():.0f}" for i in range(8)))
