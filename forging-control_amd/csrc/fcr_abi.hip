@@ -626,7 +626,7 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
                            (_Float16 *)(base + L.fa[l]));
         if ((rc = launch_check("pack_fwd16_kernel"))) return rc;
         if (with_backward) {
-            const int ni = (int)(img_bytes(L.HS, l) / 4);
+            const int ni = img_pack_threads(L.HS, l);
             hipLaunchKernelGGL(pack_img_kernel, dim3((ni + 255) / 256), dim3(256), 0, s, pa, l,
                                (_Float16 *)(base + L.img[l]));
             if ((rc = launch_check("pack_img_kernel"))) return rc;

@@ -117,8 +117,8 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     using I = Img<HS, L0>;
     using G = Geo16<HS>;
     constexpr int KB = I::KB, NB = I::NB, KBB = I::KBB;
-    constexpr uint32_t TILE = 16 * I::RB;               // one slot's 16 image rows
-    constexpr uint32_t LO = (uint32_t)I::ROWS * I::RB;  // lo image
+    constexpr uint32_t TILE = I::TILE;                  // one slot's 16 image rows
+    constexpr uint32_t LO = I::HALF;                    // lo image
     constexpr int KLO = (L0 && FIRST) ? G::XBLK : 0;
     constexpr int KHI = FIRST ? (L0 ? G::XBLK + 1 : G::KX1) : KB;
 
@@ -144,16 +144,15 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     // Recomputed forward tile r: its MFMA chain, issued two regions before its result is used (two
     // accumulators over alternate k-blocks halve the dependent-MFMA chain).
     auto fwd_tile = [&](int r, f32x4 &a) {
-        // the lo image through its own (opaque) base: with a visible constant distance the compiler
-        // pairs each hi and lo read into one ds_read2st64_b64, whose banking is not conflict-free
+        // the lo image through its own (opaque) base: its reads then also fit the 16-bit ds offset
         uint32_t fbl = fb + LO;
         asm volatile("" : "+v"(fbl));
         f32x4 a2 = {0.0f, 0.0f, 0.0f, 0.0f};
         a = a2;
 #pragma unroll
         for (int kb = KLO; kb < KHI; ++kb) {
-            const uint32_t a0 = (fb ^ (8u * (8 * kb))) + r * TILE, a1 = (fb ^ (8u * (8 * kb + 1))) + r * TILE;
-            const uint32_t b0 = (fbl ^ (8u * (8 * kb))) + r * TILE, b1 = (fbl ^ (8u * (8 * kb + 1))) + r * TILE;
+            const uint32_t a0 = fb + 8u * (2 * kb) + r * TILE, a1 = fb + 8u * (2 * kb + 1) + r * TILE;
+            const uint32_t b0 = fbl + 8u * (2 * kb) + r * TILE, b1 = fbl + 8u * (2 * kb + 1) + r * TILE;
             f16x8 ah, al = {};
             const f16x4 h0 = lds_b64_f16(a0), h1 = lds_b64_f16(a1);
 #pragma unroll
@@ -257,21 +256,22 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     for (int kbb = 0; kbb < KBB; ++kbb) {
         sched_fence();
 #if FCR_BWD_LAUNDER
-        // recompute the XOR'ed image addresses in every region instead of keeping ~30 of them live
         asm volatile("" : "+v"(fb), "+v"(tb));
 #endif
+        uint32_t tbl = tb + LO;   // lo image base (opaque: keeps the reads' offsets inside 16 bits)
+        asm volatile("" : "+v"(tbl));
         const int cu = kbb & 1, nu = cu ^ 1;
         const bool two = 2 * kbb + 1 < HS;
         if (kbb + 2 < KBB) fwd_pair(kbb + 2, fa[(kbb + 2) % 3]);
 #pragma unroll
         for (int tau = 0; tau < NB; ++tau) {
-            const uint32_t at = (tb ^ (8u * (8 * (tau >> 1) + (tau & 1)))) + 2 * kbb * TILE;
+            const uint32_t ct = 8u * (2 * (tau >> 1) + (tau & 1)) + 2 * kbb * TILE;
             f16x8 ah, al;
-            const f16x4 h0 = lds_tr_f16(at), l0 = LP ? f16x4{0, 0, 0, 0} : lds_tr_f16(at + LO);
+            const f16x4 h0 = lds_tr_f16(tb + ct), l0 = LP ? f16x4{0, 0, 0, 0} : lds_tr_f16(tbl + ct);
             f16x4 h1 = {0, 0, 0, 0}, l1 = {0, 0, 0, 0};
             if (two) {
-                h1 = lds_tr_f16(at + TILE);
-                if (!LP) l1 = lds_tr_f16(at + TILE + LO);
+                h1 = lds_tr_f16(tb + ct + TILE);
+                if (!LP) l1 = lds_tr_f16(tbl + ct + TILE);
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -287,7 +287,19 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
 #if FCR_ABLATE == 1
             acc[tau][0] += (float)ah[0] + (float)gh[cu][0];
 #else
-            acc[tau] = mma_p<LP>(ah, al, gh[cu], gl[cu], acc[tau]);
+            if (!two && !LP) {
+                // half block (odd HS: its second slot is padding, k 4..7 of every group zero): the
+                // hi·hi and hi·lo products share ONE MFMA over k = [W_hi d_hi | W_hi d_lo], then lo·hi
+                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 h = __builtin_bit_cast(u32x4, gh[cu]), l = __builtin_bit_cast(u32x4, gl[cu]);
+                f16x8 a2;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) a2[k] = a2[4 + k] = h0[k];
+                acc[tau] = mfma16(a2, __builtin_bit_cast(f16x8, u32x4{h[0], h[1], l[0], l[1]}), acc[tau]);
+                acc[tau] = mfma16(al, gh[cu], acc[tau]);
+            } else {
+                acc[tau] = mma_p<LP>(ah, al, gh[cu], gl[cu], acc[tau]);
+            }
 #endif
         }
         if (kbb + 1 < KBB) dgate_block(kbb + 1, fa[(kbb + 1) % 3], gh[nu], gl[nu]);
@@ -315,16 +327,17 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     }
 }
 
-// fp32 mode: [layer 2|1 image (hi, lo), refilled per phase | layer-0 image | misc];
+// fp32 mode: [one image region, refilled per phase (layer 2, 1, 0: hi then lo) | misc];
 // f16 mode:  [layer 2 hi | layer 1 hi | layer 0 hi | misc], all resident (no refills)
 template <int HS, bool LP>
 struct BwdLds {
-    static constexpr int IMG1 = LP ? Img<HS, false>::BYTES / 2 : Img<HS, false>::BYTES;
-    static constexpr int IMG0 = LP ? Img<HS, true>::BYTES / 2 : Img<HS, true>::BYTES;
-    static constexpr int NIMG1 = LP ? 2 : 1;
+    using I1 = Img<HS, false>;
+    using I0 = Img<HS, true>;
+    static constexpr int REGION = LP ? 2 * I1::HALF + I0::HALF : (I1::BYTES > I0::BYTES ? I1::BYTES : I0::BYTES);
     static constexpr int FNP = kMS * 4 * kFnpStride, FCP = kOut * HS * 4;
-    static constexpr int BYTES = NIMG1 * IMG1 + IMG0 + (FNP + FCP) * 4;
+    static constexpr int BYTES = REGION + (FNP + FCP) * 4;
     static_assert(BYTES <= 163840, "weight images exceed the 160 KiB LDS");
+    static_assert(I1::HALF % 16 == 0 && I0::HALF % 16 == 0, "images must be whole 16-B chunks");
 };
 
 template <int HS, bool LP>
@@ -333,15 +346,15 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
     using I1 = Img<HS, false>;
     using I0 = Img<HS, true>;
     extern __shared__ __attribute__((aligned(16))) float lw[];
-    float *lw1 = lw + (LP ? LD::IMG1 / 4 : 0);  // layer-1 image (f16 mode: resident beside layer 2's)
-    float *lw0 = lw + LD::NIMG1 * LD::IMG1 / 4; // resident layer-0 image
-    float *lfnp = lw0 + LD::IMG0 / 4;           // resident controller records
-    float *lfcp = lfnp + LD::FNP;               // resident fc.weight (lane layout)
+    float *lw1 = lw + (LP ? I1::HALF / 4 : 0);      // layer-1 image (f16 mode: resident beside layer 2's)
+    float *lw0 = lw + (LP ? 2 * I1::HALF / 4 : 0);  // layer-0 image (fp32 mode: the same refilled region)
+    float *lfnp = lw + LD::REGION / 4;              // resident controller records
+    float *lfcp = lfnp + LD::FNP;                   // resident fc.weight (lane layout)
     if (LP) {
-        lds_copy(lw, a.p.img[2], LD::IMG1 / 4);     // hi images only: the first half of each
-        lds_copy(lw1, a.p.img[1], LD::IMG1 / 4);
+        lds_copy(lw, a.p.img[2], I1::HALF / 4);     // hi images only: the first half of each
+        lds_copy(lw1, a.p.img[1], I1::HALF / 4);
+        lds_copy(lw0, a.p.img[0], I0::HALF / 4);
     }
-    lds_copy(lw0, a.p.img[0], LD::IMG0 / 4);
     lds_copy(lfnp, a.p.fnp, LD::FNP);
     lds_copy(lfcp, a.p.fcp, LD::FCP);
     __syncthreads();
@@ -359,9 +372,9 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
     const float s84 = a.states[(size_t)bc * kL * kIn + (kL - 2) * kIn + 4];
     const float *pred = a.prediction + (size_t)bc * N;
     const float *xh = a.xhat + (size_t)bc * N * kOut;
-    const ImgLane<I1::RB> L1 = img_lane<I1::RB>(lds_offset(lw), lane);      // layer 2 (fp32: layers 2, 1)
-    const ImgLane<I1::RB> L1b = img_lane<I1::RB>(lds_offset(lw1), lane);    // layer 1
-    const ImgLane<I0::RB> L0 = img_lane<I0::RB>(lds_offset(lw0), lane);
+    const ImgLane<I1::U> L1 = img_lane<I1::U>(lds_offset(lw), lane);      // layer 2 (fp32: layers 2, 1)
+    const ImgLane<I1::U> L1b = img_lane<I1::U>(lds_offset(lw1), lane);    // layer 1
+    const ImgLane<I0::U> L0 = img_lane<I0::U>(lds_offset(lw0), lane);
 
     // window-row gradients dx(w, t) (lane group q: column q; lane group 0 also column 4) go to a
     // per-wave slab; row rho = w + t of the extended sequence sums the windows that contained it.
@@ -462,7 +475,7 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         float unused0, unused1;
         const unsigned long long tw1 = stamp_now();
         if (!LP) {
-            lds_fill<LD::IMG1, kBwdWaves>(lw, a.p.img[2]);
+            lds_fill<I1::BYTES, kBwdWaves>(lw, a.p.img[2]);
             stagger();
         }
         if (FCR_STAMP) {
@@ -492,7 +505,7 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         // ---- layer 1 ----
         const unsigned long long tw3 = stamp_now();
         if (!LP) {
-            lds_fill<LD::IMG1, kBwdWaves>(lw, a.p.img[1]);
+            lds_fill<I1::BYTES, kBwdWaves>(lw, a.p.img[1]);
             stagger();
         }
         if (FCR_STAMP) sp.t[7] += stamp_now() - tw3;
@@ -510,6 +523,10 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
                                                         unused1, ci, next_of(j, 1, 0), sp);
         store_quads<HS>(dseq_w + doff(j, 1, 0), dxo, lane);
         // ---- layer 0: dx -> window-row gradients ----
+        if (!LP) {
+            lds_fill<I0::BYTES, kBwdWaves>(lw, a.p.img[0]);
+            stagger();
+        }
 #pragma unroll
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
         for (int t = kL - 1; t >= 2; --t) {

@@ -203,13 +203,19 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
     f32x2 *xw_wave = a.xw + (size_t)wave * N * kL * kWave;
 
     unsigned long long st_fill = 0, st_l0 = 0, st_l12 = 0, st_head = 0, st_drain = 0, st_skew1 = 0, st_dma = 0;
-    __shared__ int prog[kFwdWaves];
     Pace turn;
     turn.turn = (threadIdx.x >> 8) & 1;   // waves w and w+4 share a SIMD: start out of phase
-    turn.prog = prog;
     turn.me = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     turn.cnt = turn.other = 0;
+#if FCR_FWD_PRIO == 3
+    // (diagnostic only: a static __shared__ array shifts the dynamic LDS base, which the b128 fragment
+    // reads need 16-B aligned — 32 B keeps it aligned)
+    __shared__ __attribute__((aligned(16))) int prog[kFwdWaves];
+    turn.prog = prog;
     if (lane == 0) prog[turn.me] = 0;
+#else
+    turn.prog = nullptr;
+#endif
     const unsigned long long st_k0 = fstamp();
     for (int j = 0; j < N; ++j) {
         const unsigned long long st_w0 = fstamp();
