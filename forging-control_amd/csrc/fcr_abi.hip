@@ -178,6 +178,9 @@ int launch_bwd(const BwdArgs &ba, const Layout &L, bool lp, hipStream_t s) {
 struct WideLayout {
     size_t wih[3], whh[3], fcw, fcb, cwi, cbi, cwo, fcp, fcbo, fnp, xhat, tot, cmd, err, X0, Hs, Cs, G;
     size_t Act, dH, dC, D[2], rowg, dv, fnn_part, total;
+    // split-f16 gate GEMM operands (fcr_wide.h: forward A per layer, backward A per weight, the cells'
+    // operand rows XB [3][10][B][6H], the dgate rows [B][12H]; layer 0's W_ih, K = 5, stays fp32)
+    size_t fa[3], bih[3], bhh[3], XB, dGsp, consts;
     int ctrl_blocks;
 };
 
@@ -210,7 +213,18 @@ WideLayout make_wide(const fcr_dims *d, int with_backward) {
     L.Hs = take(F * kLayers * kL * B * H);
     L.Cs = take(F * kLayers * kL * B * H);
     L.G = take(F * B * 4 * H);
+    const size_t F16 = sizeof(_Float16), WW = 4 * H * H;
+    for (int l = 0; l < kLayers; ++l) {
+        L.fa[l] = take(F16 * WW * (l == 0 ? 3 : 6));
+        if (with_backward) {
+            if (l > 0) L.bih[l] = take(F16 * 3 * WW);
+            L.bhh[l] = take(F16 * 3 * WW);
+        }
+    }
+    L.XB = take(F16 * kLayers * kL * B * 6 * H);
     if (with_backward) {
+        L.dGsp = take(F16 * B * 12 * H);
+        L.consts = take(F * 4);
         L.Act = take(F * kLayers * kL * B * 4 * H);
         L.dH = take(F * B * H);
         L.dC = take(F * B * H);
@@ -247,6 +261,69 @@ int gemm_gw(rocblas_handle h, int B, int H4, int K, const float *W, const float 
     return st == rocblas_status_success ? FCR_OK : fail(FCR_EHIP, "rocblas_sgemm (backward) failed: %d", (int)st);
 }
 
+// G (row-major B x 4H) (+)= XB A^T on split-f16 operands, fp32 accumulate: A row-major [4H][lda] (the
+// forward A of fcr_wide.h), XB row-major [B][ldb]; K = the concatenated split length (3H per input part).
+int gemm16_fwd(rocblas_handle h, int B, int H4, int K, const _Float16 *A, int lda, const _Float16 *XB, int ldb,
+               float beta, float *G) {
+    const float one = 1.0f;
+    const rocblas_status st = rocblas_gemm_ex(h, rocblas_operation_transpose, rocblas_operation_none, H4, B, K, &one, A,
+                                              rocblas_datatype_f16_r, lda, XB, rocblas_datatype_f16_r, ldb, &beta, G,
+                                              rocblas_datatype_f32_r, H4, G, rocblas_datatype_f32_r, H4,
+                                              rocblas_datatype_f32_r, rocblas_gemm_algo_standard, 0, 0);
+    return st == rocblas_status_success ? FCR_OK : fail(FCR_EHIP, "rocblas_gemm_ex (forward, f16 split) failed: %d", (int)st);
+}
+// dX (row-major B x H) = dGs A on split-f16 operands: A row-major [12H][H] = [W_hi ; W_hi ; W_lo], dGs row-major
+// [B][12H] = [hi | lo | hi] of dG * scale; consts (device) = [alpha = 1/scale, 0, 1, scale].
+int gemm16_bwd(rocblas_handle h, int B, int H, const _Float16 *A, const _Float16 *dGs, const float *consts, float *dX) {
+    rocblas_set_pointer_mode(h, rocblas_pointer_mode_device);
+    const rocblas_status st = rocblas_gemm_ex(h, rocblas_operation_none, rocblas_operation_none, H, B, 12 * H, consts, A,
+                                              rocblas_datatype_f16_r, H, dGs, rocblas_datatype_f16_r, 12 * H, consts + 1,
+                                              dX, rocblas_datatype_f32_r, H, dX, rocblas_datatype_f32_r, H,
+                                              rocblas_datatype_f32_r, rocblas_gemm_algo_standard, 0, 0);
+    rocblas_set_pointer_mode(h, rocblas_pointer_mode_host);
+    return st == rocblas_status_success ? FCR_OK : fail(FCR_EHIP, "rocblas_gemm_ex (backward, f16 split) failed: %d", (int)st);
+}
+
+// Device pointers of the split-f16 operands (rollout only; the surrogate's training step stays fp32)
+struct WideSplit {
+    const _Float16 *fa[kLayers], *bih[kLayers], *bhh[kLayers];
+    _Float16 *XB, *dGsp;
+    float *consts;
+};
+
+WideSplit wide_split(const WideLayout &L, char *base) {
+    WideSplit w{};
+    for (int l = 0; l < kLayers; ++l) {
+        w.fa[l] = (const _Float16 *)(base + L.fa[l]);
+        w.bih[l] = L.bih[l] ? (const _Float16 *)(base + L.bih[l]) : nullptr;
+        w.bhh[l] = L.bhh[l] ? (const _Float16 *)(base + L.bhh[l]) : nullptr;
+    }
+    w.XB = (_Float16 *)(base + L.XB);
+    w.dGsp = L.dGsp ? (_Float16 *)(base + L.dGsp) : nullptr;
+    w.consts = L.consts ? (float *)(base + L.consts) : nullptr;
+    return w;
+}
+
+// Pack the split-f16 GEMM operands of the current weights (fcr_wide.h layouts)
+int wide_pack_split(const float *const *w_ih, const float *const *w_hh, int H, bool backward, const WideSplit &sp,
+                    hipStream_t s) {
+    const size_t WW = (size_t)4 * H * H;
+    int rc;
+    for (int l = 0; l < kLayers; ++l) {
+        const size_t n = WW * (l == 0 ? 3 : 6);
+        hipLaunchKernelGGL(wide_split_fa_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                           l == 0 ? (const float *)nullptr : w_ih[l], w_hh[l], H, (_Float16 *)sp.fa[l]);
+        if ((rc = launch_check("wide_split_fa_kernel"))) return rc;
+        if (!backward) continue;
+        for (int k = (l == 0 ? 1 : 0); k < 2; ++k) {
+            hipLaunchKernelGGL(wide_split_ba_kernel, dim3((unsigned)((3 * WW + 255) / 256)), dim3(256), 0, s,
+                               k == 0 ? w_ih[l] : w_hh[l], H, (_Float16 *)(k == 0 ? sp.bih[l] : sp.bhh[l]));
+            if ((rc = launch_check("wide_split_ba_kernel"))) return rc;
+        }
+    }
+    return FCR_OK;
+}
+
 WideArgs wide_args(const fcr_dims *d, const WideLayout &L, char *base) {
     WideArgs a{};
     a.B = d->B;
@@ -275,24 +352,48 @@ WideArgs wide_args(const fcr_dims *d, const WideLayout &L, char *base) {
     return a;
 }
 
-// One window's cells, forward: 3 layers x 10 steps of [GEMM x_t W_ih^T, GEMM h_{t-1} W_hh^T, cell]
+// One window's cells, forward: 3 layers x 10 steps of [GEMM x_t W_ih^T, GEMM h_{t-1} W_hh^T, cell].
+// sp != nullptr (the rollout): the H-wide products as ONE K-concatenated split-f16 GEMM per cell (gemm16_fwd) — ~3x the fp32
+// GEMM rate at equal accuracy; sp == nullptr (the surrogate's training step): fp32 rocBLAS throughout.
 int wide_cells(rocblas_handle h, const WideArgs &a, const float *const *w_ih, const float *const *w_hh, bool keep_act,
-               hipStream_t s) {
+               const WideSplit *sp, hipStream_t s) {
     const int B = a.B, H = a.H;
     const size_t cell = (size_t)B * H;
     const int nb = (int)((cell + 255) / 256);
+    // operand rows of cell (l, t): layer >= 1 [x part 3H | h part 3H], layer 0 [h part 3H]
+    auto ldx = [&](int l) { return l == 0 ? 3 * H : 6 * H; };
+    auto xb = [&](int l, int t) { return sp->XB + ((size_t)l * kL + t) * B * 6 * H; };
     int rc;
     for (int l = 0; l < kLayers; ++l) {
         const float *wih = w_ih[l], *whh = w_hh[l];
         for (int t = 0; t < kL; ++t) {
             const float *x = l == 0 ? a.X0 + (size_t)t * B * kIn : a.Hs + ((size_t)(l - 1) * kL + t) * cell;
-            if ((rc = gemm_xwt(h, B, 4 * H, l == 0 ? kIn : H, wih, x, 0.0f, a.G))) return rc;
-            if (t > 0 && (rc = gemm_xwt(h, B, 4 * H, H, whh, a.Hs + ((size_t)l * kL + t - 1) * cell, 1.0f, a.G)))
-                return rc;
-            hipLaunchKernelGGL(wide_cell_kernel, dim3(nb), dim3(256), 0, s, (const float *)a.G,
+            // split path with keep_act (the backward's recompute): the gate pre-activations stay per cell in
+            // the Act slab (wide_cell_bwd_kernel<true> rebuilds the activations) instead of a second array
+            float *G = (sp && keep_act) ? a.Act + ((size_t)l * kL + t) * cell * 4 : a.G;
+            if (sp) {
+                if (l == 0) {
+                    if ((rc = gemm_xwt(h, B, 4 * H, kIn, wih, x, 0.0f, G))) return rc;
+                    if (t > 0 && (rc = gemm16_fwd(h, B, 4 * H, 3 * H, sp->fa[0], 3 * H, xb(0, t), 3 * H, 1.0f, G)))
+                        return rc;
+                } else if ((rc = gemm16_fwd(h, B, 4 * H, t > 0 ? 6 * H : 3 * H, sp->fa[l], 6 * H, xb(l, t), 6 * H, 0.0f,
+                                            G))) {
+                    return rc;
+                }
+            } else {
+                if ((rc = gemm_xwt(h, B, 4 * H, l == 0 ? kIn : H, wih, x, 0.0f, a.G))) return rc;
+                if (t > 0 && (rc = gemm_xwt(h, B, 4 * H, H, whh, a.Hs + ((size_t)l * kL + t - 1) * cell, 1.0f, a.G)))
+                    return rc;
+            }
+            _Float16 *xh = (sp && t + 1 < kL) ? xb(l, t + 1) + (l == 0 ? 0 : 3 * H) : nullptr;   // next cell's h part
+            _Float16 *xx = (sp && l + 1 < kLayers) ? xb(l + 1, t) : nullptr;                       // layer above's x part
+            // the split path reads h only through the operand rows; fp32 h is kept for the readout (2, 9)
+            float *hout = (!sp || (l == kLayers - 1 && t == kL - 1)) ? a.Hs + ((size_t)l * kL + t) * cell : nullptr;
+            hipLaunchKernelGGL(wide_cell_kernel, dim3(nb), dim3(256), 0, s, (const float *)G,
                                t > 0 ? (const float *)(a.Cs + ((size_t)l * kL + t - 1) * cell) : nullptr,
-                               a.Cs + ((size_t)l * kL + t) * cell, a.Hs + ((size_t)l * kL + t) * cell,
-                               keep_act ? a.Act + ((size_t)l * kL + t) * cell * 4 : nullptr, B, H);
+                               a.Cs + ((size_t)l * kL + t) * cell, hout,
+                               (keep_act && !sp) ? a.Act + ((size_t)l * kL + t) * cell * 4 : nullptr, xh, ldx(l), xx,
+                               ldx(l + 1 < kLayers ? l + 1 : l), B, H);
             if ((rc = launch_check("wide_cell_kernel"))) return rc;
         }
     }
@@ -331,6 +432,8 @@ int wide_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const 
     hipLaunchKernelGGL(pack_misc_kernel, dim3(2), dim3(256), 0, s, pa);
     if ((rc = launch_check("pack_misc_kernel"))) return rc;
 
+    const WideSplit sp = wide_split(L, base);
+    if ((rc = wide_pack_split(w->w_ih, w->w_hh, (int)H, with_backward != 0, sp, s))) return rc;
     rocblas_handle h = blas_on(s);
     if (!h) return fail(FCR_EHIP, "rocblas_create_handle failed");
     WideArgs a = wide_args(d, L, base);
@@ -348,7 +451,7 @@ int wide_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const 
     for (int j = 0; j < d->N; ++j) {
         hipLaunchKernelGGL(wide_window_kernel<true>, dim3(nb), dim3(256), 0, s, a, j);
         if ((rc = launch_check("wide_window_kernel"))) return rc;
-        if ((rc = wide_cells(h, a, wih, whh, false, s))) return rc;
+        if ((rc = wide_cells(h, a, wih, whh, false, &sp, s))) return rc;
         hipLaunchKernelGGL(wide_readout_kernel, dim3(nb), dim3(256), 0, s, a, j,
                            (const float *)(a.Hs + ((size_t)2 * kL + kL - 1) * d->B * H));
         if ((rc = launch_check("wide_readout_kernel"))) return rc;
@@ -382,29 +485,34 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
     }
     if (hipMemsetAsync(a.rowg, 0, sizeof(float) * (size_t)(d->N + kL - 1) * B * kIn, s) != hipSuccess)
         return fail(FCR_EHIP, "hipMemsetAsync failed");
+    const WideSplit sp = wide_split(L, base);
+    int kexp = 0;   // 2^kexp ~ B N: the dgates' scale into the f16 range (wide_bscale_kernel)
+    while (kexp < 60 && (1LL << kexp) < (long long)B * d->N) ++kexp;
+    hipLaunchKernelGGL(wide_bscale_kernel, dim3(1), dim3(64), 0, s, dloss, kexp, sp.consts);
+    if ((rc = launch_check("wide_bscale_kernel"))) return rc;
     for (int j = d->N - 1; j >= 0; --j) {
         hipLaunchKernelGGL(wide_head_kernel, dim3(nb), dim3(256), 0, s, a, j);
         if ((rc = launch_check("wide_head_kernel"))) return rc;
         hipLaunchKernelGGL(wide_window_kernel<false>, dim3(nb), dim3(256), 0, s, a, j);
         if ((rc = launch_check("wide_window_kernel"))) return rc;
-        if ((rc = wide_cells(h, a, wih, whh, true, s))) return rc;   // checkpoint: recompute the window
+        if ((rc = wide_cells(h, a, wih, whh, true, &sp, s))) return rc;   // checkpoint: recompute the window
         for (int l = kLayers - 1; l >= 0; --l) {
             if (l < kLayers - 1 && hipMemsetAsync(a.dH, 0, sizeof(float) * cell, s) != hipSuccess)
                 return fail(FCR_EHIP, "hipMemsetAsync failed");
             if (hipMemsetAsync(a.dC, 0, sizeof(float) * cell, s) != hipSuccess) return fail(FCR_EHIP, "hipMemsetAsync failed");
             for (int t = kL - 1; t >= 0; --t) {
                 const size_t c_off = ((size_t)l * kL + t) * cell;
-                hipLaunchKernelGGL(wide_cell_bwd_kernel, dim3(nc), dim3(256), 0, s, (const float *)(a.Act + c_off * 4),
+                hipLaunchKernelGGL(wide_cell_bwd_kernel<true>, dim3(nc), dim3(256), 0, s, (const float *)(a.Act + c_off * 4),
                                    (const float *)(a.Cs + c_off), t > 0 ? (const float *)(a.Cs + c_off - cell) : nullptr,
                                    (const float *)a.dH, l < kLayers - 1 ? (const float *)(D[l] + (size_t)t * cell) : nullptr,
-                                   a.dC, a.G, B, H);
+                                   a.dC, l == 0 ? a.G : nullptr, sp.dGsp, (const float *)sp.consts, B, H);
                 if ((rc = launch_check("wide_cell_bwd_kernel"))) return rc;
                 if (l > 0) {
-                    if ((rc = gemm_gw(h, B, 4 * H, H, wih[l], a.G, 0.0f, D[l - 1] + (size_t)t * cell))) return rc;
-                } else {   // layer 0: the window rows' gradients, row j + t
+                    if ((rc = gemm16_bwd(h, B, H, sp.bih[l], sp.dGsp, sp.consts, D[l - 1] + (size_t)t * cell))) return rc;
+                } else {   // layer 0: the window rows' gradients, row j + t (K = 5: fp32)
                     if ((rc = gemm_gw(h, B, 4 * H, kIn, wih[l], a.G, 1.0f, a.rowg + (size_t)(j + t) * B * kIn))) return rc;
                 }
-                if (t > 0 && (rc = gemm_gw(h, B, 4 * H, H, whh[l], a.G, 0.0f, a.dH))) return rc;
+                if (t > 0 && (rc = gemm16_bwd(h, B, H, sp.bhh[l], sp.dGsp, sp.consts, a.dH))) return rc;
             }
         }
     }
@@ -752,7 +860,7 @@ int fcr_lstm_forward(const fcr_dims *d, const fcr_weights *w, const float *x, fl
     rocblas_handle h = blas_on(s);
     if (!h) return fail(FCR_EHIP, "rocblas_create_handle failed");
     const WideArgs a = lstm_args(d, L, base);
-    if ((rc = wide_cells(h, a, w->w_ih, w->w_hh, with_backward != 0, s))) return rc;
+    if ((rc = wide_cells(h, a, w->w_ih, w->w_hh, with_backward != 0, nullptr, s))) return rc;
     hipLaunchKernelGGL(surrogate::readout_kernel, dim3((B + 255) / 256), dim3(256), 0, s,
                        (const float *)(a.Hs + ((size_t)(kLayers - 1) * kL + kL - 1) * B * H), w->fc_w, w->fc_b, y, B, H);
     return launch_check("readout_kernel");
@@ -798,10 +906,10 @@ int fcr_lstm_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, 
         for (int t = kL - 1; t >= 0; --t) {
             const size_t c_off = ((size_t)l * kL + t) * cell;
             float *dG = dGs + (size_t)t * gcell;
-            hipLaunchKernelGGL(wide_cell_bwd_kernel, dim3(nc), dim3(256), 0, s, (const float *)(a.Act + c_off * 4),
+            hipLaunchKernelGGL(wide_cell_bwd_kernel<false>, dim3(nc), dim3(256), 0, s, (const float *)(a.Act + c_off * 4),
                                (const float *)(a.Cs + c_off), t > 0 ? (const float *)(a.Cs + c_off - cell) : nullptr,
                                (const float *)a.dH, l < kLayers - 1 ? (const float *)(D[l] + (size_t)t * cell) : nullptr,
-                               a.dC, dG, B, H);
+                               a.dC, dG, (_Float16 *)nullptr, (const float *)nullptr, B, H);
             if ((rc = launch_check("wide_cell_bwd_kernel"))) return rc;
             if (l > 0) {
                 if ((rc = gemm_gw(h, B, 4 * H, H, w->w_ih[l], dG, 0.0f, D[l - 1] + (size_t)t * cell))) return rc;

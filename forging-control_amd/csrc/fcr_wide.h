@@ -82,8 +82,11 @@ __global__ void wide_window_kernel(WideArgs a, int j) {
 // backward's recompute, the activations. tanh is the library's (a few ulp RELATIVE to tanh): these
 // memory-bound kernels can afford it, and the weight gradients of the surrogate step need it when the
 // hidden states are small (1 - 2/(1 + e^{2x}) is only accurate to ~1e-7 absolute).
+// xb_h / xb_x (split-f16 path, else null): the GEMM operand rows that take this h — the h part of the
+// same layer's next cell and the x part of the layer above's cell t — as (hi, lo, hi), row strides sh / sx.
 __global__ void wide_cell_kernel(const float *__restrict__ G, const float *__restrict__ c_prev, float *c_out,
-                                 float *h_out, float *act, int B, int H) {
+                                 float *h_out, float *act, _Float16 *xb_h, int sh, _Float16 *xb_x, int sx, int B,
+                                 int H) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (size_t)B * H) return;
     const size_t b = idx / H, u = idx % H;
@@ -91,7 +94,23 @@ __global__ void wide_cell_kernel(const float *__restrict__ G, const float *__res
     const float i = sigm(g4[0]), f = sigm(g4[H]), g = tanhf(g4[2 * H]), o = sigm(g4[3 * H]);
     const float c = (c_prev ? f * c_prev[idx] : 0.0f) + i * g;
     c_out[idx] = c;
-    h_out[idx] = o * tanhf(c);
+    const float h = o * tanhf(c);
+    if (h_out) h_out[idx] = h;
+    if (xb_h || xb_x) {
+        const _Float16 hi = (_Float16)h, lo = (_Float16)(h - (float)hi);
+        if (xb_h) {
+            _Float16 *o = xb_h + b * sh + u;
+            o[0] = hi;
+            o[H] = lo;
+            o[2 * H] = hi;
+        }
+        if (xb_x) {
+            _Float16 *o = xb_x + b * sx + u;
+            o[0] = hi;
+            o[H] = lo;
+            o[2 * H] = hi;
+        }
+    }
     if (act) {
         float *a4 = act + b * 4 * H + u;
         a4[0] = i;
@@ -176,24 +195,84 @@ __global__ void wide_head_kernel(WideArgs a, int j) {
 
 // Backward of one cell: from the activations, c_t, c_{t-1}, the incoming dh (carried dH + din from the
 // layer above) and the carried dc: d loss / d (gate pre-activations) into dG, and dc_{t-1} into dC.
+// act: the gate activations (i, f, g, o) kept by the recompute, or with PRE their pre-activations (the
+// split-f16 rollout keeps the GEMM output per cell instead of writing a second 4H-wide array), from which
+// the activations are rebuilt with the forward's arithmetic. dG (fp32) may be null when only dgsp is used.
+template <bool PRE>
 __global__ void wide_cell_bwd_kernel(const float *__restrict__ act, const float *__restrict__ c,
                                      const float *__restrict__ c_prev, const float *__restrict__ dH,
-                                     const float *__restrict__ din, float *dC, float *dG, int B, int H) {
+                                     const float *__restrict__ din, float *dC, float *dG, _Float16 *dgsp,
+                                     const float *__restrict__ consts, int B, int H) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (size_t)B * H) return;
     const size_t b = idx / H, u = idx % H;
     const float *a4 = act + b * 4 * H + u;
-    const float i = a4[0], f = a4[H], g = a4[2 * H], o = a4[3 * H];
+    const float i = PRE ? sigm(a4[0]) : a4[0], f = PRE ? sigm(a4[H]) : a4[H], g = PRE ? tanhf(a4[2 * H]) : a4[2 * H],
+                o = PRE ? sigm(a4[3 * H]) : a4[3 * H];
     const float tc = tanhf(c[idx]);
     const float cp = c_prev ? c_prev[idx] : 0.0f;
     const float dh = dH[idx] + (din ? din[idx] : 0.0f);
     const float dct = dC[idx] + dh * o * (1.0f - tc * tc);
-    float *d4 = dG + b * 4 * H + u;
-    d4[0] = dct * g * i * (1.0f - i);
-    d4[H] = dct * cp * f * (1.0f - f);
-    d4[2 * H] = dct * i * (1.0f - g * g);
-    d4[3 * H] = dh * tc * o * (1.0f - o);
+    const float dg4[4] = {dct * g * i * (1.0f - i), dct * cp * f * (1.0f - f), dct * i * (1.0f - g * g),
+                          dh * tc * o * (1.0f - o)};
+    if (dG) {
+        float *d4 = dG + b * 4 * H + u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d4[k * H] = dg4[k];
+    }
+    if (dgsp) {   // split-f16 operand row [hi | lo | hi] of W^T dG, scaled into the f16 range (wide_bscale_kernel)
+        const float sc = consts[3];
+        _Float16 *o16 = dgsp + b * 12 * H + u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float v = dg4[k] * sc;
+            const _Float16 hi = (_Float16)v;
+            o16[k * H] = hi;
+            o16[(4 + k) * H] = (_Float16)(v - (float)hi);
+            o16[(8 + k) * H] = hi;
+        }
+    }
     dC[idx] = dct * f;
+}
+
+// Split-f16 operands of the config-5 gate GEMMs (fp32-accurate on the matrix cores, as fcr_f16.h does
+// for the fused kernels): every product a.b becomes a_hi b_hi + a_hi b_lo + a_lo b_hi, laid out as ONE
+// K-concatenated GEMM per cell so the fp32 gate matrix is written once (C traffic, not the MFMA, bounded
+// the per-term calls). Forward A, row-major [4H][6H] = [Wih_hi | Wih_hi | Wih_lo | Whh_hi | Whh_hi | Whh_lo]
+// against operand rows [x_hi | x_lo | x_hi | h_hi | h_lo | h_hi] (layer 0: the W_hh half only, its K = 5
+// input product stays fp32); backward A, row-major [12H][H] = [W_hi ; W_hi ; W_lo] against
+// [dG_hi | dG_lo | dG_hi].
+__global__ void wide_split_fa_kernel(const float *__restrict__ Wih, const float *__restrict__ Whh, int H,
+                                     _Float16 *dst) {
+    const int KA = Wih ? 6 * H : 3 * H;
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)4 * H * KA) return;
+    const int r = (int)(idx / KA), k = (int)(idx % KA);
+    const int part = Wih ? k / (3 * H) : 1, kk = k % (3 * H), term = kk / H, u = kk % H;
+    const float v = (part == 0 ? Wih : Whh)[(size_t)r * H + u];
+    const _Float16 hi = (_Float16)v;
+    dst[idx] = term < 2 ? hi : (_Float16)(v - (float)hi);
+}
+__global__ void wide_split_ba_kernel(const float *__restrict__ W, int H, _Float16 *dst) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t n = (size_t)4 * H * H;
+    if (idx >= 3 * n) return;
+    const int term = (int)(idx / n);
+    const float v = W[idx % n];
+    const _Float16 hi = (_Float16)v;
+    dst[idx] = term < 2 ? hi : (_Float16)(v - (float)hi);
+}
+
+// The dgates are split as dG * 2^k / dloss (|dG| ~ dloss / (B N): without it they would sit in the f16
+// subnormals); the backward GEMMs take alpha = dloss * 2^-k from device memory. consts = [alpha, 0, 1, scale].
+__global__ void wide_bscale_kernel(const float *__restrict__ dloss, int k, float *consts) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const float d = dloss[0];
+    const bool ok = d != 0.0f && isfinite(d);
+    consts[0] = ok ? ldexpf(d, -k) : 0.0f;
+    consts[1] = 0.0f;
+    consts[2] = 1.0f;
+    consts[3] = ok ? ldexpf(1.0f, k) / d : 0.0f;
 }
 
 // d loss / d u0 (Functions.py:1396 row 9 col 4, and the command costs cmd_0, cmd_1)
