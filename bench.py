@@ -149,10 +149,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl")
     dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+    torch.cuda.set_device(dev)            # before the process group: RCCL binds each rank to its own GPU
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
     B, N, H = args.batch, args.horizon, args.hidden
 
     sim, ctrl = load_weights(dev, H)
