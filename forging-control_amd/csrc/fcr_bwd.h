@@ -16,18 +16,6 @@
 
 namespace fcr {
 
-// d loss / d (gate pre-activations) of one unit slot, and the carried dc (torch LSTM semantics), from
-// P = (dh/dc, dh/do, dc/di, dc/df), Q = (dc/dg, f).
-__device__ __forceinline__ void cell_grad(const f32x4 P, const f32x2 Q, float dh, float &dc_rec, float &di,
-                                          float &df, float &dg, float &dO) {
-    const float dc = dc_rec + dh * P[0];
-    dO = dh * P[1];
-    di = dc * P[2];
-    df = dc * P[3];
-    dg = dc * Q[0];
-    dc_rec = dc * Q[1];
-}
-
 // Inputs of one backward cell, fetched one cell ahead: each register group is refilled for the next
 // cell right after this cell consumed it (x, h_{t-1}, din at the top, c_{t-1} quad by quad).
 template <int HS>
@@ -122,7 +110,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     constexpr int KLO = (L0 && FIRST) ? G::XBLK : 0;
     constexpr int KHI = FIRST ? (L0 ? G::XBLK + 1 : G::KX1) : KB;
 
-    float up, down, sg0;   // the trajectory's power-of-two scale, set once the incoming dh is in
+    float up, down, sg0, sgg;   // the trajectory's power-of-two scale, set once the incoming dh is in
 
     // packed tail block (fcr_f16.h, fcr_img.h): its hi-image row read is the packed fragment
     constexpr bool TAIL = !L0 && G::TAIL1;
@@ -185,17 +173,26 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
         }
         if (!kOneAcc && KHI - KLO > 1) a += a2;
     };
-    // pointwise + cell gradient of slot r from its pre-activations -> 4 scaled dgates
-    auto slot_grad = [&](int r, f32x4 a, float *v) {
+    // pointwise + cell gradient of slot r from its pre-activations -> the 4 dgates as (scaled factor,
+    // local derivative) pairs, multiplied inside the split (split8p): (dc s, dc/di), (dc s, dc/df),
+    // (dc s_g, dc/dg), (dh s, dh/do) — s = the trajectory scale over the exp2 pre-scale of i, f, o rows,
+    // s_g = -s/2 for the g rows (their pre-scale is -2x that of i, f, o: exact)
+    auto slot_grad = [&](int r, f32x4 a, float *va, float *vb) {
         f32x4 P;
         f32x2 Q;
         lstm_point_grad<FIRST>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], P, Q);
-        float di, df, dg, dO;
-        cell_grad(P, Q, dh[r], dc[r], di, df, dg, dO);
-        v[0] = di;              // the trajectory scale (and the exp2 pre-scale) is applied in the split;
-        v[1] = df;              // the g row's pre-scale is -2x that of i, f, o: exact
-        v[2] = dg * -0.5f;
-        v[3] = dO;
+        // torch LSTM semantics: dc = dc_carried + dh dh/dc; the carried dc of the cell below is dc f
+        const float dcv = fmaf(dh[r], P[0], dc[r]);
+        dc[r] = dcv * Q[1];
+        const float dcs = dcv * sg0;
+        va[0] = dcs;
+        vb[0] = P[2];
+        va[1] = dcs;
+        vb[1] = P[3];
+        va[2] = dcv * sgg;
+        vb[2] = Q[0];
+        va[3] = dh[r] * sg0;
+        vb[3] = P[1];
         // c_{t-1} quad of slots 4k..4k+3 consumed: the next cell's comes in
         if (NX_HC && (r & 3) == 3)
             ci.c[r >> 2] = buf_ld4(nx.rc, lane * 16, nx.c + (r >> 2) * kWave * 16);
@@ -211,17 +208,18 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     };
     // dgate block kbb (B operand of the transposed product) from the pair's pre-activations
     auto dgate_block = [&](int kbb, const f32x4 (&fp)[2], f16x8 &gh, f16x8 &gl) {
-        float v[8];
+        float va[8], vb[8];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int r = 2 * kbb + u;
             if (r < HS) {
-                slot_grad(r, fp[u], v + 4 * u);
+                slot_grad(r, fp[u], va + 4 * u, vb + 4 * u);
             } else {
-                v[4 * u] = v[4 * u + 1] = v[4 * u + 2] = v[4 * u + 3] = 0.0f;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) va[4 * u + k] = vb[4 * u + k] = 0.0f;
             }
         }
-        split_p<LP>(v, sg0, gh, gl);
+        split_pp<LP>(va, vb, gh, gl);
     };
 
     // Pipeline: region kbb issues the forward MFMAs of pair kbb+2, the transposed products of dgate
@@ -247,7 +245,8 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
         const int e = max(__builtin_amdgcn_frexp_expf(m), -100);   // m < 2^e; all-zero -> e = 0
         up = __builtin_amdgcn_ldexpf(1.0f, 13 - e);
         down = __builtin_amdgcn_ldexpf(1.0f, e - 13);
-        sg0 = up * kInvNegLog2e;   // dgate scale (the g row's -0.5 is applied per slot)
+        sg0 = up * kInvNegLog2e;   // dgate scale of the i, f, o rows
+        sgg = sg0 * -0.5f;         // and of the g rows
     }
     load_xhd<HS, NX_L0, NX_HC, NX_DIN>(ci, nx, lane);   // x, h, din of this cell are consumed
     dgate_block(0, fa[0], gh[0], gl[0]);

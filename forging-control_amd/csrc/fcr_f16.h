@@ -116,12 +116,52 @@ __device__ __forceinline__ void cvt8s(const float (&v)[8], float s, f16x8 &hi) {
     hi = __builtin_bit_cast(f16x8, h);
 }
 
+// a·b -> (hi, lo) halves, 8 at a time: the product is formed exactly inside v_fma_mix, so hi = f16(a·b)
+// and lo = f16(a·b - hi) cost the same two instructions per value as split8s with no separate multiply
+// (the backward's dgates: a = the scaled dc or dh, b = the local derivative).
+__device__ __forceinline__ void split8p(const float (&a)[8], const float (&b)[8], f16x8 &hi, f16x8 &lo) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 h, l;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        unsigned hp, lp;
+        asm("v_fma_mixlo_f16 %0, %1, %2, 0\n\t"
+            "v_fma_mixhi_f16 %0, %3, %4, 0"
+            : "=&v"(hp) : "v"(a[2 * p]), "v"(b[2 * p]), "v"(a[2 * p + 1]), "v"(b[2 * p + 1]));
+        asm("v_fma_mixlo_f16 %0, %1, %2, -%5 op_sel_hi:[0,0,1]\n\t"
+            "v_fma_mixhi_f16 %0, %3, %4, -%5 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+            : "=&v"(lp) : "v"(a[2 * p]), "v"(b[2 * p]), "v"(a[2 * p + 1]), "v"(b[2 * p + 1]), "v"(hp));
+        h[p] = hp;
+        l[p] = lp;
+    }
+    hi = __builtin_bit_cast(f16x8, h);
+    lo = __builtin_bit_cast(f16x8, l);
+}
+__device__ __forceinline__ void cvt8p(const float (&a)[8], const float (&b)[8], f16x8 &hi) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 h;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        unsigned hp;
+        asm("v_fma_mixlo_f16 %0, %1, %2, 0\n\t"
+            "v_fma_mixhi_f16 %0, %3, %4, 0"
+            : "=&v"(hp) : "v"(a[2 * p]), "v"(b[2 * p]), "v"(a[2 * p + 1]), "v"(b[2 * p + 1]));
+        h[p] = hp;
+    }
+    hi = __builtin_bit_cast(f16x8, h);
+}
+
 // Precision modes (fcr_dims.precision): LP = false — fp32-accurate split products (three MFMAs);
 // LP = true — config 3's reduced-precision mode: f16 operands, ONE MFMA per product, fp32 accumulate
 template <bool LP>
 __device__ __forceinline__ void split_p(const float (&v)[8], float s, f16x8 &hi, f16x8 &lo) {
     if (LP) cvt8s(v, s, hi);
     else split8s(v, s, hi, lo);
+}
+template <bool LP>
+__device__ __forceinline__ void split_pp(const float (&a)[8], const float (&b)[8], f16x8 &hi, f16x8 &lo) {
+    if (LP) cvt8p(a, b, hi);
+    else split8p(a, b, hi, lo);
 }
 
 // a·b with a = (ah, al), b = (bh, bl): small terms first, then the leading product
