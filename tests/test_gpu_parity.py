@@ -233,3 +233,13 @@ def test_any_hidden_size_up_to_52(H, B, N):
     assert relerr(o["xhat"], f["xhat"]) <= TOL
     for k, _ in GRADS:
         assert relerr(o[k], g[k]) <= TOL, (H, k, relerr(o[k], g[k]))
+
+
+@pytest.mark.parametrize("dloss", [1e-4, 1e4])
+def test_wide_path_any_incoming_gradient_scale(dloss):
+    """H > 52 (config 5's path, split-f16 GEMMs): the dgates enter the f16 GEMM operands as dG 2^k / dloss
+    (wide_bscale_kernel), so a scaled loss (loss * dloss).backward() neither underflows nor overflows them."""
+    c, params = load_case("h64_b24_n3")
+    o = run(params, c["X"], c["u0"], c["states"], c["N"], c["alpha"], c["noise"], dloss=dloss)
+    for k, _ in GRADS:
+        assert relerr(o[k] / dloss, c[f"{k}_64"]) <= TOL, (k, relerr(o[k] / dloss, c[f"{k}_64"]))
