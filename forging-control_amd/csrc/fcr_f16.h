@@ -219,6 +219,30 @@ __device__ __forceinline__ void lstm_point(f32x4 a, float c_prev, float &c, floa
     c = cf + gi;
     h = o * tanh_f(c);
 }
+// lstm_point in two stages (the same arithmetic in the same order), so the forward cell can spread a
+// tile pair's pointwise over the next pair's MFMA regions: A = gates and c, B = h from (c, o)
+template <bool FIRST>
+__device__ __forceinline__ void lstm_point_a(f32x4 a, float c_prev, float &c, float &o) {
+#if FCR_ABLATE == 2
+    c = a[0] + c_prev;
+    o = a[1];
+    return;
+#endif
+    const float i = sigm_pre(a[0]);
+    const float f = sigm_pre(a[1]);
+    const float g = tanh_pre(a[2]);
+    o = sigm_pre(a[3]);
+    const float gi = g * i;
+    const float cf = FIRST ? 0.0f : f * c_prev;
+    c = cf + gi;
+}
+__device__ __forceinline__ void lstm_point_b(float c, float o, float &h) {
+#if FCR_ABLATE == 2
+    h = o;
+    return;
+#endif
+    h = o * tanh_f(c);
+}
 template <bool FIRST>
 __device__ __forceinline__ void lstm_point_grad(f32x4 a, float c_prev, f32x4 &P, f32x2 &Q) {
 #if FCR_ABLATE == 2

@@ -30,6 +30,9 @@ __device__ __forceinline__ void rot_left(float (&w)[kL]) {
 #ifndef FCR_FWD_PRIO
 #define FCR_FWD_PRIO 1
 #endif
+#ifndef FCR_FWD_SPREAD
+#define FCR_FWD_SPREAD 1   // spread each tile pair's pointwise over the next pair's MFMA regions
+#endif
 
 // Issue-priority pacing of the two waves that share a SIMD (waves w and w+4 of the workgroup).
 //   FCR_FWD_PRIO 1: alternate the higher priority cell by cell;
@@ -87,6 +90,8 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
     rd(0, KLO, ah[0], al[0]);
     if (HS > 1) rd(1, KLO, ah[1], al[1]);
     f32x4 prev[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+    constexpr int R = KHI - KLO;   // regions per tile pair
+    float po[2] = {0.0f, 0.0f};    // output gates of the previous pair between the pointwise stages
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
         const int r0 = 2 * p, r1 = 2 * p + 1;
@@ -119,9 +124,25 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
                 if (two) acc[1][ch] = mma_p<LP>(ah[1], al[1], bh[kb], bl[kb], acc[1][ch]);
             }
 #endif
-            if (kb == KLO && p > 0) {
-                lstm_point<FIRST>(prev[0], c[r0 - 2], c[r0 - 2], hout[r0 - 2]);
-                lstm_point<FIRST>(prev[1], c[r1 - 2], c[r1 - 2], hout[r1 - 2]);
+            if (p > 0) {
+#if FCR_FWD_SPREAD
+                // the previous pair's pointwise, spread over this pair's regions beside its MFMAs
+                // (R >= 3: gates of slot r0 | gates of slot r1 | both h; R = 2: both gates | both h)
+                const int qr = kb - KLO;
+                if (R == 1 || (R == 2 && qr == 0) || (R >= 3 && qr == 0))
+                    lstm_point_a<FIRST>(prev[0], c[r0 - 2], c[r0 - 2], po[0]);
+                if (R == 1 || (R == 2 && qr == 0) || (R >= 3 && qr == 1))
+                    lstm_point_a<FIRST>(prev[1], c[r1 - 2], c[r1 - 2], po[1]);
+                if (R == 1 || (R == 2 && qr == 1) || (R >= 3 && qr == 2)) {
+                    lstm_point_b(c[r0 - 2], po[0], hout[r0 - 2]);
+                    lstm_point_b(c[r1 - 2], po[1], hout[r1 - 2]);
+                }
+#else
+                if (kb == KLO) {
+                    lstm_point<FIRST>(prev[0], c[r0 - 2], c[r0 - 2], hout[r0 - 2]);
+                    lstm_point<FIRST>(prev[1], c[r1 - 2], c[r1 - 2], hout[r1 - 2]);
+                }
+#endif
             }
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
