@@ -241,7 +241,12 @@ WideLayout make_wide(const fcr_dims *d, int with_backward) {
 
 rocblas_handle blas_on(hipStream_t s) {
     thread_local rocblas_handle h = nullptr;
-    if (!h && rocblas_create_handle(&h) != rocblas_status_success) return nullptr;
+    if (!h) {
+        if (rocblas_create_handle(&h) != rocblas_status_success) return nullptr;
+        // no split-K solutions that sum through atomics: every GEMM here is run-to-run deterministic
+        // (the surrogate's and the wide path's gradients, and graph replays, repeat bit for bit)
+        rocblas_set_atomics_mode(h, rocblas_atomics_not_allowed);
+    }
     rocblas_set_stream(h, s);
     return h;
 }

@@ -141,11 +141,31 @@ class NeuralNetwork:
     """Training driver with the reference's call surface (Functions.py:594-923)."""
 
     @staticmethod
+    def captured_step(simulator, model, loss_function, optimizer, device, enable_noise=False, grad_sync=None,
+                      warmup=2):
+        """The body of :meth:`train_model`'s batch loop as a :class:`~.graphed.CapturedStep` (one HIP graph
+        replay per batch; pass it as ``train_model(..., step=...)``, reusable across epochs)."""
+        from .graphed import CapturedStep
+
+        def body(X, z):
+            output = model(X)
+            loss, f = loss_function(simulator, model, X, output, z, device, enable_noise)
+            loss.backward()
+            return (loss.detach(), f["loss"], f["command"], f["error"], f["prediction"])
+
+        sync = (lambda: grad_sync(model)) if grad_sync is not None else None
+        return CapturedStep(model.parameters(), optimizer, body, sync, warmup)
+
+    @staticmethod
     def train_model(data_loader, simulator, model, loss_function, optimizer, device, enable_noise=False,
-                    grad_sync=None):
+                    grad_sync=None, step=None):
         """One epoch (Functions.py:594-676). ``grad_sync`` (optional) is called between backward and the
-        optimizer step — the data-parallel hook (see :mod:`.distributed`)."""
+        optimizer step — the data-parallel hook (see :mod:`.distributed`). ``step`` (optional, from
+        :meth:`captured_step`) replays each batch's step from a HIP graph; the epoch's loss is then summed
+        on the device and read once, not per batch."""
         model.train()
+        if step is not None:
+            return NeuralNetwork._train_model_captured(data_loader, step, device)
         total = 0.0
         feats = {"loss": [], "command": [], "error": [], "prediction": []}
         n_batches = 0
@@ -166,6 +186,22 @@ class NeuralNetwork:
         return total / max(n_batches, 1), feats
 
     @staticmethod
+    def _train_model_captured(data_loader, step, device):
+        keys = ("loss", "command", "error", "prediction")
+        feats = {k: [] for k in keys}
+        total = None
+        n_batches = 0
+        for X, _, z in data_loader:
+            X, z = X.to(device), z.to(device)
+            loss, *f = step(X, z)
+            total = loss.clone() if total is None else total + loss
+            for k, v in zip(keys, f):
+                feats[k].append(v.clone())
+            n_batches += 1
+        avg = float(total.item()) / n_batches if n_batches else 0.0
+        return avg, {k: torch.cat(v, dim=0) for k, v in feats.items()}
+
+    @staticmethod
     def validate_model(data_loader, model, loss_function, device):
         """Controller-only validation loss (Functions.py:679-717)."""
         model.eval()
@@ -180,16 +216,19 @@ class NeuralNetwork:
 
     @staticmethod
     def train_loop(controller, simulator, train_loader, val_loader, loss_function, optimizer, n_epochs,
-                   device, enable_noise=False, grad_sync=None):
+                   device, enable_noise=False, grad_sync=None, graphed=False):
         """Epoch loop (Functions.py:825-923); returns (controller, train losses, val losses, seconds,
-        stacked loss features)."""
+        stacked loss features). ``graphed=True`` replays every batch's step from one HIP graph
+        (:meth:`captured_step`) — for the launch-bound small batches the reference trains with."""
         NeuralNetwork.validate_model(val_loader, controller, nn.MSELoss(), device)
+        step = (NeuralNetwork.captured_step(simulator, controller, loss_function, optimizer, device, enable_noise,
+                                            grad_sync) if graphed else None)
         t_losses, v_losses = [], []
         stacked = {"loss": [], "command": [], "error": [], "prediction": []}
         t0 = time.time()
         for epoch in range(n_epochs):
             tl, f = NeuralNetwork.train_model(train_loader, simulator, controller, loss_function, optimizer,
-                                              device, enable_noise, grad_sync)
+                                              device, enable_noise, grad_sync, step)
             vl = NeuralNetwork.validate_model(val_loader, controller, nn.MSELoss(), device)
             if n_epochs >= 10 and epoch % (n_epochs // 10) == 0 or epoch == n_epochs - 1:
                 logger.info("[%.1f%%] Training loss: %.4f,  Validation loss: %.4f",

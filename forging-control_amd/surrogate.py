@@ -89,9 +89,30 @@ def lstm_apply(model, x: torch.Tensor) -> torch.Tensor:
     return LSTMFunction.apply(x, *p, model.fc.weight, model.fc.bias)
 
 
-def train_model(data_loader, model, loss_function, optimizer, device):
-    """Model_NN/Functions.py:520-569 with the same arguments and return value (average batch loss)."""
+def captured_step(model, loss_function, optimizer, device, warmup=2):
+    """The batch step of :func:`train_model` as a :class:`~.graphed.CapturedStep` (one HIP graph replay
+    per batch; pass it as ``train_model(..., step=...)``)."""
+    from .graphed import CapturedStep
+
+    def body(X, y):
+        loss = loss_function(model(X, device), y.squeeze())
+        loss.backward()
+        return (loss.detach(),)
+
+    return CapturedStep(model.parameters(), optimizer, body, None, warmup)
+
+
+def train_model(data_loader, model, loss_function, optimizer, device, step=None):
+    """Model_NN/Functions.py:520-569 with the same arguments and return value (average batch loss).
+    ``step`` (optional, from :func:`captured_step`) replays each batch from a HIP graph and reads the
+    summed loss once per epoch instead of once per batch."""
     model.train()
+    if step is not None:
+        total_dev = None
+        for X, y in data_loader:
+            (loss,) = step(X.to(device), y.to(device))
+            total_dev = loss.clone() if total_dev is None else total_dev + loss
+        return (float(total_dev.item()) if total_dev is not None else 0.0) / len(data_loader)
     total = 0.0
     for X, y in data_loader:
         X, y = X.to(device), y.to(device)
