@@ -357,6 +357,36 @@ WideArgs wide_args(const fcr_dims *d, const WideLayout &L, char *base) {
     return a;
 }
 
+// The cell kernels' vector width (fcr_wide.h): 16-B accesses when H % 4 == 0, 8-B when H is even.
+int cell_vec(int H) { return H % 4 == 0 ? 4 : (H % 2 == 0 ? 2 : 1); }
+
+int launch_cell(int B, int H, hipStream_t s, const float *G, const float *c_prev, float *c_out, float *h_out,
+                float *act, _Float16 *xb_h, int sh, _Float16 *xb_x, int sx) {
+    const int V = cell_vec(H);
+    const dim3 grid((unsigned)(((size_t)B * (H / V) + 255) / 256)), blk(256);
+    if (V == 4)
+        hipLaunchKernelGGL(wide_cell_kernel<4>, grid, blk, 0, s, G, c_prev, c_out, h_out, act, xb_h, sh, xb_x, sx, B, H);
+    else if (V == 2)
+        hipLaunchKernelGGL(wide_cell_kernel<2>, grid, blk, 0, s, G, c_prev, c_out, h_out, act, xb_h, sh, xb_x, sx, B, H);
+    else
+        hipLaunchKernelGGL(wide_cell_kernel<1>, grid, blk, 0, s, G, c_prev, c_out, h_out, act, xb_h, sh, xb_x, sx, B, H);
+    return launch_check("wide_cell_kernel");
+}
+
+template <bool PRE>
+int launch_cell_bwd(int B, int H, hipStream_t s, const float *act, const float *c, const float *c_prev,
+                    const float *dH, const float *din, float *dC, float *dG, _Float16 *dgsp, const float *consts) {
+    const int V = cell_vec(H);
+    const dim3 grid((unsigned)(((size_t)B * (H / V) + 255) / 256)), blk(256);
+    if (V == 4)
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, B, H);
+    else if (V == 2)
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 2>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, B, H);
+    else
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 1>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, B, H);
+    return launch_check("wide_cell_bwd_kernel");
+}
+
 // One window's cells, forward: 3 layers x 10 steps of [GEMM x_t W_ih^T, GEMM h_{t-1} W_hh^T, cell].
 // sp != nullptr (the rollout): the H-wide products as ONE K-concatenated split-f16 GEMM per cell (gemm16_fwd) — ~3x the fp32
 // GEMM rate at equal accuracy; sp == nullptr (the surrogate's training step): fp32 rocBLAS throughout.
@@ -364,7 +394,6 @@ int wide_cells(rocblas_handle h, const WideArgs &a, const float *const *w_ih, co
                const WideSplit *sp, hipStream_t s) {
     const int B = a.B, H = a.H;
     const size_t cell = (size_t)B * H;
-    const int nb = (int)((cell + 255) / 256);
     // operand rows of cell (l, t): layer >= 1 [x part 3H | h part 3H], layer 0 [h part 3H]
     auto ldx = [&](int l) { return l == 0 ? 3 * H : 6 * H; };
     auto xb = [&](int l, int t) { return sp->XB + ((size_t)l * kL + t) * B * 6 * H; };
@@ -394,12 +423,11 @@ int wide_cells(rocblas_handle h, const WideArgs &a, const float *const *w_ih, co
             _Float16 *xx = (sp && l + 1 < kLayers) ? xb(l + 1, t) : nullptr;                       // layer above's x part
             // the split path reads h only through the operand rows; fp32 h is kept for the readout (2, 9)
             float *hout = (!sp || (l == kLayers - 1 && t == kL - 1)) ? a.Hs + ((size_t)l * kL + t) * cell : nullptr;
-            hipLaunchKernelGGL(wide_cell_kernel, dim3(nb), dim3(256), 0, s, (const float *)G,
-                               t > 0 ? (const float *)(a.Cs + ((size_t)l * kL + t - 1) * cell) : nullptr,
-                               a.Cs + ((size_t)l * kL + t) * cell, hout,
-                               (keep_act && !sp) ? a.Act + ((size_t)l * kL + t) * cell * 4 : nullptr, xh, ldx(l), xx,
-                               ldx(l + 1 < kLayers ? l + 1 : l), B, H);
-            if ((rc = launch_check("wide_cell_kernel"))) return rc;
+            if ((rc = launch_cell(B, H, s, G, t > 0 ? (const float *)(a.Cs + ((size_t)l * kL + t - 1) * cell) : nullptr,
+                                  a.Cs + ((size_t)l * kL + t) * cell, hout,
+                                  (keep_act && !sp) ? a.Act + ((size_t)l * kL + t) * cell * 4 : nullptr, xh, ldx(l), xx,
+                                  ldx(l + 1 < kLayers ? l + 1 : l))))
+                return rc;
         }
     }
     return FCR_OK;
@@ -473,7 +501,7 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
     const WideLayout L = make_wide(d, 1);
     const int B = d->B, H = d->H;
     const size_t cell = (size_t)B * H;
-    const int nb = (B + 255) / 256, nc = (int)((cell + 255) / 256);
+    const int nb = (B + 255) / 256;
     int rc;
     rocblas_handle h = blas_on(s);
     if (!h) return fail(FCR_EHIP, "rocblas_create_handle failed");
@@ -507,11 +535,10 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
             if (hipMemsetAsync(a.dC, 0, sizeof(float) * cell, s) != hipSuccess) return fail(FCR_EHIP, "hipMemsetAsync failed");
             for (int t = kL - 1; t >= 0; --t) {
                 const size_t c_off = ((size_t)l * kL + t) * cell;
-                hipLaunchKernelGGL(wide_cell_bwd_kernel<true>, dim3(nc), dim3(256), 0, s, (const float *)(a.Act + c_off * 4),
-                                   (const float *)(a.Cs + c_off), t > 0 ? (const float *)(a.Cs + c_off - cell) : nullptr,
-                                   (const float *)a.dH, l < kLayers - 1 ? (const float *)(D[l] + (size_t)t * cell) : nullptr,
-                                   a.dC, l == 0 ? a.G : nullptr, sp.dGsp, (const float *)sp.consts, B, H);
-                if ((rc = launch_check("wide_cell_bwd_kernel"))) return rc;
+                if ((rc = launch_cell_bwd<true>(B, H, s, a.Act + c_off * 4, a.Cs + c_off, t > 0 ? a.Cs + c_off - cell : nullptr,
+                                                a.dH, l < kLayers - 1 ? D[l] + (size_t)t * cell : nullptr, a.dC,
+                                                l == 0 ? a.G : nullptr, sp.dGsp, sp.consts)))
+                    return rc;
                 if (l > 0) {
                     if ((rc = gemm16_bwd(h, B, H, sp.bih[l], sp.dGsp, sp.consts, D[l - 1] + (size_t)t * cell))) return rc;
                 } else {   // layer 0: the window rows' gradients, row j + t (K = 5: fp32)
@@ -911,11 +938,10 @@ int fcr_lstm_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, 
         for (int t = kL - 1; t >= 0; --t) {
             const size_t c_off = ((size_t)l * kL + t) * cell;
             float *dG = dGs + (size_t)t * gcell;
-            hipLaunchKernelGGL(wide_cell_bwd_kernel<false>, dim3(nc), dim3(256), 0, s, (const float *)(a.Act + c_off * 4),
-                               (const float *)(a.Cs + c_off), t > 0 ? (const float *)(a.Cs + c_off - cell) : nullptr,
-                               (const float *)a.dH, l < kLayers - 1 ? (const float *)(D[l] + (size_t)t * cell) : nullptr,
-                               a.dC, dG, (_Float16 *)nullptr, (const float *)nullptr, B, H);
-            if ((rc = launch_check("wide_cell_bwd_kernel"))) return rc;
+            if ((rc = launch_cell_bwd<false>(B, H, s, a.Act + c_off * 4, a.Cs + c_off, t > 0 ? a.Cs + c_off - cell : nullptr,
+                                             a.dH, l < kLayers - 1 ? D[l] + (size_t)t * cell : nullptr, a.dC, dG, nullptr,
+                                             nullptr)))
+                return rc;
             if (l > 0) {
                 if ((rc = gemm_gw(h, B, 4 * H, H, w->w_ih[l], dG, 0.0f, D[l - 1] + (size_t)t * cell))) return rc;
             } else if (g_x) {

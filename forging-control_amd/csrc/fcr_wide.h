@@ -84,39 +84,62 @@ __global__ void wide_window_kernel(WideArgs a, int j) {
 // hidden states are small (1 - 2/(1 + e^{2x}) is only accurate to ~1e-7 absolute).
 // xb_h / xb_x (split-f16 path, else null): the GEMM operand rows that take this h — the h part of the
 // same layer's next cell and the x part of the layer above's cell t — as (hi, lo, hi), row strides sh / sx.
+// V consecutive units per thread (V = 4 when H % 4 == 0: 16-B gate / state accesses, 8-B f16 stores —
+// the kernel is HBM-bound and the wide accesses are what it runs at; V = 1 otherwise).
+template <int V>
+struct WideVec {
+    typedef float F __attribute__((ext_vector_type(V)));
+    typedef _Float16 h __attribute__((ext_vector_type(V)));
+    static __device__ __forceinline__ F ld(const float *p) { return *(const F *)p; }
+    static __device__ __forceinline__ void st(float *p, F v) { *(F *)p = v; }
+    static __device__ __forceinline__ void st16(_Float16 *p, h v) { *(h *)p = v; }
+};
+
+template <int V>
 __global__ void wide_cell_kernel(const float *__restrict__ G, const float *__restrict__ c_prev, float *c_out,
                                  float *h_out, float *act, _Float16 *xb_h, int sh, _Float16 *xb_x, int sx, int B,
                                  int H) {
-    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (size_t)B * H) return;
-    const size_t b = idx / H, u = idx % H;
+    using W = WideVec<V>;
+    const int HV = H / V;
+    const size_t iv = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (iv >= (size_t)B * HV) return;
+    const size_t b = iv / HV, u = (iv % HV) * V, idx = b * H + u;
     const float *g4 = G + b * 4 * H + u;
-    const float i = sigm(g4[0]), f = sigm(g4[H]), g = tanhf(g4[2 * H]), o = sigm(g4[3 * H]);
-    const float c = (c_prev ? f * c_prev[idx] : 0.0f) + i * g;
-    c_out[idx] = c;
-    const float h = o * tanhf(c);
-    if (h_out) h_out[idx] = h;
-    if (xb_h || xb_x) {
-        const _Float16 hi = (_Float16)h, lo = (_Float16)(h - (float)hi);
-        if (xb_h) {
-            _Float16 *o = xb_h + b * sh + u;
-            o[0] = hi;
-            o[H] = lo;
-            o[2 * H] = hi;
-        }
-        if (xb_x) {
-            _Float16 *o = xb_x + b * sx + u;
-            o[0] = hi;
-            o[H] = lo;
-            o[2 * H] = hi;
-        }
+    const typename W::F gi = W::ld(g4), gf = W::ld(g4 + H), gg = W::ld(g4 + 2 * H), go = W::ld(g4 + 3 * H);
+    typename W::F cp = {}, i, f, g, o, c, h;
+    if (c_prev) cp = W::ld(c_prev + idx);
+    typename W::h hi, lo;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+        i[k] = sigm(gi[k]);
+        f[k] = sigm(gf[k]);
+        g[k] = tanhf(gg[k]);
+        o[k] = sigm(go[k]);
+        c[k] = (c_prev ? f[k] * cp[k] : 0.0f) + i[k] * g[k];
+        h[k] = o[k] * tanhf(c[k]);
+        hi[k] = (_Float16)h[k];
+        lo[k] = (_Float16)(h[k] - (float)hi[k]);
+    }
+    W::st(c_out + idx, c);
+    if (h_out) W::st(h_out + idx, h);
+    if (xb_h) {
+        _Float16 *p = xb_h + b * sh + u;
+        W::st16(p, hi);
+        W::st16(p + H, lo);
+        W::st16(p + 2 * H, hi);
+    }
+    if (xb_x) {
+        _Float16 *p = xb_x + b * sx + u;
+        W::st16(p, hi);
+        W::st16(p + H, lo);
+        W::st16(p + 2 * H, hi);
     }
     if (act) {
         float *a4 = act + b * 4 * H + u;
-        a4[0] = i;
-        a4[H] = f;
-        a4[2 * H] = g;
-        a4[3 * H] = o;
+        W::st(a4, i);
+        W::st(a4 + H, f);
+        W::st(a4 + 2 * H, g);
+        W::st(a4 + 3 * H, o);
     }
 }
 
@@ -198,41 +221,58 @@ __global__ void wide_head_kernel(WideArgs a, int j) {
 // act: the gate activations (i, f, g, o) kept by the recompute, or with PRE their pre-activations (the
 // split-f16 rollout keeps the GEMM output per cell instead of writing a second 4H-wide array), from which
 // the activations are rebuilt with the forward's arithmetic. dG (fp32) may be null when only dgsp is used.
-template <bool PRE>
+template <bool PRE, int V>
 __global__ void wide_cell_bwd_kernel(const float *__restrict__ act, const float *__restrict__ c,
                                      const float *__restrict__ c_prev, const float *__restrict__ dH,
                                      const float *__restrict__ din, float *dC, float *dG, _Float16 *dgsp,
                                      const float *__restrict__ consts, int B, int H) {
-    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (size_t)B * H) return;
-    const size_t b = idx / H, u = idx % H;
+    using W = WideVec<V>;
+    const int HV = H / V;
+    const size_t iv = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (iv >= (size_t)B * HV) return;
+    const size_t b = iv / HV, u = (iv % HV) * V, idx = b * H + u;
     const float *a4 = act + b * 4 * H + u;
-    const float i = PRE ? sigm(a4[0]) : a4[0], f = PRE ? sigm(a4[H]) : a4[H], g = PRE ? tanhf(a4[2 * H]) : a4[2 * H],
-                o = PRE ? sigm(a4[3 * H]) : a4[3 * H];
-    const float tc = tanhf(c[idx]);
-    const float cp = c_prev ? c_prev[idx] : 0.0f;
-    const float dh = dH[idx] + (din ? din[idx] : 0.0f);
-    const float dct = dC[idx] + dh * o * (1.0f - tc * tc);
-    const float dg4[4] = {dct * g * i * (1.0f - i), dct * cp * f * (1.0f - f), dct * i * (1.0f - g * g),
-                          dh * tc * o * (1.0f - o)};
+    const typename W::F ai = W::ld(a4), af = W::ld(a4 + H), ag = W::ld(a4 + 2 * H), ao = W::ld(a4 + 3 * H);
+    const typename W::F cv = W::ld(c + idx), dhv = W::ld(dH + idx), dcv = W::ld(dC + idx);
+    typename W::F cp = {}, dn = {}, dg[4], dco;
+    if (c_prev) cp = W::ld(c_prev + idx);
+    if (din) dn = W::ld(din + idx);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+        const float i = PRE ? sigm(ai[k]) : ai[k], f = PRE ? sigm(af[k]) : af[k], g = PRE ? tanhf(ag[k]) : ag[k],
+                    o = PRE ? sigm(ao[k]) : ao[k];
+        const float tc = tanhf(cv[k]);
+        const float dh = dhv[k] + dn[k];
+        const float dct = dcv[k] + dh * o * (1.0f - tc * tc);
+        dg[0][k] = dct * g * i * (1.0f - i);
+        dg[1][k] = dct * cp[k] * f * (1.0f - f);
+        dg[2][k] = dct * i * (1.0f - g * g);
+        dg[3][k] = dh * tc * o * (1.0f - o);
+        dco[k] = dct * f;
+    }
     if (dG) {
         float *d4 = dG + b * 4 * H + u;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) d4[k * H] = dg4[k];
+        for (int k = 0; k < 4; ++k) W::st(d4 + k * H, dg[k]);
     }
     if (dgsp) {   // split-f16 operand row [hi | lo | hi] of W^T dG, scaled into the f16 range (wide_bscale_kernel)
         const float sc = consts[3];
         _Float16 *o16 = dgsp + b * 12 * H + u;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const float v = dg4[k] * sc;
-            const _Float16 hi = (_Float16)v;
-            o16[k * H] = hi;
-            o16[(4 + k) * H] = (_Float16)(v - (float)hi);
-            o16[(8 + k) * H] = hi;
+            typename W::h hi, lo;
+#pragma unroll
+            for (int e = 0; e < V; ++e) {
+                const float v = dg[k][e] * sc;
+                hi[e] = (_Float16)v;
+                lo[e] = (_Float16)(v - (float)hi[e]);
+            }
+            W::st16(o16 + k * H, hi);
+            W::st16(o16 + (4 + k) * H, lo);
+            W::st16(o16 + (8 + k) * H, hi);
         }
     }
-    dC[idx] = dct * f;
+    W::st(dC + idx, dco);
 }
 
 // Split-f16 operands of the config-5 gate GEMMs (fp32-accurate on the matrix cores, as fcr_f16.h does
