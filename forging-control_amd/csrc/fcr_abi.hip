@@ -277,15 +277,16 @@ int gemm16_fwd(rocblas_handle h, int B, int H4, int K, const _Float16 *A, int ld
                                               rocblas_datatype_f32_r, rocblas_gemm_algo_standard, 0, 0);
     return st == rocblas_status_success ? FCR_OK : fail(FCR_EHIP, "rocblas_gemm_ex (forward, f16 split) failed: %d", (int)st);
 }
-// dX (row-major B x H) = dGs A on split-f16 operands: A row-major [12H][H] = [W_hi ; W_hi ; W_lo], dGs row-major
-// [B][12H] = [hi | lo | hi] of dG * scale; consts (device) = [alpha = 1/scale, 0, 1, scale].
-int gemm16_bwd(rocblas_handle h, int B, int H, const _Float16 *A, const _Float16 *dGs, const float *consts, float *dX) {
-    rocblas_set_pointer_mode(h, rocblas_pointer_mode_device);
-    const rocblas_status st = rocblas_gemm_ex(h, rocblas_operation_none, rocblas_operation_none, H, B, 12 * H, consts, A,
-                                              rocblas_datatype_f16_r, H, dGs, rocblas_datatype_f16_r, 12 * H, consts + 1,
+// dX' (row-major B x H) = dGs A on split-f16 operands: A row-major [12H][H] = [W_hi ; W_hi ; W_lo], dGs row-major
+// [B][12H] = [hi | lo | hi] of dG * scale. dX' stays in the scaled units: its consumer (wide_cell_bwd_kernel)
+// multiplies by 1/scale = consts[0] on load — the same single fp32 product a device-pointer alpha would apply,
+// without the per-call alpha/beta copies rocBLAS launches in device pointer mode.
+int gemm16_bwd(rocblas_handle h, int B, int H, const _Float16 *A, const _Float16 *dGs, float *dX) {
+    const float one = 1.0f, zero = 0.0f;
+    const rocblas_status st = rocblas_gemm_ex(h, rocblas_operation_none, rocblas_operation_none, H, B, 12 * H, &one, A,
+                                              rocblas_datatype_f16_r, H, dGs, rocblas_datatype_f16_r, 12 * H, &zero,
                                               dX, rocblas_datatype_f32_r, H, dX, rocblas_datatype_f32_r, H,
                                               rocblas_datatype_f32_r, rocblas_gemm_algo_standard, 0, 0);
-    rocblas_set_pointer_mode(h, rocblas_pointer_mode_host);
     return st == rocblas_status_success ? FCR_OK : fail(FCR_EHIP, "rocblas_gemm_ex (backward, f16 split) failed: %d", (int)st);
 }
 
@@ -375,15 +376,16 @@ int launch_cell(int B, int H, hipStream_t s, const float *G, const float *c_prev
 
 template <bool PRE>
 int launch_cell_bwd(int B, int H, hipStream_t s, const float *act, const float *c, const float *c_prev,
-                    const float *dH, const float *din, float *dC, float *dG, _Float16 *dgsp, const float *consts) {
+                    const float *dH, const float *din, float *dC, float *dG, _Float16 *dgsp, const float *consts,
+                    int dh_scaled) {
     const int V = cell_vec(H);
     const dim3 grid((unsigned)(((size_t)B * (H / V) + 255) / 256)), blk(256);
     if (V == 4)
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, B, H);
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, B, H);
     else if (V == 2)
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 2>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, B, H);
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 2>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, B, H);
     else
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 1>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, B, H);
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 1>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, B, H);
     return launch_check("wide_cell_bwd_kernel");
 }
 
@@ -537,14 +539,15 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
                 const size_t c_off = ((size_t)l * kL + t) * cell;
                 if ((rc = launch_cell_bwd<true>(B, H, s, a.Act + c_off * 4, a.Cs + c_off, t > 0 ? a.Cs + c_off - cell : nullptr,
                                                 a.dH, l < kLayers - 1 ? D[l] + (size_t)t * cell : nullptr, a.dC,
-                                                l == 0 ? a.G : nullptr, sp.dGsp, sp.consts)))
+                                                l == 0 ? a.G : nullptr, sp.dGsp, sp.consts,
+                                                l < kLayers - 1 || t < kL - 1)))   // (2, 9): the head's dH
                     return rc;
                 if (l > 0) {
-                    if ((rc = gemm16_bwd(h, B, H, sp.bih[l], sp.dGsp, sp.consts, D[l - 1] + (size_t)t * cell))) return rc;
+                    if ((rc = gemm16_bwd(h, B, H, sp.bih[l], sp.dGsp, D[l - 1] + (size_t)t * cell))) return rc;
                 } else {   // layer 0: the window rows' gradients, row j + t (K = 5: fp32)
                     if ((rc = gemm_gw(h, B, 4 * H, kIn, wih[l], a.G, 1.0f, a.rowg + (size_t)(j + t) * B * kIn))) return rc;
                 }
-                if (t > 0 && (rc = gemm16_bwd(h, B, H, sp.bhh[l], sp.dGsp, sp.consts, a.dH))) return rc;
+                if (t > 0 && (rc = gemm16_bwd(h, B, H, sp.bhh[l], sp.dGsp, a.dH))) return rc;
             }
         }
     }
@@ -940,7 +943,7 @@ int fcr_lstm_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, 
             float *dG = dGs + (size_t)t * gcell;
             if ((rc = launch_cell_bwd<false>(B, H, s, a.Act + c_off * 4, a.Cs + c_off, t > 0 ? a.Cs + c_off - cell : nullptr,
                                              a.dH, l < kLayers - 1 ? D[l] + (size_t)t * cell : nullptr, a.dC, dG, nullptr,
-                                             nullptr)))
+                                             nullptr, 0)))
                 return rc;
             if (l > 0) {
                 if ((rc = gemm_gw(h, B, 4 * H, H, w->w_ih[l], dG, 0.0f, D[l - 1] + (size_t)t * cell))) return rc;

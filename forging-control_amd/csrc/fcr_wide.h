@@ -85,7 +85,7 @@ __global__ void wide_window_kernel(WideArgs a, int j) {
 // xb_h / xb_x (split-f16 path, else null): the GEMM operand rows that take this h — the h part of the
 // same layer's next cell and the x part of the layer above's cell t — as (hi, lo, hi), row strides sh / sx.
 // V consecutive units per thread (V = 4 when H % 4 == 0: 16-B gate / state accesses, 8-B f16 stores —
-// the kernel is HBM-bound and the wide accesses are what it runs at; V = 1 otherwise).
+// the kernel is HBM-bound and the wide accesses are what it runs at; V = 2 for even H, else 1).
 template <int V>
 struct WideVec {
     typedef float F __attribute__((ext_vector_type(V)));
@@ -217,7 +217,7 @@ __global__ void wide_head_kernel(WideArgs a, int j) {
 }
 
 // Backward of one cell: from the activations, c_t, c_{t-1}, the incoming dh (carried dH + din from the
-// layer above) and the carried dc: d loss / d (gate pre-activations) into dG, and dc_{t-1} into dC.
+// layer above; see dh_scaled) and the carried dc: d loss / d (gate pre-activations) into dG, and dc_{t-1} into dC.
 // act: the gate activations (i, f, g, o) kept by the recompute, or with PRE their pre-activations (the
 // split-f16 rollout keeps the GEMM output per cell instead of writing a second 4H-wide array), from which
 // the activations are rebuilt with the forward's arithmetic. dG (fp32) may be null when only dgsp is used.
@@ -225,8 +225,11 @@ template <bool PRE, int V>
 __global__ void wide_cell_bwd_kernel(const float *__restrict__ act, const float *__restrict__ c,
                                      const float *__restrict__ c_prev, const float *__restrict__ dH,
                                      const float *__restrict__ din, float *dC, float *dG, _Float16 *dgsp,
-                                     const float *__restrict__ consts, int B, int H) {
+                                     const float *__restrict__ consts, int dh_scaled, int B, int H) {
     using W = WideVec<V>;
+    // with consts (split-f16 rollout) din, and dH unless it is the head's, come from gemm16_bwd in the
+    // scaled units of the dgates: back by 1/scale = consts[0], one fp32 product each
+    const float c0 = consts ? consts[0] : 1.0f, mh = dh_scaled ? c0 : 1.0f;
     const int HV = H / V;
     const size_t iv = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (iv >= (size_t)B * HV) return;
@@ -242,7 +245,7 @@ __global__ void wide_cell_bwd_kernel(const float *__restrict__ act, const float 
         const float i = PRE ? sigm(ai[k]) : ai[k], f = PRE ? sigm(af[k]) : af[k], g = PRE ? tanhf(ag[k]) : ag[k],
                     o = PRE ? sigm(ao[k]) : ao[k];
         const float tc = tanhf(cv[k]);
-        const float dh = dhv[k] + dn[k];
+        const float dh = dhv[k] * mh + dn[k] * c0;
         const float dct = dcv[k] + dh * o * (1.0f - tc * tc);
         dg[0][k] = dct * g * i * (1.0f - i);
         dg[1][k] = dct * cp[k] * f * (1.0f - f);
@@ -304,7 +307,8 @@ __global__ void wide_split_ba_kernel(const float *__restrict__ W, int H, _Float1
 }
 
 // The dgates are split as dG * 2^k / dloss (|dG| ~ dloss / (B N): without it they would sit in the f16
-// subnormals); the backward GEMMs take alpha = dloss * 2^-k from device memory. consts = [alpha, 0, 1, scale].
+// subnormals); the backward GEMMs' outputs stay in those units and wide_cell_bwd_kernel scales them back by
+// consts[0] = dloss * 2^-k on load (no host sync for dloss). consts = [1/scale, 0, 1, scale].
 __global__ void wide_bscale_kernel(const float *__restrict__ dloss, int k, float *consts) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const float d = dloss[0];
