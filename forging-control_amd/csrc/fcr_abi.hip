@@ -179,8 +179,9 @@ struct WideLayout {
     size_t wih[3], whh[3], fcw, fcb, cwi, cbi, cwo, fcp, fcbo, fnp, xhat, tot, cmd, err, X0, Hs, Cs, G;
     size_t Act, dH, dC, D[2], rowg, dv, fnn_part, total;
     // split-f16 gate GEMM operands (fcr_wide.h: forward A per layer, backward A per weight, the cells'
-    // operand rows XB [3][10][B][6H], the dgate rows [B][12H]; layer 0's W_ih, K = 5, stays fp32)
+    // operand rows XB [3][10][B][6H] (layer 0 rows 3H + kX16 long), the dgate rows [B][12H])
     size_t fa[3], bih[3], bhh[3], XB, dGsp, consts;
+    size_t bx0, E0;   // layer 0's backward A [12H][H + 8] and its product rows [B][H + 8]
     int ctrl_blocks;
 };
 
@@ -215,15 +216,20 @@ WideLayout make_wide(const fcr_dims *d, int with_backward) {
     L.G = take(F * B * 4 * H);
     const size_t F16 = sizeof(_Float16), WW = 4 * H * H;
     for (int l = 0; l < kLayers; ++l) {
-        L.fa[l] = take(F16 * WW * (l == 0 ? 3 : 6));
+        L.fa[l] = take(l == 0 ? F16 * 4 * H * (3 * H + kX16) : F16 * WW * 6);
         if (with_backward) {
-            if (l > 0) L.bih[l] = take(F16 * 3 * WW);
-            L.bhh[l] = take(F16 * 3 * WW);
+            if (l > 0) {
+                L.bih[l] = take(F16 * 3 * WW);
+                L.bhh[l] = take(F16 * 3 * WW);
+            } else {
+                L.bx0 = take(F16 * 12 * H * (H + 8));
+            }
         }
     }
     L.XB = take(F16 * kLayers * kL * B * 6 * H);
     if (with_backward) {
         L.dGsp = take(F16 * B * 12 * H);
+        L.E0 = take(F * B * (H + 8));
         L.consts = take(F * 4);
         L.Act = take(F * kLayers * kL * B * 4 * H);
         L.dH = take(F * B * H);
@@ -281,11 +287,12 @@ int gemm16_fwd(rocblas_handle h, int B, int H4, int K, const _Float16 *A, int ld
 // [B][12H] = [hi | lo | hi] of dG * scale. dX' stays in the scaled units: its consumer (wide_cell_bwd_kernel)
 // multiplies by 1/scale = consts[0] on load — the same single fp32 product a device-pointer alpha would apply,
 // without the per-call alpha/beta copies rocBLAS launches in device pointer mode.
-int gemm16_bwd(rocblas_handle h, int B, int H, const _Float16 *A, const _Float16 *dGs, float *dX) {
+// n output columns of A (row-major [12H][lda]) into dX rows of stride ldc.
+int gemm16_bwd(rocblas_handle h, int B, int n, int H, const _Float16 *A, int lda, const _Float16 *dGs, float *dX, int ldc) {
     const float one = 1.0f, zero = 0.0f;
-    const rocblas_status st = rocblas_gemm_ex(h, rocblas_operation_none, rocblas_operation_none, H, B, 12 * H, &one, A,
-                                              rocblas_datatype_f16_r, H, dGs, rocblas_datatype_f16_r, 12 * H, &zero,
-                                              dX, rocblas_datatype_f32_r, H, dX, rocblas_datatype_f32_r, H,
+    const rocblas_status st = rocblas_gemm_ex(h, rocblas_operation_none, rocblas_operation_none, n, B, 12 * H, &one, A,
+                                              rocblas_datatype_f16_r, lda, dGs, rocblas_datatype_f16_r, 12 * H, &zero,
+                                              dX, rocblas_datatype_f32_r, ldc, dX, rocblas_datatype_f32_r, ldc,
                                               rocblas_datatype_f32_r, rocblas_gemm_algo_standard, 0, 0);
     return st == rocblas_status_success ? FCR_OK : fail(FCR_EHIP, "rocblas_gemm_ex (backward, f16 split) failed: %d", (int)st);
 }
@@ -295,6 +302,8 @@ struct WideSplit {
     const _Float16 *fa[kLayers], *bih[kLayers], *bhh[kLayers];
     _Float16 *XB, *dGsp;
     float *consts;
+    const _Float16 *bx0;
+    float *E0;
 };
 
 WideSplit wide_split(const WideLayout &L, char *base) {
@@ -307,6 +316,8 @@ WideSplit wide_split(const WideLayout &L, char *base) {
     w.XB = (_Float16 *)(base + L.XB);
     w.dGsp = L.dGsp ? (_Float16 *)(base + L.dGsp) : nullptr;
     w.consts = L.consts ? (float *)(base + L.consts) : nullptr;
+    w.bx0 = L.bx0 ? (const _Float16 *)(base + L.bx0) : nullptr;
+    w.E0 = L.E0 ? (float *)(base + L.E0) : nullptr;
     return w;
 }
 
@@ -316,12 +327,19 @@ int wide_pack_split(const float *const *w_ih, const float *const *w_hh, int H, b
     const size_t WW = (size_t)4 * H * H;
     int rc;
     for (int l = 0; l < kLayers; ++l) {
-        const size_t n = WW * (l == 0 ? 3 : 6);
-        hipLaunchKernelGGL(wide_split_fa_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
-                           l == 0 ? (const float *)nullptr : w_ih[l], w_hh[l], H, (_Float16 *)sp.fa[l]);
+        const size_t n = l == 0 ? (size_t)4 * H * (3 * H + kX16) : WW * 6;
+        hipLaunchKernelGGL(wide_split_fa_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w_ih[l], w_hh[l], H,
+                           (int)(l == 0), (_Float16 *)sp.fa[l]);
         if ((rc = launch_check("wide_split_fa_kernel"))) return rc;
         if (!backward) continue;
-        for (int k = (l == 0 ? 1 : 0); k < 2; ++k) {
+        if (l == 0) {
+            const size_t nb0 = (size_t)12 * H * (H + 8);
+            hipLaunchKernelGGL(wide_split_bx0_kernel, dim3((unsigned)((nb0 + 255) / 256)), dim3(256), 0, s, w_ih[0], w_hh[0],
+                               H, (_Float16 *)sp.bx0);
+            if ((rc = launch_check("wide_split_bx0_kernel"))) return rc;
+            continue;
+        }
+        for (int k = 0; k < 2; ++k) {
             hipLaunchKernelGGL(wide_split_ba_kernel, dim3((unsigned)((3 * WW + 255) / 256)), dim3(256), 0, s,
                                k == 0 ? w_ih[l] : w_hh[l], H, (_Float16 *)(k == 0 ? sp.bih[l] : sp.bhh[l]));
             if ((rc = launch_check("wide_split_ba_kernel"))) return rc;
@@ -377,15 +395,15 @@ int launch_cell(int B, int H, hipStream_t s, const float *G, const float *c_prev
 template <bool PRE>
 int launch_cell_bwd(int B, int H, hipStream_t s, const float *act, const float *c, const float *c_prev,
                     const float *dH, const float *din, float *dC, float *dG, _Float16 *dgsp, const float *consts,
-                    int dh_scaled) {
+                    int dh_scaled, int ldh) {
     const int V = cell_vec(H);
     const dim3 grid((unsigned)(((size_t)B * (H / V) + 255) / 256)), blk(256);
     if (V == 4)
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, B, H);
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, B, H);
     else if (V == 2)
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 2>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, B, H);
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 2>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, B, H);
     else
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 1>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, B, H);
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 1>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, B, H);
     return launch_check("wide_cell_bwd_kernel");
 }
 
@@ -397,7 +415,7 @@ int wide_cells(rocblas_handle h, const WideArgs &a, const float *const *w_ih, co
     const int B = a.B, H = a.H;
     const size_t cell = (size_t)B * H;
     // operand rows of cell (l, t): layer >= 1 [x part 3H | h part 3H], layer 0 [h part 3H]
-    auto ldx = [&](int l) { return l == 0 ? 3 * H : 6 * H; };
+    auto ldx = [&](int l) { return l == 0 ? 3 * H + kX16 : 6 * H; };
     auto xb = [&](int l, int t) { return sp->XB + ((size_t)l * kL + t) * B * 6 * H; };
     int rc;
     for (int l = 0; l < kLayers; ++l) {
@@ -408,9 +426,10 @@ int wide_cells(rocblas_handle h, const WideArgs &a, const float *const *w_ih, co
             // the Act slab (wide_cell_bwd_kernel<true> rebuilds the activations) instead of a second array
             float *G = (sp && keep_act) ? a.Act + ((size_t)l * kL + t) * cell * 4 : a.G;
             if (sp) {
-                if (l == 0) {
-                    if ((rc = gemm_xwt(h, B, 4 * H, kIn, wih, x, 0.0f, G))) return rc;
-                    if (t > 0 && (rc = gemm16_fwd(h, B, 4 * H, 3 * H, sp->fa[0], 3 * H, xb(0, t), 3 * H, 1.0f, G)))
+                if (l == 0) {   // [h part | window-row part] (wide_window_kernel writes the latter); t = 0: no h
+                    const int k0 = t > 0 ? 0 : 3 * H;
+                    if ((rc = gemm16_fwd(h, B, 4 * H, 3 * H + kX16 - k0, sp->fa[0] + k0, ldx(0), xb(0, t) + k0, ldx(0),
+                                         0.0f, G)))
                         return rc;
                 } else if ((rc = gemm16_fwd(h, B, 4 * H, t > 0 ? 6 * H : 3 * H, sp->fa[l], 6 * H, xb(l, t), 6 * H, 0.0f,
                                             G))) {
@@ -472,6 +491,7 @@ int wide_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const 
     rocblas_handle h = blas_on(s);
     if (!h) return fail(FCR_EHIP, "rocblas_create_handle failed");
     WideArgs a = wide_args(d, L, base);
+    a.xb0 = sp.XB;
     a.X = X;
     a.u0 = u0;
     a.states = states;
@@ -487,7 +507,7 @@ int wide_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const 
         hipLaunchKernelGGL(wide_window_kernel<true>, dim3(nb), dim3(256), 0, s, a, j);
         if ((rc = launch_check("wide_window_kernel"))) return rc;
         if ((rc = wide_cells(h, a, wih, whh, false, &sp, s))) return rc;
-        hipLaunchKernelGGL(wide_readout_kernel, dim3(nb), dim3(256), 0, s, a, j,
+        hipLaunchKernelGGL(wide_readout_kernel, dim3((unsigned)(((size_t)d->B * kRoLanes + 255) / 256)), dim3(256), 0, s, a, j,
                            (const float *)(a.Hs + ((size_t)2 * kL + kL - 1) * d->B * H));
         if ((rc = launch_check("wide_readout_kernel"))) return rc;
     }
@@ -501,7 +521,7 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
                   const float *dloss, float *g_u0, float *g_w_inp, float *g_b_inp, float *g_w_out, char *base,
                   hipStream_t s) {
     const WideLayout L = make_wide(d, 1);
-    const int B = d->B, H = d->H;
+    const int B = d->B, H = d->H, H8 = H + 8;
     const size_t cell = (size_t)B * H;
     const int nb = (B + 255) / 256;
     int rc;
@@ -521,12 +541,13 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
     if (hipMemsetAsync(a.rowg, 0, sizeof(float) * (size_t)(d->N + kL - 1) * B * kIn, s) != hipSuccess)
         return fail(FCR_EHIP, "hipMemsetAsync failed");
     const WideSplit sp = wide_split(L, base);
+    a.xb0 = sp.XB;
     int kexp = 0;   // 2^kexp ~ B N: the dgates' scale into the f16 range (wide_bscale_kernel)
     while (kexp < 60 && (1LL << kexp) < (long long)B * d->N) ++kexp;
     hipLaunchKernelGGL(wide_bscale_kernel, dim3(1), dim3(64), 0, s, dloss, kexp, sp.consts);
     if ((rc = launch_check("wide_bscale_kernel"))) return rc;
     for (int j = d->N - 1; j >= 0; --j) {
-        hipLaunchKernelGGL(wide_head_kernel, dim3(nb), dim3(256), 0, s, a, j);
+        hipLaunchKernelGGL(wide_head_kernel, dim3((unsigned)(((size_t)B * kRoLanes + 255) / 256)), dim3(256), 0, s, a, j);
         if ((rc = launch_check("wide_head_kernel"))) return rc;
         hipLaunchKernelGGL(wide_window_kernel<false>, dim3(nb), dim3(256), 0, s, a, j);
         if ((rc = launch_check("wide_window_kernel"))) return rc;
@@ -537,17 +558,27 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
             if (hipMemsetAsync(a.dC, 0, sizeof(float) * cell, s) != hipSuccess) return fail(FCR_EHIP, "hipMemsetAsync failed");
             for (int t = kL - 1; t >= 0; --t) {
                 const size_t c_off = ((size_t)l * kL + t) * cell;
+                // layer 0 below t = 9 takes dh from the columns 0..H-1 of its combined product rows E0
+                const bool e0 = l == 0 && t < kL - 1;
                 if ((rc = launch_cell_bwd<true>(B, H, s, a.Act + c_off * 4, a.Cs + c_off, t > 0 ? a.Cs + c_off - cell : nullptr,
-                                                a.dH, l < kLayers - 1 ? D[l] + (size_t)t * cell : nullptr, a.dC,
-                                                l == 0 ? a.G : nullptr, sp.dGsp, sp.consts,
-                                                l < kLayers - 1 || t < kL - 1)))   // (2, 9): the head's dH
+                                                e0 ? sp.E0 : a.dH, l < kLayers - 1 ? D[l] + (size_t)t * cell : nullptr,
+                                                a.dC, nullptr, sp.dGsp, sp.consts,
+                                                l < kLayers - 1 || t < kL - 1,   // (2, 9): the head's dH
+                                                e0 ? H8 : H)))
                     return rc;
                 if (l > 0) {
-                    if ((rc = gemm16_bwd(h, B, H, sp.bih[l], sp.dGsp, D[l - 1] + (size_t)t * cell))) return rc;
-                } else {   // layer 0: the window rows' gradients, row j + t (K = 5: fp32)
-                    if ((rc = gemm_gw(h, B, 4 * H, kIn, wih[l], a.G, 1.0f, a.rowg + (size_t)(j + t) * B * kIn))) return rc;
+                    if ((rc = gemm16_bwd(h, B, H, H, sp.bih[l], H, sp.dGsp, D[l - 1] + (size_t)t * cell, H))) return rc;
+                    if (t > 0 && (rc = gemm16_bwd(h, B, H, H, sp.bhh[l], H, sp.dGsp, a.dH, H))) return rc;
+                } else {
+                    // layer 0: [dh_{t-1} | window-row gradient] in one product (t = 0: the latter only), then the
+                    // row gradient into rowg row j + t
+                    const int c0 = t > 0 ? 0 : H;
+                    if ((rc = gemm16_bwd(h, B, H8 - c0, H, sp.bx0 + c0, H8, sp.dGsp, sp.E0 + c0, H8))) return rc;
+                    hipLaunchKernelGGL(wide_rowg_kernel, dim3((unsigned)(((size_t)B * kIn + 255) / 256)), dim3(256), 0, s,
+                                       (const float *)(sp.E0 + H), H8, (const float *)sp.consts,
+                                       a.rowg + (size_t)(j + t) * B * kIn, B);
+                    if ((rc = launch_check("wide_rowg_kernel"))) return rc;
                 }
-                if (t > 0 && (rc = gemm16_bwd(h, B, H, sp.bhh[l], sp.dGsp, a.dH))) return rc;
             }
         }
     }
@@ -943,7 +974,7 @@ int fcr_lstm_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, 
             float *dG = dGs + (size_t)t * gcell;
             if ((rc = launch_cell_bwd<false>(B, H, s, a.Act + c_off * 4, a.Cs + c_off, t > 0 ? a.Cs + c_off - cell : nullptr,
                                              a.dH, l < kLayers - 1 ? D[l] + (size_t)t * cell : nullptr, a.dC, dG, nullptr,
-                                             nullptr, 0)))
+                                             nullptr, 0, H)))
                 return rc;
             if (l > 0) {
                 if ((rc = gemm_gw(h, B, 4 * H, H, w->w_ih[l], dG, 0.0f, D[l - 1] + (size_t)t * cell))) return rc;

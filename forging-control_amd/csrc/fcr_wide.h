@@ -27,7 +27,13 @@ struct WideArgs {
     float *xhat, *pred, *tot, *cmd, *err;
     float *X0, *Hs, *Cs, *Act, *G, *dH, *dC, *rowg, *dv;
     const float *dloss;
+    _Float16 *xb0;   // split-f16 rollout: layer-0 operand rows (slot stride B 6H, row stride 3H + kX16), else null
 };
+
+// layer 0's K = 5 window-row input as the last kX16 columns of its split-f16 operand rows and weights:
+// [x_hi (5) | x_lo (5) | x_hi (5) | 0] against [Wih_hi | Wih_hi | Wih_lo | 0]
+constexpr int kX16 = 16;
+static_assert(3 * kIn < kX16, "layer-0 input split exceeds its padded block");
 
 
 // controller (FNNModel.forward, Functions.py:261-289) pre-Hardtanh output, and its ReLU inputs' signs
@@ -74,8 +80,23 @@ __global__ void wide_window_kernel(WideArgs a, int j) {
         }
         a.pred[(size_t)b * a.N + j] = u;
     }
-    for (int t = 0; t < kL; ++t)
-        for (int col = 0; col < kIn; ++col) a.X0[((size_t)t * a.B + b) * kIn + col] = ext_row(a, b, j + t, col);
+    for (int t = 0; t < kL; ++t) {
+        float x[kIn];
+        for (int col = 0; col < kIn; ++col) {
+            x[col] = ext_row(a, b, j + t, col);
+            a.X0[((size_t)t * a.B + b) * kIn + col] = x[col];
+        }
+        if (a.xb0) {
+            _Float16 *p = a.xb0 + (size_t)t * a.B * 6 * a.H + (size_t)b * (3 * a.H + kX16) + 3 * a.H;
+            for (int col = 0; col < kIn; ++col) {
+                const _Float16 hi = (_Float16)x[col];
+                p[col] = hi;
+                p[kIn + col] = (_Float16)(x[col] - (float)hi);
+                p[2 * kIn + col] = hi;
+            }
+            for (int k = 3 * kIn; k < kX16; ++k) p[k] = (_Float16)0.0f;
+        }
+    }
 }
 
 // Cell update from the gate pre-activations G [B][4H] (torch gate order i|f|g|o): c, h; and, for the
@@ -145,14 +166,25 @@ __global__ void wide_cell_kernel(const float *__restrict__ G, const float *__res
 
 // Readout fc(h_9 of layer 2) (Functions.py:377), noise (:1400-1402), and the step's error and
 // constraint costs (:1405-1414, :1443-1452).
+// kRoLanes lanes per trajectory: each lane reads a strided slice of the trajectory's h row (the group's
+// loads of one row are contiguous: coalesced), partial dot products reduced across the group by shuffles.
+constexpr int kRoLanes = 16;
 __global__ void wide_readout_kernel(WideArgs a, int j, const float *__restrict__ h) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= a.B) return;
+    const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = (int)(gid / kRoLanes), q = (int)(gid % kRoLanes);
+    const bool live = b < a.B;
     float xo[kOut];
     for (int o = 0; o < kOut; ++o) {
         float s = 0.0f;
-        for (int u = 0; u < a.H; ++u) s += a.fcw[o * a.H + u] * h[(size_t)b * a.H + u];
-        xo[o] = s + a.fcb[o] + (a.noise ? a.noise[((size_t)b * a.N + j) * kOut + o] : 0.0f);
+        if (live)
+            for (int u = q; u < a.H; u += kRoLanes) s += a.fcw[o * a.H + u] * h[(size_t)b * a.H + u];
+#pragma unroll
+        for (int m = kRoLanes / 2; m > 0; m >>= 1) s += __shfl_xor(s, m, kRoLanes);
+        xo[o] = s;
+    }
+    if (!live || q != 0) return;
+    for (int o = 0; o < kOut; ++o) {
+        xo[o] += a.fcb[o] + (a.noise ? a.noise[((size_t)b * a.N + j) * kOut + o] : 0.0f);
         a.xhat[((size_t)b * a.N + j) * kOut + o] = xo[o];
     }
     const float ref = a.X[(size_t)b * kCtrlIn + 2];
@@ -176,9 +208,8 @@ __global__ void wide_finish_kernel(WideArgs a, float *cost, float *command, floa
 // Backward head of window j: d loss / d xhat_j from the step costs and from every later window that
 // read row 10+j (rowg), the controller's backward at (xhat_j[0], xhat_j[3], ref) (stores dv for the
 // parameter gradients), and dh_9 of layer 2 = fc.Wᵀ dxhat_j into dH. Same algebra as fcr_bwd.h.
-__global__ void wide_head_kernel(WideArgs a, int j) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= a.B) return;
+// kRoLanes lanes per trajectory: the group's first lane runs the scalar algebra, all of them write dH.
+__device__ __forceinline__ void wide_head_dxhat(const WideArgs &a, int j, int b, float (&d)[kOut]) {
     const int N = a.N;
     const float wgt = a.dloss[0] / ((float)a.B * (float)N);
     const float ref = a.X[(size_t)b * kCtrlIn + 2];
@@ -212,8 +243,22 @@ __global__ void wide_head_kernel(WideArgs a, int j) {
     } else {
         a.dv[(size_t)b * N + j] = 0.0f;
     }
-    for (int u = 0; u < a.H; ++u)
-        a.dH[(size_t)b * a.H + u] = a.fcw[u] * d0 + a.fcw[a.H + u] * d1 + a.fcw[2 * a.H + u] * d2 + a.fcw[3 * a.H + u] * d3;
+    d[0] = d0;
+    d[1] = d1;
+    d[2] = d2;
+    d[3] = d3;
+}
+__global__ void wide_head_kernel(WideArgs a, int j) {
+    const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = (int)(gid / kRoLanes), q = (int)(gid % kRoLanes);
+    const bool live = b < a.B;
+    float d[kOut] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (live && q == 0) wide_head_dxhat(a, j, b, d);
+#pragma unroll
+    for (int k = 0; k < kOut; ++k) d[k] = __shfl(d[k], 0, kRoLanes);
+    if (!live) return;
+    for (int u = q; u < a.H; u += kRoLanes)
+        a.dH[(size_t)b * a.H + u] = a.fcw[u] * d[0] + a.fcw[a.H + u] * d[1] + a.fcw[2 * a.H + u] * d[2] + a.fcw[3 * a.H + u] * d[3];
 }
 
 // Backward of one cell: from the activations, c_t, c_{t-1}, the incoming dh (carried dH + din from the
@@ -225,7 +270,7 @@ template <bool PRE, int V>
 __global__ void wide_cell_bwd_kernel(const float *__restrict__ act, const float *__restrict__ c,
                                      const float *__restrict__ c_prev, const float *__restrict__ dH,
                                      const float *__restrict__ din, float *dC, float *dG, _Float16 *dgsp,
-                                     const float *__restrict__ consts, int dh_scaled, int B, int H) {
+                                     const float *__restrict__ consts, int dh_scaled, int ldh, int B, int H) {
     using W = WideVec<V>;
     // with consts (split-f16 rollout) din, and dH unless it is the head's, come from gemm16_bwd in the
     // scaled units of the dgates: back by 1/scale = consts[0], one fp32 product each
@@ -236,7 +281,7 @@ __global__ void wide_cell_bwd_kernel(const float *__restrict__ act, const float 
     const size_t b = iv / HV, u = (iv % HV) * V, idx = b * H + u;
     const float *a4 = act + b * 4 * H + u;
     const typename W::F ai = W::ld(a4), af = W::ld(a4 + H), ag = W::ld(a4 + 2 * H), ao = W::ld(a4 + 3 * H);
-    const typename W::F cv = W::ld(c + idx), dhv = W::ld(dH + idx), dcv = W::ld(dC + idx);
+    const typename W::F cv = W::ld(c + idx), dhv = W::ld(dH + b * ldh + u), dcv = W::ld(dC + idx);
     typename W::F cp = {}, dn = {}, dg[4], dco;
     if (c_prev) cp = W::ld(c_prev + idx);
     if (din) dn = W::ld(din + idx);
@@ -282,17 +327,35 @@ __global__ void wide_cell_bwd_kernel(const float *__restrict__ act, const float 
 // for the fused kernels): every product a.b becomes a_hi b_hi + a_hi b_lo + a_lo b_hi, laid out as ONE
 // K-concatenated GEMM per cell so the fp32 gate matrix is written once (C traffic, not the MFMA, bounded
 // the per-term calls). Forward A, row-major [4H][6H] = [Wih_hi | Wih_hi | Wih_lo | Whh_hi | Whh_hi | Whh_lo]
-// against operand rows [x_hi | x_lo | x_hi | h_hi | h_lo | h_hi] (layer 0: the W_hh half only, its K = 5
-// input product stays fp32); backward A, row-major [12H][H] = [W_hi ; W_hi ; W_lo] against
+// against operand rows [x_hi | x_lo | x_hi | h_hi | h_lo | h_hi] (layer 0: [h part | x part of kX16 columns]);
+// backward A, row-major [12H][H] = [W_hi ; W_hi ; W_lo] against
 // [dG_hi | dG_lo | dG_hi].
-__global__ void wide_split_fa_kernel(const float *__restrict__ Wih, const float *__restrict__ Whh, int H,
+__global__ void wide_split_fa_kernel(const float *__restrict__ Wih, const float *__restrict__ Whh, int H, int layer0,
                                      _Float16 *dst) {
-    const int KA = Wih ? 6 * H : 3 * H;
+    const int KA = layer0 ? 3 * H + kX16 : 6 * H;
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (size_t)4 * H * KA) return;
     const int r = (int)(idx / KA), k = (int)(idx % KA);
-    const int part = Wih ? k / (3 * H) : 1, kk = k % (3 * H), term = kk / H, u = kk % H;
-    const float v = (part == 0 ? Wih : Whh)[(size_t)r * H + u];
+    float v;
+    int term;
+    if (layer0) {
+        if (k < 3 * H) {
+            term = k / H;
+            v = Whh[(size_t)r * H + k % H];
+        } else {
+            const int kk = k - 3 * H;
+            if (kk >= 3 * kIn) {
+                dst[idx] = (_Float16)0.0f;
+                return;
+            }
+            term = kk / kIn;
+            v = Wih[(size_t)r * kIn + kk % kIn];
+        }
+    } else {
+        const int part = k / (3 * H), kk = k % (3 * H), u = kk % H;
+        term = kk / H;
+        v = (part == 0 ? Wih : Whh)[(size_t)r * H + u];
+    }
     const _Float16 hi = (_Float16)v;
     dst[idx] = term < 2 ? hi : (_Float16)(v - (float)hi);
 }
@@ -304,6 +367,29 @@ __global__ void wide_split_ba_kernel(const float *__restrict__ W, int H, _Float1
     const float v = W[idx % n];
     const _Float16 hi = (_Float16)v;
     dst[idx] = term < 2 ? hi : (_Float16)(v - (float)hi);
+}
+
+// Layer 0's backward A, row-major [12H][H + 8]: per split row the W_hh row (H columns), then the W_ih row
+// (kIn columns) and zero padding — ONE product gives dh_{t-1} and the window-row gradient of the cell.
+__global__ void wide_split_bx0_kernel(const float *__restrict__ Wih, const float *__restrict__ Whh, int H,
+                                      _Float16 *dst) {
+    const int ld = H + 8;
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)12 * H * ld) return;
+    const int r = (int)(idx / ld), col = (int)(idx % ld), term = r / (4 * H), g = r % (4 * H);
+    float v = 0.0f;
+    if (col < H) v = Whh[(size_t)g * H + col];
+    else if (col < H + kIn) v = Wih[(size_t)g * kIn + col - H];
+    const _Float16 hi = (_Float16)v;
+    dst[idx] = term < 2 ? hi : (_Float16)(v - (float)hi);
+}
+// rowg row += the window-row gradient part of layer 0's backward product (scaled units, see dh_scaled)
+__global__ void wide_rowg_kernel(const float *__restrict__ E, int ldE, const float *__restrict__ consts, float *rowg,
+                                 int B) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)B * kIn) return;
+    const size_t b = idx / kIn, col = idx % kIn;
+    rowg[idx] += consts[0] * E[b * ldE + col];
 }
 
 // The dgates are split as dG * 2^k / dloss (|dG| ~ dloss / (B N): without it they would sit in the f16
