@@ -180,7 +180,7 @@ struct WideLayout {
     size_t Act, dH, dC, D[2], rowg, dv, fnn_part, total;
     // split-f16 gate GEMM operands (fcr_wide.h: forward A per layer, backward A per weight, the cells'
     // operand rows XB [3][10][B][6H] (layer 0 rows 3H + kX16 long), the dgate rows [B][12H])
-    size_t fa[3], bih[3], bhh[3], XB, dGsp, consts;
+    size_t fa[3], bih[3], XB, dGsp, consts;   // bih: layers >= 1 backward A [12H][2H]
     size_t bx0, E0;   // layer 0's backward A [12H][H + 8] and its product rows [B][H + 8]
     int ctrl_blocks;
 };
@@ -219,8 +219,7 @@ WideLayout make_wide(const fcr_dims *d, int with_backward) {
         L.fa[l] = take(l == 0 ? F16 * 4 * H * (3 * H + kX16) : F16 * WW * 6);
         if (with_backward) {
             if (l > 0) {
-                L.bih[l] = take(F16 * 3 * WW);
-                L.bhh[l] = take(F16 * 3 * WW);
+                L.bih[l] = take(F16 * 6 * WW);   // [12H][2H]: W_ih | W_hh per split row (wide_split_bcat_kernel)
             } else {
                 L.bx0 = take(F16 * 12 * H * (H + 8));
             }
@@ -234,8 +233,8 @@ WideLayout make_wide(const fcr_dims *d, int with_backward) {
         L.Act = take(F * kLayers * kL * B * 4 * H);
         L.dH = take(F * B * H);
         L.dC = take(F * B * H);
-        L.D[0] = take(F * kL * B * H);
-        L.D[1] = take(F * kL * B * H);
+        L.D[0] = take(F * kL * B * 2 * H);   // per t: [input gradient of the layer above | its dh_{t-1}]
+        L.D[1] = take(F * kL * B * 2 * H);
         L.rowg = take(F * (N + kL - 1) * B * kIn);
         L.dv = take(F * B * N);
         L.ctrl_blocks = (int)(((long long)B * N + kCtrlItems - 1) / kCtrlItems);
@@ -283,7 +282,7 @@ int gemm16_fwd(rocblas_handle h, int B, int H4, int K, const _Float16 *A, int ld
                                               rocblas_datatype_f32_r, rocblas_gemm_algo_standard, 0, 0);
     return st == rocblas_status_success ? FCR_OK : fail(FCR_EHIP, "rocblas_gemm_ex (forward, f16 split) failed: %d", (int)st);
 }
-// dX' (row-major B x H) = dGs A on split-f16 operands: A row-major [12H][H] = [W_hi ; W_hi ; W_lo], dGs row-major
+// dX' (row-major B x n) = dGs A on split-f16 operands: A row-major [12H][lda] = [W_hi ; W_hi ; W_lo], dGs row-major
 // [B][12H] = [hi | lo | hi] of dG * scale. dX' stays in the scaled units: its consumer (wide_cell_bwd_kernel)
 // multiplies by 1/scale = consts[0] on load — the same single fp32 product a device-pointer alpha would apply,
 // without the per-call alpha/beta copies rocBLAS launches in device pointer mode.
@@ -299,7 +298,7 @@ int gemm16_bwd(rocblas_handle h, int B, int n, int H, const _Float16 *A, int lda
 
 // Device pointers of the split-f16 operands (rollout only; the surrogate's training step stays fp32)
 struct WideSplit {
-    const _Float16 *fa[kLayers], *bih[kLayers], *bhh[kLayers];
+    const _Float16 *fa[kLayers], *bih[kLayers];
     _Float16 *XB, *dGsp;
     float *consts;
     const _Float16 *bx0;
@@ -311,7 +310,6 @@ WideSplit wide_split(const WideLayout &L, char *base) {
     for (int l = 0; l < kLayers; ++l) {
         w.fa[l] = (const _Float16 *)(base + L.fa[l]);
         w.bih[l] = L.bih[l] ? (const _Float16 *)(base + L.bih[l]) : nullptr;
-        w.bhh[l] = L.bhh[l] ? (const _Float16 *)(base + L.bhh[l]) : nullptr;
     }
     w.XB = (_Float16 *)(base + L.XB);
     w.dGsp = L.dGsp ? (_Float16 *)(base + L.dGsp) : nullptr;
@@ -339,11 +337,9 @@ int wide_pack_split(const float *const *w_ih, const float *const *w_hh, int H, b
             if ((rc = launch_check("wide_split_bx0_kernel"))) return rc;
             continue;
         }
-        for (int k = 0; k < 2; ++k) {
-            hipLaunchKernelGGL(wide_split_ba_kernel, dim3((unsigned)((3 * WW + 255) / 256)), dim3(256), 0, s,
-                               k == 0 ? w_ih[l] : w_hh[l], H, (_Float16 *)(k == 0 ? sp.bih[l] : sp.bhh[l]));
-            if ((rc = launch_check("wide_split_ba_kernel"))) return rc;
-        }
+        hipLaunchKernelGGL(wide_split_bcat_kernel, dim3((unsigned)((6 * WW + 255) / 256)), dim3(256), 0, s, w_ih[l],
+                           w_hh[l], H, (_Float16 *)sp.bih[l]);
+        if ((rc = launch_check("wide_split_bcat_kernel"))) return rc;
     }
     return FCR_OK;
 }
@@ -395,15 +391,15 @@ int launch_cell(int B, int H, hipStream_t s, const float *G, const float *c_prev
 template <bool PRE>
 int launch_cell_bwd(int B, int H, hipStream_t s, const float *act, const float *c, const float *c_prev,
                     const float *dH, const float *din, float *dC, float *dG, _Float16 *dgsp, const float *consts,
-                    int dh_scaled, int ldh) {
+                    int dh_scaled, int ldh, int ldx) {
     const int V = cell_vec(H);
     const dim3 grid((unsigned)(((size_t)B * (H / V) + 255) / 256)), blk(256);
     if (V == 4)
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, B, H);
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H);
     else if (V == 2)
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 2>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, B, H);
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 2>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H);
     else
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 1>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, B, H);
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 1>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H);
     return launch_check("wide_cell_bwd_kernel");
 }
 
@@ -558,17 +554,20 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
             if (hipMemsetAsync(a.dC, 0, sizeof(float) * cell, s) != hipSuccess) return fail(FCR_EHIP, "hipMemsetAsync failed");
             for (int t = kL - 1; t >= 0; --t) {
                 const size_t c_off = ((size_t)l * kL + t) * cell;
-                // layer 0 below t = 9 takes dh from the columns 0..H-1 of its combined product rows E0
-                const bool e0 = l == 0 && t < kL - 1;
+                // dh_t below t = 9 comes from cell t+1's combined product: layer 0 columns 0..H-1 of E0, layers
+                // >= 1 columns H..2H-1 of D[l-1] row t+1; the layer above's input gradient from D[l] row t
+                const float *dh_src = t == kL - 1 ? a.dH : l == 0 ? sp.E0 : D[l - 1] + (size_t)(t + 1) * 2 * cell + H;
+                const int ldh = t == kL - 1 ? H : l == 0 ? H8 : 2 * H;
                 if ((rc = launch_cell_bwd<true>(B, H, s, a.Act + c_off * 4, a.Cs + c_off, t > 0 ? a.Cs + c_off - cell : nullptr,
-                                                e0 ? sp.E0 : a.dH, l < kLayers - 1 ? D[l] + (size_t)t * cell : nullptr,
-                                                a.dC, nullptr, sp.dGsp, sp.consts,
+                                                dh_src, l < kLayers - 1 ? D[l] + (size_t)t * 2 * cell : nullptr, a.dC,
+                                                nullptr, sp.dGsp, sp.consts,
                                                 l < kLayers - 1 || t < kL - 1,   // (2, 9): the head's dH
-                                                e0 ? H8 : H)))
+                                                ldh, 2 * H)))
                     return rc;
-                if (l > 0) {
-                    if ((rc = gemm16_bwd(h, B, H, H, sp.bih[l], H, sp.dGsp, D[l - 1] + (size_t)t * cell, H))) return rc;
-                    if (t > 0 && (rc = gemm16_bwd(h, B, H, H, sp.bhh[l], H, sp.dGsp, a.dH, H))) return rc;
+                if (l > 0) {   // [input gradient | dh_{t-1}] (t = 0: the former only) into D[l-1] row t
+                    if ((rc = gemm16_bwd(h, B, t > 0 ? 2 * H : H, H, sp.bih[l], 2 * H, sp.dGsp, D[l - 1] + (size_t)t * 2 * cell,
+                                         2 * H)))
+                        return rc;
                 } else {
                     // layer 0: [dh_{t-1} | window-row gradient] in one product (t = 0: the latter only), then the
                     // row gradient into rowg row j + t
@@ -974,7 +973,7 @@ int fcr_lstm_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, 
             float *dG = dGs + (size_t)t * gcell;
             if ((rc = launch_cell_bwd<false>(B, H, s, a.Act + c_off * 4, a.Cs + c_off, t > 0 ? a.Cs + c_off - cell : nullptr,
                                              a.dH, l < kLayers - 1 ? D[l] + (size_t)t * cell : nullptr, a.dC, dG, nullptr,
-                                             nullptr, 0, H)))
+                                             nullptr, 0, H, H)))
                 return rc;
             if (l > 0) {
                 if ((rc = gemm_gw(h, B, 4 * H, H, w->w_ih[l], dG, 0.0f, D[l - 1] + (size_t)t * cell))) return rc;

@@ -270,7 +270,8 @@ template <bool PRE, int V>
 __global__ void wide_cell_bwd_kernel(const float *__restrict__ act, const float *__restrict__ c,
                                      const float *__restrict__ c_prev, const float *__restrict__ dH,
                                      const float *__restrict__ din, float *dC, float *dG, _Float16 *dgsp,
-                                     const float *__restrict__ consts, int dh_scaled, int ldh, int B, int H) {
+                                     const float *__restrict__ consts, int dh_scaled, int ldh, int ldx, int B,
+                                     int H) {
     using W = WideVec<V>;
     // with consts (split-f16 rollout) din, and dH unless it is the head's, come from gemm16_bwd in the
     // scaled units of the dgates: back by 1/scale = consts[0], one fp32 product each
@@ -284,7 +285,7 @@ __global__ void wide_cell_bwd_kernel(const float *__restrict__ act, const float 
     const typename W::F cv = W::ld(c + idx), dhv = W::ld(dH + b * ldh + u), dcv = W::ld(dC + idx);
     typename W::F cp = {}, dn = {}, dg[4], dco;
     if (c_prev) cp = W::ld(c_prev + idx);
-    if (din) dn = W::ld(din + idx);
+    if (din) dn = W::ld(din + b * ldx + u);
 #pragma unroll
     for (int k = 0; k < V; ++k) {
         const float i = PRE ? sigm(ai[k]) : ai[k], f = PRE ? sigm(af[k]) : af[k], g = PRE ? tanhf(ag[k]) : ag[k],
@@ -328,8 +329,7 @@ __global__ void wide_cell_bwd_kernel(const float *__restrict__ act, const float 
 // K-concatenated GEMM per cell so the fp32 gate matrix is written once (C traffic, not the MFMA, bounded
 // the per-term calls). Forward A, row-major [4H][6H] = [Wih_hi | Wih_hi | Wih_lo | Whh_hi | Whh_hi | Whh_lo]
 // against operand rows [x_hi | x_lo | x_hi | h_hi | h_lo | h_hi] (layer 0: [h part | x part of kX16 columns]);
-// backward A, row-major [12H][H] = [W_hi ; W_hi ; W_lo] against
-// [dG_hi | dG_lo | dG_hi].
+// backward A (below) stacks [W_hi ; W_hi ; W_lo] (12H rows) against the dgate rows [dG_hi | dG_lo | dG_hi].
 __global__ void wide_split_fa_kernel(const float *__restrict__ Wih, const float *__restrict__ Whh, int H, int layer0,
                                      _Float16 *dst) {
     const int KA = layer0 ? 3 * H + kX16 : 6 * H;
@@ -359,15 +359,6 @@ __global__ void wide_split_fa_kernel(const float *__restrict__ Wih, const float 
     const _Float16 hi = (_Float16)v;
     dst[idx] = term < 2 ? hi : (_Float16)(v - (float)hi);
 }
-__global__ void wide_split_ba_kernel(const float *__restrict__ W, int H, _Float16 *dst) {
-    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t n = (size_t)4 * H * H;
-    if (idx >= 3 * n) return;
-    const int term = (int)(idx / n);
-    const float v = W[idx % n];
-    const _Float16 hi = (_Float16)v;
-    dst[idx] = term < 2 ? hi : (_Float16)(v - (float)hi);
-}
 
 // Layer 0's backward A, row-major [12H][H + 8]: per split row the W_hh row (H columns), then the W_ih row
 // (kIn columns) and zero padding — ONE product gives dh_{t-1} and the window-row gradient of the cell.
@@ -380,6 +371,17 @@ __global__ void wide_split_bx0_kernel(const float *__restrict__ Wih, const float
     float v = 0.0f;
     if (col < H) v = Whh[(size_t)g * H + col];
     else if (col < H + kIn) v = Wih[(size_t)g * kIn + col - H];
+    const _Float16 hi = (_Float16)v;
+    dst[idx] = term < 2 ? hi : (_Float16)(v - (float)hi);
+}
+// Layers >= 1: backward A row-major [12H][2H], per split row [W_ih row | W_hh row] — ONE product gives the
+// cell's input gradient (the layer below's incoming dh) and dh_{t-1}, side by side in rows of 2H.
+__global__ void wide_split_bcat_kernel(const float *__restrict__ Wih, const float *__restrict__ Whh, int H,
+                                       _Float16 *dst) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)24 * H * H) return;
+    const int r = (int)(idx / (2 * H)), col = (int)(idx % (2 * H)), term = r / (4 * H), g = r % (4 * H);
+    const float v = col < H ? Wih[(size_t)g * H + col] : Whh[(size_t)g * H + col - H];
     const _Float16 hi = (_Float16)v;
     dst[idx] = term < 2 ? hi : (_Float16)(v - (float)hi);
 }
