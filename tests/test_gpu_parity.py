@@ -243,3 +243,23 @@ def test_wide_path_any_incoming_gradient_scale(dloss):
     o = run(params, c["X"], c["u0"], c["states"], c["N"], c["alpha"], c["noise"], dloss=dloss)
     for k, _ in GRADS:
         assert relerr(o[k] / dloss, c[f"{k}_64"]) <= TOL, (k, relerr(o[k] / dloss, c[f"{k}_64"]))
+
+
+@pytest.mark.parametrize("H,B,N", [(54, 300, 3), (57, 77, 2), (96, 520, 4)])
+def test_wide_path_hidden_sizes(H, B, N):
+    """H > 52 at sizes the golden cases do not hit: even H not a multiple of 4 (cell kernels 2 units per
+    thread), odd H (1 unit per thread), and a multiple of 4 at a few hundred trajectories — the window-row
+    columns inside layer 0's split GEMM and the combined [input gradient | dh] backward products, against
+    the fp64 oracle on seeded synthetic weights (parity unpinned: no reference output at these sizes)."""
+    from tests.golden.make_golden import synth_params
+    params = synth_params(H, 300 + H)
+    X, S, _ = _synth(B, N, 400 + H)
+    u0 = _u0(params, X)
+    o = run(params, X, u0, S, N, 20.0)
+    _, f, tape = R.rollout_forward(params, X, u0, S, N, 20.0)
+    g = R.rollout_backward(params, tape)
+    for k in FEATS:
+        assert relerr(o[k], f[k]) <= TOL, (H, k, relerr(o[k], f[k]))
+    assert relerr(o["xhat"], f["xhat"]) <= TOL
+    for k, _ in GRADS:
+        assert relerr(o[k], g[k]) <= TOL, (H, k, relerr(o[k], g[k]))
