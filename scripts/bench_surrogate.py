@@ -11,13 +11,11 @@ import os
 import sys
 import time
 
-import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
-import forging_control_amd as fca  # noqa: E402
 from oracle import surrogate_torch as S  # noqa: E402
 
 

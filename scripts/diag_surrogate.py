@@ -2,7 +2,7 @@
 import sys, os
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "tests"))
-import numpy as np, torch
+import torch
 from test_surrogate import params_for, batch, model_for, grads_of
 from oracle import surrogate_torch as S
 from conftest import relerr
