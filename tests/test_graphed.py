@@ -103,3 +103,38 @@ def test_graphed_surrogate_training_matches_eager():
         for a, b in zip(m.parameters(), m_g.parameters()):
             assert torch.equal(a, b)
     assert step.replays == 2 * 5 - step.warmup
+
+
+@pytest.mark.gpu
+def test_graphed_step_with_grad_sync_matches_eager():
+    """With a data-parallel grad_sync hook the captured step is two graphs (forward + backward, then AdamW)
+    around the eager RCCL all-reduce; one rank on the box's GPU exercises that split against the eager loop."""
+    import os
+    import socket
+
+    import torch.distributed as dist
+
+    dev = torch.device("cuda", 0)
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    try:
+        sim, ctrl = _controller_setup(dev, seed=5)
+        ctrl_g = copy.deepcopy(ctrl)
+        loss_fn = fca.MPCLoss(prediction_horizon=10, alpha=20.0)
+        opt = torch.optim.AdamW(ctrl.parameters(), lr=1e-3, capturable=True)
+        opt_g = torch.optim.AdamW(ctrl_g.parameters(), lr=1e-3, capturable=True)
+        sync = fca.distributed.GradAllReduce()
+        loader = _controller_batches(dev, [32] * 5, seed=6)
+        step = fca.NeuralNetwork.captured_step(sim, ctrl_g, loss_fn, opt_g, dev, grad_sync=sync)
+        for _ in range(2):
+            l_e, _ = fca.NeuralNetwork.train_model(loader, sim, ctrl, loss_fn, opt, dev, grad_sync=sync)
+            l_g, _ = fca.NeuralNetwork.train_model(loader, sim, ctrl_g, loss_fn, opt_g, dev, grad_sync=sync, step=step)
+            assert abs(l_g - l_e) <= 1e-6 * abs(l_e)
+            for a, b in zip(ctrl.parameters(), ctrl_g.parameters()):
+                assert torch.equal(a, b)
+        assert step.replays == 2 * 5 - step.warmup and step._g_opt is not None
+    finally:
+        dist.destroy_process_group()
