@@ -228,7 +228,7 @@ WideLayout make_wide(const fcr_dims *d, int with_backward) {
     L.XB = take(F16 * kLayers * kL * B * 6 * H);
     if (with_backward) {
         L.dGsp = take(F16 * B * 12 * H);
-        L.E0 = take(F * B * (H + 8));
+        L.E0 = take(F * B * ((H + 8 + 31) / 32 * 32));
         L.consts = take(F * 4);
         L.Act = take(F * kLayers * kL * B * 4 * H);
         L.dH = take(F * B * H);
@@ -411,7 +411,7 @@ int wide_cells(rocblas_handle h, const WideArgs &a, const float *const *w_ih, co
     const int B = a.B, H = a.H;
     const size_t cell = (size_t)B * H;
     // operand rows of cell (l, t): layer >= 1 [x part 3H | h part 3H], layer 0 [h part 3H]
-    auto ldx = [&](int l) { return l == 0 ? 3 * H + kX16 : 6 * H; };
+    auto ldx = [&](int l) { return l == 0 ? xb0_ld(H) : 6 * H; };
     auto xb = [&](int l, int t) { return sp->XB + ((size_t)l * kL + t) * B * 6 * H; };
     int rc;
     for (int l = 0; l < kLayers; ++l) {
@@ -424,7 +424,7 @@ int wide_cells(rocblas_handle h, const WideArgs &a, const float *const *w_ih, co
             if (sp) {
                 if (l == 0) {   // [h part | window-row part] (wide_window_kernel writes the latter); t = 0: no h
                     const int k0 = t > 0 ? 0 : 3 * H;
-                    if ((rc = gemm16_fwd(h, B, 4 * H, 3 * H + kX16 - k0, sp->fa[0] + k0, ldx(0), xb(0, t) + k0, ldx(0),
+                    if ((rc = gemm16_fwd(h, B, 4 * H, 3 * H + kX16 - k0, sp->fa[0] + k0, 3 * H + kX16, xb(0, t) + k0, ldx(0),
                                          0.0f, G)))
                         return rc;
                 } else if ((rc = gemm16_fwd(h, B, 4 * H, t > 0 ? 6 * H : 3 * H, sp->fa[l], 6 * H, xb(l, t), 6 * H, 0.0f,
@@ -518,6 +518,7 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
                   hipStream_t s) {
     const WideLayout L = make_wide(d, 1);
     const int B = d->B, H = d->H, H8 = H + 8;
+    const int LE = (H8 + 31) / 32 * 32;   // E0 rows padded to whole 128-B lines
     const size_t cell = (size_t)B * H;
     const int nb = (B + 255) / 256;
     int rc;
@@ -557,7 +558,7 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
                 // dh_t below t = 9 comes from cell t+1's combined product: layer 0 columns 0..H-1 of E0, layers
                 // >= 1 columns H..2H-1 of D[l-1] row t+1; the layer above's input gradient from D[l] row t
                 const float *dh_src = t == kL - 1 ? a.dH : l == 0 ? sp.E0 : D[l - 1] + (size_t)(t + 1) * 2 * cell + H;
-                const int ldh = t == kL - 1 ? H : l == 0 ? H8 : 2 * H;
+                const int ldh = t == kL - 1 ? H : l == 0 ? LE : 2 * H;
                 if ((rc = launch_cell_bwd<true>(B, H, s, a.Act + c_off * 4, a.Cs + c_off, t > 0 ? a.Cs + c_off - cell : nullptr,
                                                 dh_src, l < kLayers - 1 ? D[l] + (size_t)t * 2 * cell : nullptr, a.dC,
                                                 nullptr, sp.dGsp, sp.consts,
@@ -572,9 +573,9 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
                     // layer 0: [dh_{t-1} | window-row gradient] in one product (t = 0: the latter only), then the
                     // row gradient into rowg row j + t
                     const int c0 = t > 0 ? 0 : H;
-                    if ((rc = gemm16_bwd(h, B, H8 - c0, H, sp.bx0 + c0, H8, sp.dGsp, sp.E0 + c0, H8))) return rc;
+                    if ((rc = gemm16_bwd(h, B, H8 - c0, H, sp.bx0 + c0, H8, sp.dGsp, sp.E0 + c0, LE))) return rc;
                     hipLaunchKernelGGL(wide_rowg_kernel, dim3((unsigned)(((size_t)B * kIn + 255) / 256)), dim3(256), 0, s,
-                                       (const float *)(sp.E0 + H), H8, (const float *)sp.consts,
+                                       (const float *)(sp.E0 + H), LE, (const float *)sp.consts,
                                        a.rowg + (size_t)(j + t) * B * kIn, B);
                     if ((rc = launch_check("wide_rowg_kernel"))) return rc;
                 }

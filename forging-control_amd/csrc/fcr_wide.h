@@ -27,13 +27,16 @@ struct WideArgs {
     float *xhat, *pred, *tot, *cmd, *err;
     float *X0, *Hs, *Cs, *Act, *G, *dH, *dC, *rowg, *dv;
     const float *dloss;
-    _Float16 *xb0;   // split-f16 rollout: layer-0 operand rows (slot stride B 6H, row stride 3H + kX16), else null
+    _Float16 *xb0;   // split-f16 rollout: layer-0 operand rows (slot stride B 6H, row stride xb0_ld), else null
 };
 
 // layer 0's K = 5 window-row input as the last kX16 columns of its split-f16 operand rows and weights:
 // [x_hi (5) | x_lo (5) | x_hi (5) | 0] against [Wih_hi | Wih_hi | Wih_lo | 0]
 constexpr int kX16 = 16;
 static_assert(3 * kIn < kX16, "layer-0 input split exceeds its padded block");
+// row stride of layer 0's operand rows [h part 3H | x part kX16], padded to whole 128-B lines (rows that
+// straddle lines cost the GEMM's operand loads)
+__host__ __device__ constexpr int xb0_ld(int H) { return (3 * H + kX16 + 63) / 64 * 64; }
 
 
 // controller (FNNModel.forward, Functions.py:261-289) pre-Hardtanh output, and its ReLU inputs' signs
@@ -87,7 +90,7 @@ __global__ void wide_window_kernel(WideArgs a, int j) {
             a.X0[((size_t)t * a.B + b) * kIn + col] = x[col];
         }
         if (a.xb0) {
-            _Float16 *p = a.xb0 + (size_t)t * a.B * 6 * a.H + (size_t)b * (3 * a.H + kX16) + 3 * a.H;
+            _Float16 *p = a.xb0 + (size_t)t * a.B * 6 * a.H + (size_t)b * xb0_ld(a.H) + 3 * a.H;
             for (int col = 0; col < kIn; ++col) {
                 const _Float16 hi = (_Float16)x[col];
                 p[col] = hi;
