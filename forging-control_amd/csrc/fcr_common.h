@@ -33,13 +33,13 @@ constexpr int kFwdWaves = FCR_FWD_WAVES;  // waves per forward workgroup (8 = 2 
 #ifndef FCR_BWD_WAVES
 #define FCR_BWD_WAVES 8
 #endif
-constexpr int kBwdWaves = FCR_BWD_WAVES;
+constexpr int kBwdWaves = FCR_BWD_WAVES;   // waves per backward workgroup (8 = 2 per SIMD)
 // One accumulator per gate tile (a dependent 16x16x32 MFMA chain issues back to back, MI355X_MICROARCH.md)
 // instead of two over alternate k-blocks, whose final sum costs packed-f32 adds beside the MFMAs.
 #ifndef FCR_ONEACC
 #define FCR_ONEACC 1
 #endif
-constexpr bool kOneAcc = FCR_ONEACC;   // waves per backward workgroup (8 = 2 per SIMD)
+constexpr bool kOneAcc = FCR_ONEACC;
 constexpr float kP1Max = 2.122366f;  // Functions.py:1411 (32e6 / p1 max_abs_)
 constexpr float kP2Max = 1.036233f;  // Functions.py:1411 (32e6 / p2 max_abs_)
 

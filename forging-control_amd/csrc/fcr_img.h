@@ -1,5 +1,5 @@
 // fcr_img.h — one LDS image of a layer's weights that serves BOTH matrix products of the
-// recompute-in-backward cell (fcr_bwd4.h):
+// recompute-in-backward cell (fcr_bwd.h):
 //   forward  gates = W · [x ; h_{t-1}]        A operand = 8 consecutive INPUT columns of one gate row
 //   backward [dx ; dh_prev] = Wᵀ · dgates     A operand = 8 consecutive GATE rows of one input column
 // A fragment always holds 8 consecutive k per lane, so the two products need the weights contiguous
