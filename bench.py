@@ -99,37 +99,145 @@ def synth_batch(B, dev, seed):
     return X.to(dev), S.to(dev)
 
 
-def cpu_baseline(budget_s=15.0, B=256, N=10, threads=None):
-    """The reference CPU path (stock torch ops in MPCLoss's order, oracle/rollout_torch.py) timed on the
-    host: forward + backward + AdamW per step, on a bounded sample."""
+def host_cpu_info():
+    """What the host offers this process: nproc (the machine), the CPUs it may run on (affinity), the
+    cgroup CPU quota (the box's share), and lscpu's model name."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        info["affinity"] = info["nproc"]
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    info["cgroup_cpus"] = quota
+    model = None
+    try:
+        import subprocess
+        for line in subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout.splitlines():
+            if line.startswith("Model name"):
+                model = line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    info["model"] = model
+    usable = info["affinity"]
+    if quota:
+        usable = min(usable, max(1, int(quota)))
+    info["usable"] = usable
+    return info
+
+
+def cpu_baseline(budget_s=24.0, N=10):
+    """The reference CPU path (stock torch ops in MPCLoss's order, oracle/rollout_torch.py, with the
+    reference's requires_grad on the frozen LSTM) timed on the host: forward + backward + AdamW per step,
+    at B = 15 (the reference's training batch, UL/Main.py:84), B = 256 (BASELINE config 1 as written) and
+    B = 4 096 (stands in for config 2's B = 65 536: rollout-steps/s is per (trajectory, step), and the CPU
+    path is throughput-bound from a few thousand trajectories on), each on all usable host cores and on
+    one thread. The reported value is B = 256 at the faster of the two thread counts (torch's intra-op
+    threads do not pay at these small per-op sizes on a shared host)."""
     from oracle import rollout_torch as T
-    threads = threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
-    torch.set_num_threads(threads)
+    info = host_cpu_info()
     w = np.load(os.path.join(ROOT, "tests", "golden", "weights_ref.npz"))
     params = {"Wih": [w[f"Wih{k}"] for k in range(3)], "Whh": [w[f"Whh{k}"] for k in range(3)], "fcW": w["fcW"],
               "fcb": w["fcb"], "W_inp": w["W_inp"], "b_inp": w["b_inp"], "W_out": w["W_out"]}
     sim, ctrl = T.build_modules(params, torch.float32)
     opt = torch.optim.AdamW(ctrl.parameters(), lr=1e-4)
-    X, S = synth_batch(B, "cpu", 99)
+    runs = []
+    share = {15: 0.15, 256: 0.35, 4096: 0.5}
+    for B in (15, 256, 4096):
+        X, S = synth_batch(B, "cpu", 99)
 
-    def step():
-        opt.zero_grad()
+        def step():
+            opt.zero_grad()
+            u0 = ctrl(X)
+            loss, _ = T.mpc_loss(sim, ctrl, X, u0, S, N, ALPHA)
+            loss.backward()
+            opt.step()
+
+        for threads in (info["usable"], 1):
+            torch.set_num_threads(threads)
+            step()
+            t0 = time.perf_counter()
+            iters = 0
+            while iters < 1 or (time.perf_counter() - t0 < budget_s * share[B] / 2 and iters < 500):
+                step()
+                iters += 1
+            dt = time.perf_counter() - t0
+            runs.append({"batch": B, "threads": threads, "steps": iters, "seconds": round(dt, 3),
+                         "rollout_steps_per_s": B * N * iters / dt})
+    main_run = max((r for r in runs if r["batch"] == 256), key=lambda r: r["rollout_steps_per_s"])
+    return {"value": main_run["rollout_steps_per_s"], "unit": "rollout-steps/s", "cores": main_run["threads"],
+            "kind": "port",
+            "sample": f"oracle/rollout_torch.py fwd+bwd+AdamW (reference op order, LSTM weight grads on), N={N} "
+                      f"H=50; value = B=256 at the faster of {info['usable']} threads and 1 thread; B=4096 stands in "
+                      f"for B=65536 (per rollout-step rate); torch {torch.__version__}",
+            "runs": runs, "host": info}
+
+
+# v_mfma_f32_16x16x32_f16 issued per 16-trajectory wave and LSTM cell (layer 0, layers >= 1) in the fp32-accurate
+# H <= 52 kernels at HS = 13 (DESIGN.md §2 "Packed tail block"; cross-checked against SQ_INSTS_VALU_MFMA_F16 in
+# profiles/round2_pmc.json): the forward's three split products, the backward's recompute + transposed products
+MFMA_PER_WAVE_CELL = {"fwd": (78, 130), "bwd": (158, 270)}
+MFMA_FLOP = 16 * 16 * 32 * 2
+
+
+def executed_mfma_flop(kind, B, N, L=10):
+    """f16 MFMA FLOP one launch of the fp32-accurate H = 50 kernel executes (padding and recompute included)."""
+    waves = (B + 15) // 16
+    l0, l12 = MFMA_PER_WAVE_CELL[kind]
+    return waves * N * L * (l0 + 2 * l12) * MFMA_FLOP
+
+
+def grad_check(sim, ctrl, X, S, N, dev, precision, B_check=None):
+    """grad fp32 max-rel-err vs the PyTorch restatement (BASELINE.json's metric): the HIP MPCLoss forward +
+    backward on the benchmarked batch (u0 = controller(X) as a leaf, as the parity tests take it) against
+    oracle/rollout_torch.py in fp64 on the same device, chunked over trajectories. Per tensor
+    max|g - g_ref| / max|g_ref|; run after the timed region, as the checker only."""
+    from oracle import rollout_torch as T
+    if B_check is not None and B_check < X.shape[0]:
+        X, S = X[:B_check].contiguous(), S[:B_check].contiguous()
+    B = X.shape[0]
+    with torch.no_grad():
         u0 = ctrl(X)
-        loss, _ = T.mpc_loss(sim, ctrl, X, u0, S, N, ALPHA)
-        loss.backward()
-        opt.step()
-        return loss.item()
-
-    step()
-    t0 = time.perf_counter()
-    iters = 0
-    while time.perf_counter() - t0 < budget_s and iters < 200:
-        step()
-        iters += 1
-    dt = time.perf_counter() - t0
-    return {"value": B * N * iters / dt, "unit": "rollout-steps/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/rollout_torch.py fwd+bwd+AdamW, B={B} N={N} H=50, {iters} steps in {dt:.1f}s, "
-                      f"torch {torch.__version__}, {threads} threads"}
+    u = u0.detach().clone().requires_grad_(True)
+    fn = fca.MPCLoss(prediction_horizon=N, alpha=ALPHA, precision=precision)
+    for p in ctrl.parameters():
+        p.grad = None
+    loss, f = fn(sim, ctrl, X, u, S, dev)
+    loss.backward()
+    got = {"loss": f["loss"], "prediction": f["prediction"], "xhat": fn.last_trajectory, "g_u0": u.grad.reshape(-1),
+           "g_W_inp": ctrl.fc_inp.weight.grad, "g_b_inp": ctrl.fc_inp.bias.grad, "g_W_out": ctrl.fc_out.weight.grad}
+    cpu = lambda t: t.detach().double().cpu().numpy()
+    params = {"Wih": [cpu(getattr(sim.lstm, f"weight_ih_l{k}")) for k in range(3)],
+              "Whh": [cpu(getattr(sim.lstm, f"weight_hh_l{k}")) for k in range(3)],
+              "fcW": cpu(sim.fc.weight), "fcb": cpu(sim.fc.bias), "W_inp": cpu(ctrl.fc_inp.weight),
+              "b_inp": cpu(ctrl.fc_inp.bias), "W_out": cpu(ctrl.fc_out.weight)}
+    H = params["Whh"][0].shape[1]
+    ref = T.loss_and_grads_chunked(params, X, u.detach(), S, N, ALPHA, device=dev,
+                                   chunk=16384 if H <= 64 else 2048)
+    # per-trajectory tensors are compared outside the kink band (trajectories whose fp64 rollout passes within
+    # 1e-5 of a ReLU/Hardtanh/constraint kink, where an fp32 mask may flip: tests/test_gpu_fullsize.py); the
+    # parameter gradients are the full-batch sums, flips included
+    reg = T.kink_margin(params, X.double(), ref["xhat"].reshape(B, N, 4)) > 1e-5
+    got["prediction"] = got["prediction"].reshape(B, N)
+    err = {}
+    for k, v in got.items():
+        r = ref[k].reshape(v.shape)
+        a = v.double()
+        if k in ("loss", "prediction", "xhat", "g_u0"):
+            a, r = a[reg], r[reg]
+        err[k] = float((a - r).abs().max() / r.abs().max().clamp_min(1e-300))
+    for p in ctrl.parameters():
+        p.grad = None
+    grads = ("g_u0", "g_W_inp", "g_b_inp", "g_W_out")
+    return {"grad_max_rel_err": max(err[k] for k in grads),
+            "out_max_rel_err": max(err[k] for k in ("loss", "prediction", "xhat")),
+            "per_tensor": err, "batch": B, "kink_band_trajectories": int((~reg).sum()),
+            "oracle": "oracle/rollout_torch.py fp64 on the GPU, chunked over trajectories (checker only)"}
 
 
 def main():
@@ -140,19 +248,26 @@ def main():
     ap.add_argument("--batch", type=int, default=65536, help="trajectories per GPU")
     ap.add_argument("--horizon", type=int, default=10)
     ap.add_argument("--hidden", type=int, default=50)
-    ap.add_argument("--cpu-budget", type=float, default=15.0)
+    ap.add_argument("--cpu-budget", type=float, default=24.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--precision", choices=("fp32", "f16"), default="fp32",
-                    help="fp32: reference-accurate (default, config 2); f16: config 3's reduced-precision mode")
+    ap.add_argument("--grad-check", choices=("full", "off"), default="full",
+                    help="full: grad max-rel-err of the benchmarked batch vs the fp64 torch restatement (after timing)")
+    ap.add_argument("--precision", choices=("fp32", "f16", "f16fwd"), default="fp32",
+                    help="fp32: reference-accurate (default, config 2); f16: gate products in f16 in both passes; "
+                         "f16fwd: f16 forward, fp32-accurate backward (config 3)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # --gpus N without a launcher: start N ranks (torchrun) as a child BEFORE anything touches the GPU
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(fca.launch.spawn_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
+    rank, local, world = fca.launch.rank_env()
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)            # before the process group: RCCL binds each rank to its own GPU
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        world = dist.get_world_size()
     B, N, H = args.batch, args.horizon, args.hidden
 
     sim, ctrl = load_weights(dev, H)
@@ -162,12 +277,20 @@ def main():
     loss_fn = fca.MPCLoss(prediction_horizon=N, alpha=ALPHA, precision=args.precision)
     sync = fca.distributed.GradAllReduce() if world > 1 else None
     X, S = synth_batch(B, dev, 1000 + rank)
+    stream = torch.cuda.current_stream(dev)      # the stream the C ABI launches on
+    marks = []
 
-    def step():
+    def step(ev=None):
         opt.zero_grad()
         out = ctrl(X)
+        if ev is not None:
+            ev[0].record(stream)
         loss, feats = loss_fn(sim, ctrl, X, out, S, dev)
+        if ev is not None:
+            ev[1].record(stream)
         loss.backward()
+        if ev is not None:
+            ev[2].record(stream)
         if sync is not None:
             sync(ctrl, B, B * world, loss)
         opt.step()
@@ -177,30 +300,15 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    # per-kernel timing with events on the stream the kernels launch on (torch's current stream)
-    fl = flops_per_rollout_step(H)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    fwd_ms, bwd_ms = [], []
-    for _ in range(3):
-        opt.zero_grad()
-        out = ctrl(X)
-        ev[0].record()
-        loss, _ = loss_fn(sim, ctrl, X, out, S, dev)
-        ev[1].record()
-        ev[2].record()
-        loss.backward()
-        ev[3].record()
-        torch.cuda.synchronize()
-        fwd_ms.append(ev[0].elapsed_time(ev[1]))
-        bwd_ms.append(ev[2].elapsed_time(ev[3]))
-    opt.zero_grad()
-
+    # timed region: K steps; HIP events on the launching stream bracket the fused forward and backward of
+    # EVERY timed step (the per-kernel times come from the same steps as ms_per_step)
+    marks = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loss = step()
+    for k in range(args.steps):
+        loss = step(marks[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -211,37 +319,66 @@ def main():
         dt = float(t.item())
     ms = 1000.0 * dt / args.steps
     value = world * B * N / (dt / args.steps)
+    fwd_ms = [e[0].elapsed_time(e[1]) for e in marks]
+    bwd_ms = [e[1].elapsed_time(e[2]) for e in marks]
 
     if rank == 0:
-        f_ms, b_ms = float(np.median(fwd_ms)), float(np.median(bwd_ms))
+        f_ms, b_ms = float(np.mean(fwd_ms)), float(np.mean(bwd_ms))
+        fl = flops_per_rollout_step(H)
         dom = ("bwd", b_ms) if b_ms >= f_ms else ("fwd", f_ms)
+        narrow = H <= 52
+        kernel = f"fcr_{dom[0]}_kernel" if narrow else "wide path (split-f16 GEMMs + cell kernels)"
         achieved = B * N * fl[dom[0]] / (dom[1] * 1e-3) / 1e12
         hbm_roof = HBM_PEAK_GBS * 1e9 / hbm_bytes_per_rollout_step(N)
         default_cfg = (B, N, H, args.precision) == (65536, 10, 50, "fp32")
         traffic, traffic_src = pmc_traffic(f"fcr_{dom[0]}_kernel") if default_cfg else (None, None)
-        peak = FP32_PEAK_TFLOPS if args.precision == "fp32" else F16_PEAK_TFLOPS
+        # ceiling of the arithmetic as executed: an fp32-accurate product is three f16 MFMA products
+        # (hi.hi + hi.lo + lo.hi, fcr_f16.h), so the fp32-equivalent ceiling is the f16 peak / 3;
+        # in the reduced-precision pass one f16 product each
+        f16_pass = args.precision == "f16" or (args.precision == "f16fwd" and dom[0] == "fwd")
+        peak = F16_PEAK_TFLOPS if f16_pass else F16_PEAK_TFLOPS / 3
+        roof = {"bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                "frac": achieved / peak, "traffic": traffic, "traffic_unit": "bytes/launch",
+                "traffic_source": traffic_src,
+                "achieved_def": f"algorithmic {fl[dom[0]]} FLOP per rollout-step x B*N / mean HIP-event time of the "
+                                f"{dom[0]} pass over the timed steps",
+                "peak_def": ("f16 dense MFMA peak (one f16 product per algorithmic product)" if f16_pass else
+                             "f16 dense MFMA peak / 3: the ceiling of fp32-accurate products built from three f16 "
+                             "MFMA products"),
+                "fp32_peak_frac": achieved / FP32_PEAK_TFLOPS}
+        if narrow and args.precision == "fp32":
+            ex = executed_mfma_flop(dom[0], B, N) / (dom[1] * 1e-3) / 1e12
+            roof["executed"] = {"instr": "v_mfma_f32_16x16x32_f16", "achieved": ex, "peak": F16_PEAK_TFLOPS,
+                                "unit": "TFLOP/s", "frac": ex / F16_PEAK_TFLOPS,
+                                "def": "MFMA FLOP issued (split products, padding, backward recompute) / time"}
+        prec_label = {"fp32": "fp32", "f16": "f16 fwd+bwd", "f16fwd": "f16 fwd / fp32-accurate bwd"}[args.precision]
         line = {
             "metric": "rollout-steps/s (batch x horizon), fwd+bwd+AdamW step",
             "value": value, "unit": "rollout-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f32" if args.precision == "fp32" else "f16", "data": "synthetic (SURVEY §8d distribution); reference-trained LSTM/controller weights",
+            "dtype": {"fp32": "f32", "f16": "f16", "f16fwd": "f16fwd/f32bwd"}[args.precision],
+            "data": "synthetic (SURVEY §8d distribution); reference-trained LSTM/controller weights",
             "config": {"workload": f"unsupervised-MPC rollout train step, B={B}/GPU, N={N}, H={H}, 3-layer LSTM, "
-                                   f"ctrl 3-50-1, {args.precision}", "batch_per_gpu": B, "global_batch": B * world, "horizon": N,
-                       "hidden": H, "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": f"fcr_{dom[0]}_kernel", "achieved": achieved,
-                         "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
-                         "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src},
-            "kernels_ms": {"fwd": f_ms, "bwd": b_ms},
+                                   f"ctrl 3-50-1, {prec_label}", "batch_per_gpu": B, "global_batch": B * world,
+                       "horizon": N, "hidden": H, "parallelism": f"dp{world}", "world_size": world},
+            "roofline": roof,
+            "kernels_ms": {"fwd": f_ms, "bwd": b_ms, "source": "HIP events on the launching stream, every timed step"},
             # the design's own HBM traffic (activation records and hand-off slabs, PMC-measured) against
             # 8 TB/s: how close the dominant kernel runs to the bandwidth its data movement needs
             "hbm_traffic_frac": (traffic / (dom[1] * 1e-3) / (HBM_PEAK_GBS * 1e9)) if traffic else None,
             "hbm_roofline_frac": value / world / hbm_roof,
             "loss": float(loss.item()),
         }
+        if args.grad_check != "off":
+            gc = grad_check(sim, ctrl, X, S, N, dev, args.precision)
+            line["grad_max_rel_err"] = gc.pop("grad_max_rel_err")
+            line["out_max_rel_err"] = gc.pop("out_max_rel_err")
+            line["grad_check"] = gc
         if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_budget)
+            line["cpu_baseline"] = cpu_baseline(args.cpu_budget, N=10)
         print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -4,7 +4,7 @@ Drop-in for the hot path of marcowus/forging-control: ``MPCLoss`` (the batched c
 the FNN controller through the 3-layer LSTM plant surrogate, Functions.py:1336-1472) and its
 backward, as hand-written HIP kernels behind the C ABI in include/fcr.h.
 """
-from . import _native, closed_loop, data, distributed, graphed, inference, plant, rollout, surrogate
+from . import _native, closed_loop, data, distributed, graphed, inference, launch, plant, rollout, surrogate
 from .functions import FNNModel, LSTMModel, MPCLoss, NeuralNetwork
 from .inference import controller_step, simulate_step, simulator_make_step
 from .plant import ForgingRK4, forging_rk4
@@ -15,4 +15,4 @@ from .graphed import CapturedStep
 __all__ = ["FNNModel", "LSTMModel", "MPCLoss", "NeuralNetwork", "rollout", "distributed", "inference",
            "simulate_step", "controller_step", "simulator_make_step", "plant", "ForgingRK4", "forging_rk4",
            "data", "SequenceWindows", "DeviceLoader", "surrogate", "closed_loop", "ClosedLoop", "graphed",
-           "CapturedStep", "_native"]
+           "CapturedStep", "launch", "_native"]

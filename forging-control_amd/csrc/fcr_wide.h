@@ -402,12 +402,13 @@ __global__ void wide_rowg_kernel(const float *__restrict__ E, int ldE, const flo
 // consts[0] = dloss * 2^-k on load (no host sync for dloss). consts = [1/scale, 0, 1, scale].
 __global__ void wide_bscale_kernel(const float *__restrict__ dloss, int k, float *consts) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    // dloss = 0: every gradient is 0 (no 0 * inf). A non-finite dloss must come out non-finite (as torch's
+    // would, for GradScaler / anomaly detection): the NaN scale turns every dgate operand into NaN.
     const float d = dloss[0];
-    const bool ok = d != 0.0f && isfinite(d);
-    consts[0] = ok ? ldexpf(d, -k) : 0.0f;
+    consts[0] = d != 0.0f ? ldexpf(d, -k) : 0.0f;
     consts[1] = 0.0f;
     consts[2] = 1.0f;
-    consts[3] = ok ? ldexpf(1.0f, k) / d : 0.0f;
+    consts[3] = !isfinite(d) ? __builtin_nanf("") : d != 0.0f ? ldexpf(1.0f, k) / d : 0.0f;
 }
 
 // d loss / d u0 (Functions.py:1396 row 9 col 4, and the command costs cmd_0, cmd_1)

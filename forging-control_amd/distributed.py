@@ -2,12 +2,14 @@
 
 The rollout shards trivially by trajectory (no cross-sample op before the batch mean,
 Functions.py:1387-1463). Each rank runs the fused forward/backward on its B_local trajectories; the
-only exchange is ONE all-reduce of the packed controller gradients (250 floats) plus the loss (one
-float) per optimizer step — about 1 KB, latency-bound, so it is a single flat bucket, not a
-bandwidth-tuned ring schedule. AdamW then runs identically on every rank (same reduced gradients,
-same deterministic update), so no parameter broadcast is needed after the first sync.
+only exchange is ONE all-reduce of the packed controller gradients (250 floats) plus the loss and the
+shard size (two floats) per optimizer step — about 1 KB, latency-bound, so it is a single flat bucket,
+not a bandwidth-tuned ring schedule. AdamW then runs identically on every rank (same reduced
+gradients, same deterministic update), so no parameter broadcast is needed after the first sync.
 """
 from __future__ import annotations
+
+import warnings
 
 import torch
 import torch.distributed as dist
@@ -27,15 +29,23 @@ def broadcast_params(module: torch.nn.Module, src: int = 0, group=None) -> None:
 
 
 class GradAllReduce:
-    """Callable grad hook for NeuralNetwork.train_model(grad_sync=...).
+    """Callable grad hook for ``NeuralNetwork.train_model(grad_sync=...)``.
 
     Each rank's loss is the mean over its B_local trajectories; the global loss is the mean over
-    B_global = sum(B_local). So each rank scales its gradient by B_local / B_global before the SUM
-    all-reduce, which makes the reduced gradient exactly d(global mean)/d(theta).
+    B_global = sum(B_local), so the global-mean gradient is sum_r (B_r / B_global) g_r.
+
+    * ``hook(module, b_local, b_global)``: each rank scales by b_local / b_global before the SUM.
+    * ``hook(module, b_local)`` (what ``train_model`` passes: the batch it just ran): b_local rides in the
+      same buffer — [b_r g_r, b_r loss_r, b_r] is summed and divided by the summed b_r afterwards — so
+      uneven shards and short last batches still give the global-mean gradient with ONE all-reduce.
+    * ``hook(module)``: equal shards are assumed (1/world), with a one-time warning.
+
+    Returns the global-mean loss when ``loss`` is given, else None.
     """
 
     def __init__(self, group=None):
         self.group = group
+        self._warned = False
 
     def __call__(self, module: torch.nn.Module, b_local: int | None = None, b_global: int | None = None,
                  loss: torch.Tensor | None = None):
@@ -43,11 +53,23 @@ class GradAllReduce:
         if not params:
             return loss
         world = dist.get_world_size(self.group)
-        scale = (b_local / b_global) if (b_local is not None and b_global) else 1.0 / world
-        flat = torch.cat([p.grad.reshape(-1) for p in params]
-                         + ([loss.detach().reshape(1)] if loss is not None else []))
-        flat.mul_(scale)
+        count = b_local is not None and not b_global
+        if b_local is None and not self._warned:
+            warnings.warn("GradAllReduce called without the shard size: assuming equal shards (1/world)")
+            self._warned = True
+        pieces = [p.grad.reshape(-1) for p in params]
+        if loss is not None:
+            pieces.append(loss.detach().reshape(1).to(pieces[0].dtype))
+        if count:
+            pieces.append(pieces[0].new_ones(1))
+        flat = torch.cat(pieces)
+        if count:
+            flat.mul_(float(b_local))
+        else:
+            flat.mul_((b_local / b_global) if b_local is not None else 1.0 / world)
         dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+        if count:
+            flat = flat[:-1] / flat[-1]
         off = 0
         for p in params:
             n = p.grad.numel()

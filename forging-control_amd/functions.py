@@ -71,10 +71,17 @@ class LSTMModel(nn.Module):
                 torch.zeros(shape, device=device).requires_grad_())
 
     def forward(self, x: torch.Tensor, device: torch.device):
-        """fc(h_9 of the top layer) from a zero state (Functions.py:353-379), on the gfx950 path
-        (forging-control_amd/surrogate.py: fcr_lstm_forward, and fcr_lstm_backward under autograd)."""
-        from .surrogate import lstm_apply
-        return lstm_apply(self, x)
+        """fc(h_9 of the top layer) from a zero state (Functions.py:353-379). The reference's shape —
+        LSTM(5, H, 3) without bias on (B, 10, 5) windows, on a ROCm device — runs the gfx950 path
+        (surrogate.py: fcr_lstm_forward, and fcr_lstm_backward under autograd). Anything else — above all
+        the closed-loop harness's ``model(X_new, "cpu")`` on a model moved to the CPU (Functions.py:999,
+        UL/Main.py:347-348) — is this module's own ``nn.LSTM`` + ``fc``, exactly the reference's forward."""
+        from .surrogate import hip_shape_ok, lstm_apply
+        if hip_shape_ok(self, x):
+            return lstm_apply(self, x)
+        h0, c0 = self.initialize_hidden_states(x.shape[0], x.device)
+        out, _ = self.lstm(x, (h0.detach(), c0.detach()))
+        return self.fc(out[:, -1, :])
 
 
 def _controller_params(controller):
@@ -114,7 +121,7 @@ class MPCLoss(nn.Module):
         super().__init__()
         self.N = prediction_horizon
         self.alpha = alpha
-        self.precision = precision     # "fp32" (reference-accurate) or "f16" (config 3, include/fcr.h)
+        self.precision = precision     # "fp32" (reference-accurate), "f16fwd" (config 3) or "f16" (include/fcr.h)
         self.activation = nn.ReLU()
         self.last_trajectory = None
 
@@ -153,14 +160,15 @@ class NeuralNetwork:
             loss.backward()
             return (loss.detach(), f["loss"], f["command"], f["error"], f["prediction"])
 
-        sync = (lambda: grad_sync(model)) if grad_sync is not None else None
+        sync = (lambda X, z: grad_sync(model, X.shape[0])) if grad_sync is not None else None
         return CapturedStep(model.parameters(), optimizer, body, sync, warmup)
 
     @staticmethod
     def train_model(data_loader, simulator, model, loss_function, optimizer, device, enable_noise=False,
                     grad_sync=None, step=None):
-        """One epoch (Functions.py:594-676). ``grad_sync`` (optional) is called between backward and the
-        optimizer step — the data-parallel hook (see :mod:`.distributed`). ``step`` (optional, from
+        """One epoch (Functions.py:594-676). ``grad_sync`` (optional) is called as ``grad_sync(model, B_local)``
+        between backward and the optimizer step — the data-parallel hook (:class:`.distributed.GradAllReduce`
+        weights each rank's gradient by its batch size, so uneven shards give the global-mean gradient). ``step`` (optional, from
         :meth:`captured_step`) replays each batch's step from a HIP graph; the epoch's loss is then summed
         on the device and read once, not per batch."""
         model.train()
@@ -178,7 +186,7 @@ class NeuralNetwork:
                 feats[k].append(f[k])
             loss.backward()
             if grad_sync is not None:
-                grad_sync(model)
+                grad_sync(model, X.shape[0])   # this rank's batch: the hook weights it into the global mean
             optimizer.step()
             total += loss.item()
             n_batches += 1
@@ -212,7 +220,27 @@ class NeuralNetwork:
                 X, y = X.to(device), y.to(device)
                 total += loss_function(model(X), y).item()
                 n += 1
-        return total / max(n, 1)
+        return total / n if n else 0.0
+
+    @staticmethod
+    def predict(data_loader, model):
+        """Controller predictions over a loader (Functions.py:720-748): ``model(X)`` per batch, evaluation
+        mode, no gradients, concatenated along the batch. The batches go to the device the model lives on
+        (the reference leaves that to the loader); on a ROCm device that is the HIP controller kernel."""
+        model.eval()
+        dev = next(model.parameters()).device
+        preds = []
+        with torch.no_grad():
+            for X, _, _ in data_loader:
+                preds.append(model(X.to(dev)))
+        return torch.cat(preds, dim=0)
+
+    @staticmethod
+    def simulator_make_step(X, model, scalers, noise):
+        """Functions.py:969-1011: the surrogate's unscaled one-step prediction for the closed-loop harness
+        (see :func:`.inference.simulator_make_step`; runs where the model is)."""
+        from .inference import simulator_make_step
+        return simulator_make_step(X, model, scalers, noise)
 
     @staticmethod
     def train_loop(controller, simulator, train_loader, val_loader, loss_function, optimizer, n_epochs,

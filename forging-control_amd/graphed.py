@@ -38,7 +38,7 @@ def _make_capturable(optimizer: torch.optim.Optimizer) -> None:
 
 
 class CapturedStep:
-    """``step(*batch)`` = zero_grad -> ``body(*batch)`` -> [``grad_sync()``] -> ``optimizer.step()``.
+    """``step(*batch)`` = zero_grad -> ``body(*batch)`` -> [``grad_sync(*batch)``] -> ``optimizer.step()``.
 
     ``body`` runs the forward AND calls ``backward()`` itself; it returns a tuple of tensors (loss and
     whatever else the caller keeps). The first ``warmup`` calls run eagerly on a side stream (they are
@@ -48,7 +48,7 @@ class CapturedStep:
     """
 
     def __init__(self, params: Sequence[torch.Tensor], optimizer: torch.optim.Optimizer,
-                 body: Callable[..., tuple], grad_sync: Callable[[], None] | None = None, warmup: int = 2):
+                 body: Callable[..., tuple], grad_sync: Callable[..., None] | None = None, warmup: int = 2):
         self.params = list(params)
         self.optimizer = optimizer
         self.body = body
@@ -68,7 +68,7 @@ class CapturedStep:
         self.optimizer.zero_grad(set_to_none=True)
         out = self.body(*batch)
         if self.grad_sync is not None:
-            self.grad_sync()
+            self.grad_sync(*batch)
         self.optimizer.step()
         self.eager_steps += 1
         return out
@@ -99,7 +99,7 @@ class CapturedStep:
             p.grad = gr
         self._g_fb.replay()
         if self.grad_sync is not None:
-            self.grad_sync()
+            self.grad_sync(*batch)
             self._g_opt.replay()
         self.replays += 1
         return self._out

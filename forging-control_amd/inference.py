@@ -38,15 +38,26 @@ def controller_step(controller, X: torch.Tensor) -> torch.Tensor:
         return controller(X)
 
 
-def simulator_make_step(X: np.ndarray, model, scalers: dict, noise: np.ndarray, device="cuda") -> np.ndarray:
+def simulator_make_step(X: np.ndarray, model, scalers: dict, noise: np.ndarray, device=None) -> np.ndarray:
     """Drop-in for ``NeuralNetwork.simulator_make_step`` (Functions.py:969-1011) with the same arguments:
-    X (B, 10, 5) scaled LSTM inputs, noise (4,) or (B, 4) in scaled units; returns the unscaled
-    prediction ``scalers['output'].inverse_transform(model(X) + noise)``, computed on the GPU for the
-    whole batch."""
+    X (B, 10, 5) or (10, 5) scaled LSTM inputs, noise (4,) or (B, 4) in scaled units; returns the unscaled
+    prediction ``scalers['output'].inverse_transform(model(X) + noise)``.
+
+    ``device`` defaults to where the model's weights are. A model on a ROCm device runs the whole batch
+    through the fused gfx950 forward; a model the harness moved to the CPU (UL/Main.py:347-348) runs
+    ``model(X_new, "cpu")`` exactly as the reference does — its own ``nn.LSTM`` (LSTMModel.forward)."""
+    if device is None:
+        device = next(model.parameters()).device
+    device = torch.device(device)
     Xt = torch.as_tensor(np.asarray(X, np.float32), device=device)
     if Xt.dim() == 2:
         Xt = Xt.unsqueeze(0)
     nz = torch.as_tensor(np.broadcast_to(np.asarray(noise, np.float32), (Xt.shape[0], 4)).copy(), device=device)
+    if device.type == "cpu":
+        model.eval()
+        with torch.no_grad():
+            y = (model(Xt, "cpu") + nz).numpy()
+        return scalers["output"].inverse_transform(y)
     y = simulate_step(model, Xt, nz).cpu().numpy().astype(np.float64)
     return scalers["output"].inverse_transform(y)
 

@@ -99,13 +99,14 @@ class RolloutFn(torch.autograd.Function):
         return (None, g_u0, None, None, g_wi, g_bi, g_wo) + (None,) * 11
 
 
-PRECISIONS = {"fp32": _native.PRECISION_FP32, "f16": _native.PRECISION_F16}
+PRECISIONS = {"fp32": _native.PRECISION_FP32, "f16": _native.PRECISION_F16, "f16fwd": _native.PRECISION_F16_FWD}
 
 
 def rollout(X, u0, states, ctrl_params, lstm_params, N, alpha, noise=None, precision="fp32"):
     """Functional entry: ctrl_params = (W_inp, b_inp, W_out), lstm_params = (w_ih[3], w_hh[3], fc_w, fc_b).
-    precision: "fp32" (fp32-accurate, the default) or "f16" (config 3's reduced-precision gate products,
-    include/fcr.h FCR_PRECISION_F16)."""
+    precision: "fp32" (fp32-accurate, the default), "f16fwd" (config 3: f16 gate products in the forward,
+    fp32-accurate backward, include/fcr.h FCR_PRECISION_F16_FWD) or "f16" (f16 gate products in both passes,
+    FCR_PRECISION_F16)."""
     if precision not in PRECISIONS:
         raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {precision!r}")
     w_ih, w_hh, fc_w, fc_b = lstm_params

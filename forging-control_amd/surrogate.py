@@ -74,17 +74,22 @@ class LSTMFunction(torch.autograd.Function):
         return tuple(gi if need else None for gi, need in zip(g, ctx.needs_input_grad))
 
 
-def lstm_apply(model, x: torch.Tensor) -> torch.Tensor:
-    """LSTMModel forward on the HIP path (x (B, 10, 5) on a ROCm device)."""
+def hip_shape_ok(model, x) -> bool:
+    """True when ``model(x)`` is the shape the gfx950 LSTM path is built for: LSTM(5, H, 3) without LSTM
+    bias -> Linear(H, 4), fp32 (B, 10, 5) windows on the device the weights live on."""
     lstm = model.lstm
-    if x.device.type != "cuda":
-        raise RuntimeError(f"LSTMModel runs on a ROCm device only (got {x.device}); move the model and the "
-                           "windows to the GPU — there is no CPU path")
-    if lstm.bias or lstm.num_layers != 3 or lstm.input_size != 5 or model.fc.out_features != 4:
-        raise RuntimeError("the gfx950 LSTM path is built for LSTMModel(5, H, 4, 3) without LSTM bias "
-                           "(Model_NN/Main.py:225, UL/Main.py:144-154)")
-    if x.dim() != 3 or x.shape[1:] != (WINDOW_ROWS, 5):
-        raise ValueError(f"x must be (B, 10, 5), got {tuple(x.shape)}")
+    return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 3 and tuple(x.shape[1:]) == (WINDOW_ROWS, 5)
+            and not lstm.bias and lstm.num_layers == 3 and lstm.input_size == 5 and model.fc.out_features == 4
+            and lstm.batch_first and all(p.dtype == torch.float32 and p.device == x.device for p in model.parameters()))
+
+
+def lstm_apply(model, x: torch.Tensor) -> torch.Tensor:
+    """LSTMModel forward on the HIP path (x (B, 10, 5) on a ROCm device); :func:`hip_shape_ok` must hold."""
+    if not hip_shape_ok(model, x):
+        raise RuntimeError("the gfx950 LSTM path is built for LSTMModel(5, H, 4, 3) without LSTM bias on fp32 "
+                           f"(B, 10, 5) device windows (Model_NN/Main.py:225, UL/Main.py:144-154); got {tuple(x.shape)} "
+                           f"on {x.device}")
+    lstm = model.lstm
     p = [getattr(lstm, f"weight_ih_l{k}") for k in range(3)] + [getattr(lstm, f"weight_hh_l{k}") for k in range(3)]
     return LSTMFunction.apply(x, *p, model.fc.weight, model.fc.bias)
 

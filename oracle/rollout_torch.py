@@ -137,3 +137,66 @@ def loss_and_grads(params, X, u0, states, N, alpha, noise=None, dtype=torch.floa
     out["g_b_inp"] = g(ctrl.fc_inp.bias)
     out["g_W_out"] = g(ctrl.fc_out.weight)
     return out
+
+
+def loss_and_grads_chunked(params, X, u0, states, N, alpha, noise=None, device="cpu", dtype=torch.float64,
+                           chunk=16384):
+    """:func:`loss_and_grads` for a large batch, evaluated chunk by chunk (on ``device``, e.g. the GPU in
+    fp64: stock torch ops, the checker for full-size batches).
+
+    Trajectories are independent until the batch mean (Functions.py:1463), so each chunk's loss is weighted
+    by b_chunk / B and the parameter gradients summed over chunks are the full-batch gradients; per-
+    trajectory outputs and g_u0 are concatenated. Inputs are arrays or tensors (any device); returns
+    tensors on ``device`` in ``dtype``: loss (0-d), loss/command/error (B,), prediction (B*N,), xhat
+    (B,N,4), g_u0 (B,), g_W_inp, g_b_inp, g_W_out.
+    """
+    sim, ctrl = build_modules(params, dtype, lstm_requires_grad=False)
+    sim, ctrl = sim.to(device), ctrl.to(device)
+    t = lambda a: torch.as_tensor(a).to(device=device, dtype=dtype)
+    X, u0, states = t(X), t(u0).reshape(-1, 1), t(states)
+    noise = None if noise is None else t(noise)
+    B = X.shape[0]
+    outs = {k: [] for k in ("loss", "command", "error", "prediction", "xhat", "g_u0")}
+    total = torch.zeros((), dtype=dtype, device=device)
+    for lo in range(0, B, chunk):
+        hi = min(B, lo + chunk)
+        u = u0[lo:hi].clone().requires_grad_(True)
+        loss, f = mpc_loss(sim, ctrl, X[lo:hi], u, states[lo:hi], N, alpha, None if noise is None else noise[lo:hi])
+        (loss * ((hi - lo) / B)).backward()
+        total += loss.detach() * ((hi - lo) / B)
+        for k in ("loss", "command", "error", "prediction", "xhat"):
+            outs[k].append(f[k].detach())
+        outs["g_u0"].append(u.grad.reshape(-1))
+    out = {k: torch.cat(v) for k, v in outs.items()}
+    out["loss_scalar"] = total
+    g = lambda p: (p.grad if p.grad is not None else torch.zeros_like(p)).detach()
+    out["g_W_inp"], out["g_b_inp"], out["g_W_out"] = g(ctrl.fc_inp.weight), g(ctrl.fc_inp.bias), g(ctrl.fc_out.weight)
+    return out
+
+
+def kink_margin(params, X, xhat):
+    """Per-trajectory distance of the rollout's controller evaluations to the kinks of its piecewise-linear
+    activations: min over horizon steps j >= 1 and hidden units of |z| (ReLU, Functions.py:276) and of
+    |1 - |v|| (Hardtanh, :287), for the controller inputs [x̂_j[0], x̂_j[3], ref] of the fp64 trajectory
+    ``xhat`` (B,N,4), and of the pressure predictions to the constraint ReLUs' kinks (0, P1_MAX, P2_MAX,
+    :1411). Where an fp32 evaluation lands within its own rounding of a kink, its mask (and the
+    gradient's slope there) can flip against fp64's: those trajectories' per-trajectory gradients differ by
+    O(1) of one term, independent of the implementation's accuracy. Returns a (B,) fp64 tensor.
+    """
+    X = torch.as_tensor(X)
+    xhat = torch.as_tensor(xhat).to(device=X.device, dtype=torch.float64)
+    Wi = torch.as_tensor(params["W_inp"], dtype=torch.float64, device=X.device)
+    bi = torch.as_tensor(params["b_inp"], dtype=torch.float64, device=X.device)
+    Wo = torch.as_tensor(params["W_out"], dtype=torch.float64, device=X.device)
+    B, N = xhat.shape[0], xhat.shape[1]
+    # pressure-constraint ReLUs on every prediction (Functions.py:1411, 1449)
+    p = xhat[..., 1:3]
+    con = torch.minimum(p.abs(), (p - torch.tensor([P1_MAX, P2_MAX], dtype=torch.float64, device=X.device)).abs())
+    con = con.amin(dim=(1, 2))
+    if N < 2:
+        return con
+    ref = X[:, 2].to(torch.float64)
+    cin = torch.stack((xhat[:, :-1, 0], xhat[:, :-1, 3], ref[:, None].expand(B, N - 1)), dim=-1)   # (B,N-1,3)
+    z = cin @ Wi.T + bi
+    v = torch.relu(z) @ Wo[0]
+    return torch.minimum(con, torch.minimum(z.abs().amin(dim=(1, 2)), (1 - v.abs()).abs().amin(dim=1)))

@@ -1,0 +1,87 @@
+"""World-size-N data-parallel training through the package's launcher (test helper, CPU / gloo).
+
+``python tests/dp_train_worker.py --ranks N --out DIR`` re-launches itself as N ranks with
+``forging_control_amd.launch.spawn_ranks`` — the launcher ``bench.py --gpus N`` uses — and each rank runs
+the real ``NeuralNetwork.train_model(..., grad_sync=GradAllReduce())`` over its contiguous shard of every
+global batch (the reference's B = 15, so shards are uneven: 8 / 7, and the last batch of 7 splits 4 / 3).
+The loss is a CPU stand-in with MPCLoss's call signature: the stock-torch restatement of the rollout
+(oracle/rollout_torch.py) on the reference's trained surrogate — the GPU kernels are not needed to test
+the data-parallel plumbing. Every rank writes its final controller parameters and epoch losses to DIR.
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import forging_control_amd as fca  # noqa: E402
+from oracle import rollout_torch as T  # noqa: E402
+
+N_HORIZON, ALPHA = 3, 20.0
+BATCHES = [15, 15, 7]
+
+
+class StandInMPCLoss(torch.nn.Module):
+    """MPCLoss's call surface (Functions.py:1353) over the CPU restatement of its arithmetic."""
+
+    def forward(self, simulator, controller, input_controller, output_controller, states, device, enable_noise=False):
+        loss, f = T.mpc_loss(simulator, controller, input_controller, output_controller, states, N_HORIZON, ALPHA)
+        return loss, {k: f[k].detach() for k in ("loss", "command", "error", "prediction")}
+
+
+def surrogate():
+    w = np.load(os.path.join(ROOT, "tests", "golden", "weights_ref.npz"))
+    params = {"Wih": [w[f"Wih{k}"] for k in range(3)], "Whh": [w[f"Whh{k}"] for k in range(3)], "fcW": w["fcW"],
+              "fcb": w["fcb"], "W_inp": w["W_inp"], "b_inp": w["b_inp"], "W_out": w["W_out"]}
+    sim, _ = T.build_modules(params, torch.float32)
+    return sim
+
+
+def global_batches(seed=0):
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for b in BATCHES:
+        X = torch.rand(b, 3, generator=g) * 2 - 1
+        z = torch.rand(b, 10, 5, generator=g) * 2 - 1
+        z[:, :, 1:3] = torch.rand(b, 10, 2, generator=g) * 1.1
+        out.append((X, torch.zeros(b, 1), z))
+    return out
+
+
+def train(loader, grad_sync=None, epochs=2):
+    torch.manual_seed(11)
+    ctrl = fca.FNNModel(3, 50, 1, 1)
+    if grad_sync is not None:
+        fca.distributed.broadcast_params(ctrl)
+    opt = torch.optim.AdamW(ctrl.parameters(), lr=1e-2)
+    sim = surrogate()
+    losses = [fca.NeuralNetwork.train_model(loader, sim, ctrl, StandInMPCLoss(), opt, "cpu", grad_sync=grad_sync)[0]
+              for _ in range(epochs)]
+    return torch.cat([p.detach().reshape(-1) for p in ctrl.parameters()]).numpy(), np.array(losses)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ranks", type=int, default=2)
+    ap.add_argument("--out", required=True)
+    args = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ:
+        sys.exit(fca.launch.spawn_ranks(args.ranks, os.path.abspath(__file__), sys.argv[1:], timeout=300))
+    rank, _, world = fca.launch.rank_env()
+    assert world == args.ranks
+    dist.init_process_group("gloo")
+    shard = []
+    for X, y, z in global_batches():
+        lo, hi = fca.distributed.shard_range(X.shape[0], rank, world)
+        shard.append((X[lo:hi], y[lo:hi], z[lo:hi]))
+    params, losses = train(shard, fca.distributed.GradAllReduce())
+    np.savez(os.path.join(args.out, f"rank{rank}.npz"), params=params, losses=losses, world=dist.get_world_size())
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

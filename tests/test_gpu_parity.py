@@ -263,3 +263,14 @@ def test_wide_path_hidden_sizes(H, B, N):
     assert relerr(o["xhat"], f["xhat"]) <= TOL
     for k, _ in GRADS:
         assert relerr(o[k], g[k]) <= TOL, (H, k, relerr(o[k], g[k]))
+
+
+@pytest.mark.parametrize("case", ["ref_b15_n10", "h64_b24_n3"])
+def test_nonfinite_incoming_gradient_propagates(case):
+    """A non-finite upstream gradient (an overflowed loss scale) must come out non-finite, as torch's does —
+    not as partly-zeroed finite gradients that hide the overflow from GradScaler / anomaly detection — on the
+    fused path (H <= 52) and the GEMM path (H > 52, wide_bscale_kernel)."""
+    c, params = load_case(case)
+    o = run(params, c["X"], c["u0"], c["states"], c["N"], c["alpha"], c["noise"], dloss=float("inf"))
+    for k, _ in GRADS:
+        assert not np.isfinite(o[k]).all(), k

@@ -147,3 +147,23 @@ def test_inference_refuses_cpu_tensors():
     sim = fca.LSTMModel(5, 50, 4, 3)
     with pytest.raises(RuntimeError, match="ROCm device"):
         fca.simulate_step(sim, torch.zeros(2, 10, 5))
+
+
+def test_train_model_data_parallel_through_launcher_gloo(tmp_path):
+    """The launcher bench.py --gpus N uses (forging_control_amd.launch) starts 2 gloo ranks that each run the
+    real NeuralNetwork.train_model(grad_sync=GradAllReduce()) on UNEVEN shards of the reference's B = 15
+    batches (8/7, last batch 4/3): after two epochs both ranks hold bit-identical parameters equal to one
+    process training on the whole batches (train_model passes each rank's batch size to the hook)."""
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__))))
+    import dp_train_worker as W
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dp_train_worker.py")
+    rc = subprocess.run([sys.executable, script, "--ranks", "2", "--out", str(tmp_path)], timeout=400).returncode
+    assert rc == 0
+    res = [np.load(tmp_path / f"rank{r}.npz") for r in (0, 1)]
+    assert all(int(r["world"]) == 2 for r in res)
+    assert np.array_equal(res[0]["params"], res[1]["params"])
+    ref_params, _ = W.train(W.global_batches())
+    assert np.allclose(res[0]["params"], ref_params, rtol=0, atol=2e-6), np.abs(res[0]["params"] - ref_params).max()
+    assert not np.allclose(ref_params, W.train(W.global_batches(), epochs=0)[0])   # training moved them

@@ -57,10 +57,16 @@ def test_oracle_gradients_match_finite_differences():
             assert (lp - lm) / (2 * eps) == pytest.approx(g[key][k][i], rel=1e-6, abs=1e-10)
 
 
-def test_lstm_model_refuses_cpu_tensors():
+def test_lstm_model_on_cpu_is_its_own_nn_lstm():
+    """Off the device the drop-in runs its own nn.LSTM + fc from a zero state (Functions.py:353-379), as the
+    reference's closed-loop harness needs (model(X_new, "cpu"), Functions.py:999); the HIP entry refuses."""
     m = fca.LSTMModel(5, 50, 4, 3)
-    with pytest.raises(RuntimeError, match="ROCm device only"):
-        m(torch.zeros(2, 10, 5), "cpu")
+    x = torch.randn(2, 10, 5)
+    zeros = torch.zeros(3, 2, 50)
+    out, _ = m.lstm(x, (zeros, zeros))
+    assert torch.equal(m(x, "cpu"), m.fc(out[:, -1, :]))
+    with pytest.raises(RuntimeError, match="gfx950 LSTM path"):
+        fca.surrogate.lstm_apply(m, x)
 
 
 def test_abi_validates_before_any_device_call():
