@@ -48,18 +48,22 @@ def hbm_bytes_per_rollout_step(N=10):
 
 
 def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary
-    (profiles/r*_pmc.json, collected by scripts/profile.sh on this workload), or None."""
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of this workload
+    (profiles/round<k>_pmc.json, scripts/profile_round.sh; older profiles/r<k>_pmc.json otherwise), or None."""
     import glob
     import re
-    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json"))
-                   if re.fullmatch(r"r\d+_pmc\.json", os.path.basename(f)))   # the rollout's, not the plant's
-    if not files:
+    pick = []
+    for f in glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")):
+        m = re.fullmatch(r"(round|r)(\d+)_pmc\.json", os.path.basename(f))   # the rollout's, not the plant's
+        if m:
+            pick.append((m.group(1) == "round", int(m.group(2)), f))
+    if not pick:
         return None, None
-    d = json.load(open(files[-1]))
-    if kernel not in d:
+    f = max(pick)[2]
+    d = json.load(open(f))
+    if kernel not in d or not d[kernel].get("hbm_bytes_corrected"):
         return None, None
-    return d[kernel]["hbm_bytes_corrected"], os.path.basename(files[-1])
+    return d[kernel]["hbm_bytes_corrected"], os.path.basename(f)
 
 
 def load_weights(dev, H):

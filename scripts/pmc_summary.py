@@ -1,22 +1,71 @@
-"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes (scripts/profile.sh) into profiles/<tag>_pmc.json."""
+"""Summarise a round profile (scripts/profile_round.sh) into profiles/<tag>_pmc.json and
+profiles/<tag>_kernel_stats.csv: HBM bytes per launch (FETCH_SIZE / WRITE_SIZE passes, gfx950 correction),
+MFMA / VALU / LDS instructions per launch and per wave-cell, and the clock each kernel ran at."""
 import csv
+import glob
 import json
+import shutil
 import sys
 
 tag = sys.argv[1]
-root = sys.argv[2] if len(sys.argv) > 2 else "gpurun_out/prof"
+root = sys.argv[2]
+KERNELS = ("fcr_fwd_kernel", "fcr_bwd_kernel")
+B, N, L, LAYERS, TILE = 65536, 10, 10, 3, 16   # bench.py defaults (config 2)
+WAVES = (B + TILE - 1) // TILE
+
+
+def rows(kind):
+    f = glob.glob(f"{root}/{kind}/**/*counter_collection.csv", recursive=True)
+    return list(csv.DictReader(open(f[0]))) if f else []
+
+
+def per_launch(rs, name, counter):
+    # one row per (dispatch, counter); values are summed over the dispatch's XCDs / SEs by rocprofv3
+    by = {}
+    for r in rs:
+        if name in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            by[r.get("Dispatch_Id", len(by))] = by.get(r.get("Dispatch_Id", len(by)), 0.0) + float(r["Counter_Value"])
+    return (sum(by.values()) / len(by), len(by)) if by else (None, 0)
+
+
 out = {}
-for kind, cnt in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
-    rows = list(csv.DictReader(open(f"{root}/{kind}/{tag}_counter_collection.csv")))
-    for name in ("fcr_fwd_kernel", "fcr_bwd_kernel"):
-        v = [float(r["Counter_Value"]) for r in rows if name in r["Kernel_Name"] and r["Counter_Name"] == cnt]
-        out.setdefault(name, {})[cnt + "_KB_per_launch"] = sum(v) / len(v)
-        out[name]["launches"] = len(v)
-for k, v in out.items():
-    v["hbm_bytes_raw"] = (v["FETCH_SIZE_KB_per_launch"] + v["WRITE_SIZE_KB_per_launch"]) * 1024
-    v["hbm_bytes_corrected"] = (2 * v["FETCH_SIZE_KB_per_launch"] + v["WRITE_SIZE_KB_per_launch"]) * 1024
-out["_note"] = ("rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes (MI355X_MICROARCH.md §HBM); "
-                "units KB; corrected = 2*FETCH (gfx950 reports half of wide coalesced reads) + WRITE. "
-                "Workload: bench.py B=65536 N=10 H=50.")
+for name in KERNELS:
+    d = {}
+    for kind, cnt in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        v, n = per_launch(rows(kind), name, cnt)
+        d[cnt + "_KB_per_launch"] = v
+        d["launches"] = n
+    if d["FETCH_SIZE_KB_per_launch"] is not None and d["WRITE_SIZE_KB_per_launch"] is not None:
+        d["hbm_bytes_raw"] = (d["FETCH_SIZE_KB_per_launch"] + d["WRITE_SIZE_KB_per_launch"]) * 1024
+        d["hbm_bytes_corrected"] = (2 * d["FETCH_SIZE_KB_per_launch"] + d["WRITE_SIZE_KB_per_launch"]) * 1024
+    ins = rows("inst")
+    for cnt in ("SQ_INSTS_VALU_MFMA_F16", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_WAVES", "GRBM_GUI_ACTIVE"):
+        d[cnt + "_per_launch"] = per_launch(ins, name, cnt)[0]
+    m = d["SQ_INSTS_VALU_MFMA_F16_per_launch"]
+    if m:
+        d["mfma_per_wave_cell"] = m / (WAVES * N * L * LAYERS)
+        d["valu_non_mfma_per_wave_cell"] = (d["SQ_INSTS_VALU_per_launch"] - m) / (WAVES * N * L * LAYERS)
+        d["mfma_flop_per_launch"] = m * 16 * 16 * 32 * 2
+    out[name] = d
+
+stats = glob.glob(f"{root}/trace/**/*kernel_stats.csv", recursive=True)
+if stats:
+    shutil.copy(stats[0], f"profiles/{tag}_kernel_stats.csv")
+    for r in csv.DictReader(open(stats[0])):
+        for name in KERNELS:
+            if name in r["Name"]:
+                out[name]["rocprof_avg_ms"] = float(r["AverageNs"]) / 1e6
+                out[name]["rocprof_calls"] = int(r["Calls"])
+for name in KERNELS:
+    d = out[name]
+    if d.get("GRBM_GUI_ACTIVE_per_launch") and d.get("rocprof_avg_ms"):
+        # MI355X_MICROARCH.md DVFS: clock ~ GRBM_GUI_ACTIVE / 8 XCDs / kernel time
+        d["clock_ghz_est"] = d["GRBM_GUI_ACTIVE_per_launch"] / 8 / (d["rocprof_avg_ms"] * 1e-3) / 1e9
+    if d.get("mfma_flop_per_launch") and d.get("rocprof_avg_ms"):
+        d["mfma_tflops_executed"] = d["mfma_flop_per_launch"] / (d["rocprof_avg_ms"] * 1e-3) / 1e12
+out["_note"] = ("rocprofv3 PMC passes of bench.py B=65536 N=10 H=50 (scripts/profile_round.sh): FETCH_SIZE and "
+                "WRITE_SIZE in separate passes, KB; hbm_bytes_corrected = 2*FETCH (gfx950 reports half of wide "
+                "coalesced reads, MI355X_MICROARCH.md HBM) + WRITE. Instruction counts are wave-instructions per "
+                "launch; per wave-cell = / (B/16 waves * N windows * 10 steps * 3 layers).")
 json.dump(out, open(f"profiles/{tag}_pmc.json", "w"), indent=1)
 print(json.dumps(out, indent=1))
