@@ -40,11 +40,23 @@ int launch_check(const char *what) {
     return FCR_OK;
 }
 
+// window-column scales of the f16 split's range guard (fcr_pack.h) -> wsc[8], from the call's inputs
+int launch_range(const fcr_dims *d, const float *states, const float *u0, const float *noise, const float *fcw,
+                 const float *fcb, float *part, float *wsc, hipStream_t s) {
+    hipLaunchKernelGGL(range_partial_kernel, dim3(kRangeBlocks), dim3(kRangeThreads), 0, s, states, u0, noise, d->B,
+                       d->N, part);
+    int rc = launch_check("range_partial_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(range_final_kernel, dim3(1), dim3(64), 0, s, (const float *)part, kRangeBlocks, fcw, fcb, d->H,
+                       wsc);
+    return launch_check("range_final_kernel");
+}
+
 namespace {
 
 struct Layout {
     int HS, nw, nw_pad;
-    size_t fa[3], img[3], fcp, fcb, fnp, xhat, dv, loss_part, fnn_part, hseq, cseq, xw, dseq, dxrow, stamp, total;
+    size_t fa[3], img[3], fcp, fcb, fnp, wsc, rng, xhat, dv, loss_part, fnn_part, hseq, cseq, xw, dseq, dxrow, stamp, total;
     int ctrl_blocks;
 };
 
@@ -100,6 +112,8 @@ Layout make_layout(const fcr_dims *d, int with_backward) {
     L.fcp = take(sizeof(float) * kOut * HS * 4);
     L.fcb = take(sizeof(float) * kOut);
     L.fnp = take(sizeof(float) * kMS * 4 * kFnpStride);
+    L.wsc = take(sizeof(float) * 8);
+    L.rng = take(sizeof(float) * 8 * kRangeBlocks);
     L.xhat = take(sizeof(float) * (size_t)d->B * d->N * kOut);
     L.loss_part = take(sizeof(float) * L.nw_pad);
     L.dv = take(sizeof(float) * (size_t)d->B * d->N);
@@ -131,6 +145,7 @@ Packed packed_ptrs(const Layout &L, char *ws) {
     p.fcp = (const float *)(ws + L.fcp);
     p.fcb = (const float *)(ws + L.fcb);
     p.fnp = (const float *)(ws + L.fnp);
+    p.wsc = (const float *)(ws + L.wsc);
     return p;
 }
 
@@ -179,7 +194,7 @@ int launch_bwd(const BwdArgs &ba, const Layout &L, bool lp, hipStream_t s) {
 // ---------------------------------------------------------------------------------------------
 struct WideLayout {
     size_t wih[3], whh[3], fcw, fcb, cwi, cbi, cwo, fcp, fcbo, fnp, xhat, tot, cmd, err, X0, Hs, Cs, G;
-    size_t Act, dH, dC, D[2], rowg, dv, fnn_part, total;
+    size_t Act, dH, dC, D[2], rowg, dv, fnn_part, wsc, rng, total;
     // split-f16 gate GEMM operands (fcr_wide.h: forward A per layer, backward A per weight, the cells'
     // operand rows XB [3][10][B][6H] (layer 0 rows 3H + kX16 long), the dgate rows [B][12H])
     size_t fa[3], bih[3], XB, dGsp, consts;   // bih: layers >= 1 backward A [12H][2H]
@@ -208,6 +223,8 @@ WideLayout make_wide(const fcr_dims *d, int with_backward) {
     L.fcp = take(F * kOut * kMaxSlots * 4);
     L.fcbo = take(F * kOut);
     L.fnp = take(F * kMS * 4 * kFnpStride);
+    L.wsc = take(F * 8);
+    L.rng = take(F * 8 * kRangeBlocks);
     L.xhat = take(F * B * N * kOut);
     L.tot = take(F * B);
     L.cmd = take(F * B);
@@ -323,19 +340,19 @@ WideSplit wide_split(const WideLayout &L, char *base) {
 
 // Pack the split-f16 GEMM operands of the current weights (fcr_wide.h layouts)
 int wide_pack_split(const float *const *w_ih, const float *const *w_hh, int H, bool backward, const WideSplit &sp,
-                    hipStream_t s) {
+                    const float *wsc, hipStream_t s) {
     const size_t WW = (size_t)4 * H * H;
     int rc;
     for (int l = 0; l < kLayers; ++l) {
         const size_t n = l == 0 ? (size_t)4 * H * (3 * H + kX16) : WW * 6;
         hipLaunchKernelGGL(wide_split_fa_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w_ih[l], w_hh[l], H,
-                           (int)(l == 0), (_Float16 *)sp.fa[l]);
+                           (int)(l == 0), wsc, (_Float16 *)sp.fa[l]);
         if ((rc = launch_check("wide_split_fa_kernel"))) return rc;
         if (!backward) continue;
         if (l == 0) {
             const size_t nb0 = (size_t)12 * H * (H + 8);
             hipLaunchKernelGGL(wide_split_bx0_kernel, dim3((unsigned)((nb0 + 255) / 256)), dim3(256), 0, s, w_ih[0], w_hh[0],
-                               H, (_Float16 *)sp.bx0);
+                               H, wsc, (_Float16 *)sp.bx0);
             if ((rc = launch_check("wide_split_bx0_kernel"))) return rc;
             continue;
         }
@@ -371,6 +388,7 @@ WideArgs wide_args(const fcr_dims *d, const WideLayout &L, char *base) {
     a.dC = L.dC ? (float *)(base + L.dC) : nullptr;
     a.rowg = L.rowg ? (float *)(base + L.rowg) : nullptr;
     a.dv = L.dv ? (float *)(base + L.dv) : nullptr;
+    a.wsc = (const float *)(base + L.wsc);
     return a;
 }
 
@@ -485,7 +503,10 @@ int wide_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const 
     if ((rc = launch_check("pack_misc_kernel"))) return rc;
 
     const WideSplit sp = wide_split(L, base);
-    if ((rc = wide_pack_split(w->w_ih, w->w_hh, (int)H, with_backward != 0, sp, s))) return rc;
+    if ((rc = launch_range(d, states, u0, noise, w->fc_w, w->fc_b, (float *)(base + L.rng), (float *)(base + L.wsc), s)))
+        return rc;
+    if ((rc = wide_pack_split(w->w_ih, w->w_hh, (int)H, with_backward != 0, sp, (const float *)(base + L.wsc), s)))
+        return rc;
     rocblas_handle h = blas_on(s);
     if (!h) return fail(FCR_EHIP, "rocblas_create_handle failed");
     WideArgs a = wide_args(d, L, base);
@@ -577,7 +598,7 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
                     const int c0 = t > 0 ? 0 : H;
                     if ((rc = gemm16_bwd(h, B, H8 - c0, H, sp.bx0 + c0, H8, sp.dGsp, sp.E0 + c0, LE))) return rc;
                     hipLaunchKernelGGL(wide_rowg_kernel, dim3((unsigned)(((size_t)B * kIn + 255) / 256)), dim3(256), 0, s,
-                                       (const float *)(sp.E0 + H), LE, (const float *)sp.consts,
+                                       (const float *)(sp.E0 + H), LE, (const float *)sp.consts, a.wsc,
                                        a.rowg + (size_t)(j + t) * B * kIn, B);
                     if ((rc = launch_check("wide_rowg_kernel"))) return rc;
                 }
@@ -796,6 +817,9 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
     pa.fcp = (float *)(base + L.fcp);
     pa.fcbo = (float *)(base + L.fcb);
     pa.fnp = (float *)(base + L.fnp);
+    pa.wsc = (const float *)(base + L.wsc);
+    if ((rc = launch_range(d, states, u0, noise, w->fc_w, w->fc_b, (float *)(base + L.rng), (float *)(base + L.wsc), s)))
+        return rc;
     for (int l = 0; l < kLayers; ++l) {
         const int nf = L.HS * (l == 0 ? (L.HS + 2 + 7) / 8 : (2 * L.HS + 7) / 8) * kWave * 8;   // per (tile, block, lane, k)
         hipLaunchKernelGGL(pack_fwd16_kernel, dim3((nf + 255) / 256), dim3(256), 0, s, pa, l,

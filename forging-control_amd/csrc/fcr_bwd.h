@@ -368,6 +368,7 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
     // d loss / d (one step-cost term) = dloss / (B N)   (Functions.py:1458, 1463)
     const float wgt = valid ? a.dloss[0] / ((float)a.B * (float)N) : 0.0f;
     const float ref = a.X[(size_t)bc * kCtrlIn + 2];
+    const float scq = a.p.wsc[q], sc4 = a.p.wsc[4];   // range guard (fcr_pack.h): d/dv = 2^-s_c d/dv'
     const float s84 = a.states[(size_t)bc * kL * kIn + (kL - 2) * kIn + 4];
     const float *pred = a.prediction + (size_t)bc * N;
     const float *xh = a.xhat + (size_t)bc * N * kOut;
@@ -532,16 +533,16 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
             float dxq, dx4;
             bwd_cell<HS, true, true, false, true, true, true, LP>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
                                                             next_of(j, 0, t), sp);
-            buf_st2(rr, lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{dxq, dx4});   // row j+t
+            buf_st2(rr, lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{dxq * scq, dx4 * sc4});   // row j+t
         }
         {
             float dxq, dx4;
             bwd_cell<HS, true, true, false, true, false, true, LP>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
                                                              next_of(j, 0, 1), sp);
-            buf_st2(rr, lane * 8, (uint32_t)((j * kL + 1) * kWave * 8), f32x2{dxq, dx4});   // row j+1
+            buf_st2(rr, lane * 8, (uint32_t)((j * kL + 1) * kWave * 8), f32x2{dxq * scq, dx4 * sc4});   // row j+1
             bwd_cell<HS, true, true, true, false, true, false, LP>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
                                                              next_of(j, 0, 0), sp);
-            buf_st2(rr, lane * 8, (uint32_t)((j * kL) * kWave * 8), f32x2{dxq, dx4});   // row j
+            buf_st2(rr, lane * 8, (uint32_t)((j * kL) * kWave * 8), f32x2{dxq * scq, dx4 * sc4});   // row j
         }
     }
     const float g_u0_rows = row_grad(kL - 1)[1];   // row 9, col 4 = u0 (Functions.py:1396)

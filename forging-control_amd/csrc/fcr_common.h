@@ -55,6 +55,7 @@ struct Packed {                    // device pointers into the workspace
     const float *fcp;              // fc.weight in lane layout [o][slot][q]
     const float *fcb;              // fc.bias [4]
     const float *fnp;              // controller records [m][q][8]
+    const float *wsc;              // window-column scales 2^-s_c [8] (range_final_kernel, fcr_pack.h)
 };
 
 // Sequence slabs (per wave, each address written once per call):

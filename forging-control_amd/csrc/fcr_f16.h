@@ -281,9 +281,9 @@ __device__ __forceinline__ float fwd16_weight(const PackArgs &a, int l, int unit
                 const int u = 4 * s + kq;
                 if (u < H) v = a.whh[0][grow * H + u];
             } else if (s == HS) {
-                v = a.wih[0][grow * kIn + kq];
+                v = a.wih[0][grow * kIn + kq] / a.wsc[kq];          // range guard (fcr_pack.h): exact
             } else if (s == HS + 1 && kq == 0) {
-                v = a.wih[0][grow * kIn + 4];
+                v = a.wih[0][grow * kIn + 4] / a.wsc[4];
             }
         } else if (s < HS) {
             const int u = 4 * s + kq;

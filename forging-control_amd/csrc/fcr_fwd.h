@@ -202,13 +202,14 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
     const float ref = a.X[(size_t)bc * kCtrlIn + 2];                 // Functions.py:1392
     const float *st = a.states + (size_t)bc * kL * kIn;
     float w0[kL], w1[kL];                                             // window ring, B-operand layout
+    const float scq = a.p.wsc[q], sc4 = a.p.wsc[4];   // range guard (fcr_pack.h): the ring holds v 2^-s_c
 #pragma unroll
     for (int t = 0; t < kL; ++t) {
-        w0[t] = st[t * kIn + q];
-        w1[t] = (q == 0) ? st[t * kIn + 4] : 0.0f;
+        w0[t] = st[t * kIn + q] * scq;
+        w1[t] = (q == 0) ? st[t * kIn + 4] * sc4 : 0.0f;
     }
     const float u0 = a.u0[bc];
-    if (q == 0) w1[kL - 1] = u0;                                      // Functions.py:1396
+    if (q == 0) w1[kL - 1] = u0 * sc4;                                // Functions.py:1396
     float u_prev = u0;
     float cmd_j = alpha * sq(st[(kL - 2) * kIn + 4] - u0);            // Functions.py:1405
     float cmd_sum = 0.0f, err_sum = 0.0f, tot_sum = 0.0f;
@@ -251,8 +252,8 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
                 w0[k] = w0[k + 1];
                 w1[k] = w1[k + 1];
             }
-            w0[kL - 1] = sel4(q, xh0, xh1, xh2, xh3);
-            w1[kL - 1] = (q == 0) ? un : 0.0f;
+            w0[kL - 1] = sel4(q, xh0, xh1, xh2, xh3) * scq;
+            w1[kL - 1] = (q == 0) ? un * sc4 : 0.0f;
             u_prev = un;
             pred = un;
         }

@@ -85,9 +85,9 @@ __global__ void pack_img_kernel(PackArgs a, int l, _Float16 *dst) {
                     const int u = 4 * s + grp;
                     if (u < H) v = a.whh[0][grow * H + u];
                 } else if (s == HS) {
-                    v = a.wih[0][grow * kIn + grp];
+                    v = a.wih[0][grow * kIn + grp] / a.wsc[grp];   // range guard (fcr_pack.h): exact
                 } else if (grp == 0) {   // s == HS + 1
-                    v = a.wih[0][grow * kIn + 4];
+                    v = a.wih[0][grow * kIn + 4] / a.wsc[4];
                 }
             } else if (s < HS) {
                 const int u = 4 * s + grp;

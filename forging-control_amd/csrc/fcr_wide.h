@@ -28,6 +28,7 @@ struct WideArgs {
     float *X0, *Hs, *Cs, *Act, *G, *dH, *dC, *rowg, *dv;
     const float *dloss;
     _Float16 *xb0;   // split-f16 rollout: layer-0 operand rows (slot stride B 6H, row stride xb0_ld), else null
+    const float *wsc;   // window-column scales of the split's range guard (fcr_pack.h)
 };
 
 // layer 0's K = 5 window-row input as the last kX16 columns of its split-f16 operand rows and weights:
@@ -92,9 +93,10 @@ __global__ void wide_window_kernel(WideArgs a, int j) {
         if (a.xb0) {
             _Float16 *p = a.xb0 + (size_t)t * a.B * 6 * a.H + (size_t)b * xb0_ld(a.H) + 3 * a.H;
             for (int col = 0; col < kIn; ++col) {
-                const _Float16 hi = (_Float16)x[col];
+                const float v = x[col] * a.wsc[col];   // range guard (fcr_pack.h): v 2^-s_c against W_ih0 2^s_c
+                const _Float16 hi = (_Float16)v;
                 p[col] = hi;
-                p[kIn + col] = (_Float16)(x[col] - (float)hi);
+                p[kIn + col] = (_Float16)(v - (float)hi);
                 p[2 * kIn + col] = hi;
             }
             for (int k = 3 * kIn; k < kX16; ++k) p[k] = (_Float16)0.0f;
@@ -334,7 +336,7 @@ __global__ void wide_cell_bwd_kernel(const float *__restrict__ act, const float 
 // against operand rows [x_hi | x_lo | x_hi | h_hi | h_lo | h_hi] (layer 0: [h part | x part of kX16 columns]);
 // backward A (below) stacks [W_hi ; W_hi ; W_lo] (12H rows) against the dgate rows [dG_hi | dG_lo | dG_hi].
 __global__ void wide_split_fa_kernel(const float *__restrict__ Wih, const float *__restrict__ Whh, int H, int layer0,
-                                     _Float16 *dst) {
+                                     const float *__restrict__ wsc, _Float16 *dst) {
     const int KA = layer0 ? 3 * H + kX16 : 6 * H;
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (size_t)4 * H * KA) return;
@@ -352,7 +354,7 @@ __global__ void wide_split_fa_kernel(const float *__restrict__ Wih, const float 
                 return;
             }
             term = kk / kIn;
-            v = Wih[(size_t)r * kIn + kk % kIn];
+            v = Wih[(size_t)r * kIn + kk % kIn] / wsc[kk % kIn];   // range guard (fcr_pack.h): exact
         }
     } else {
         const int part = k / (3 * H), kk = k % (3 * H), u = kk % H;
@@ -366,14 +368,14 @@ __global__ void wide_split_fa_kernel(const float *__restrict__ Wih, const float 
 // Layer 0's backward A, row-major [12H][H + 8]: per split row the W_hh row (H columns), then the W_ih row
 // (kIn columns) and zero padding — ONE product gives dh_{t-1} and the window-row gradient of the cell.
 __global__ void wide_split_bx0_kernel(const float *__restrict__ Wih, const float *__restrict__ Whh, int H,
-                                      _Float16 *dst) {
+                                      const float *__restrict__ wsc, _Float16 *dst) {
     const int ld = H + 8;
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (size_t)12 * H * ld) return;
     const int r = (int)(idx / ld), col = (int)(idx % ld), term = r / (4 * H), g = r % (4 * H);
     float v = 0.0f;
     if (col < H) v = Whh[(size_t)g * H + col];
-    else if (col < H + kIn) v = Wih[(size_t)g * kIn + col - H];
+    else if (col < H + kIn) v = Wih[(size_t)g * kIn + col - H] / wsc[col - H];
     const _Float16 hi = (_Float16)v;
     dst[idx] = term < 2 ? hi : (_Float16)(v - (float)hi);
 }
@@ -388,13 +390,14 @@ __global__ void wide_split_bcat_kernel(const float *__restrict__ Wih, const floa
     const _Float16 hi = (_Float16)v;
     dst[idx] = term < 2 ? hi : (_Float16)(v - (float)hi);
 }
-// rowg row += the window-row gradient part of layer 0's backward product (scaled units, see dh_scaled)
-__global__ void wide_rowg_kernel(const float *__restrict__ E, int ldE, const float *__restrict__ consts, float *rowg,
-                                 int B) {
+// rowg row += the window-row gradient part of layer 0's backward product (scaled units, see dh_scaled; the
+// range guard's column scale back, fcr_pack.h)
+__global__ void wide_rowg_kernel(const float *__restrict__ E, int ldE, const float *__restrict__ consts,
+                                 const float *__restrict__ wsc, float *rowg, int B) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= (size_t)B * kIn) return;
     const size_t b = idx / kIn, col = idx % kIn;
-    rowg[idx] += consts[0] * E[b * ldE + col];
+    rowg[idx] += consts[0] * E[b * ldE + col] * wsc[col];
 }
 
 // The dgates are split as dG * 2^k / dloss (|dG| ~ dloss / (B N): without it they would sit in the f16

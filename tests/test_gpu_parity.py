@@ -274,3 +274,34 @@ def test_nonfinite_incoming_gradient_propagates(case):
     o = run(params, c["X"], c["u0"], c["states"], c["N"], c["alpha"], c["noise"], dloss=float("inf"))
     for k, _ in GRADS:
         assert not np.isfinite(o[k]).all(), k
+
+
+@pytest.mark.parametrize("H", [50, 64])
+@pytest.mark.parametrize("scale", [1e5, 3e7])
+def test_unscaled_window_values_stay_finite_like_torch_fp32(H, scale):
+    """Window values beyond the f16 range (states x 1e5; x 3e7 ~ unscaled press pressures in Pa,
+    results/*_dataframe.txt) would overflow the f16 split of the gate-product operands (hi = f16(v) = inf ->
+    NaN), where torch fp32 stays finite. The range guard (fcr_pack.h) runs those columns on v 2^-s_c against
+    W_ih0 2^s_c: the rollout stays finite and close to fp64 on the fused path and the GEMM path. At these
+    magnitudes a layer-0 gate pre-activation carries an absolute error ~|W||v| 2^-24 in fp32 (torch) and
+    ~|W||v| 2^-22 in the split product (the dropped lo·lo term): the rare gate whose |W||v| ~ 1e7 terms cancel
+    to near 0 lands on a different sigmoid value in any fp32 implementation. Bound: 5e-5, or 4x torch fp32's
+    own distance to fp64 (measured at x 3e7, H = 50: prediction 1.3e-5 vs torch fp32 1.3e-7)."""
+    from oracle import rollout_torch as TT
+    from tests.golden.make_golden import synth_params
+    params = load_case("ref_b15_n10")[1] if H == 50 else synth_params(H, 7)
+    if H != 50:
+        params = {"Wih": [np.asarray(a, np.float64) for a in params["Wih"]],
+                  "Whh": [np.asarray(a, np.float64) for a in params["Whh"]],
+                  **{k: np.asarray(params[k], np.float64) for k in ("fcW", "fcb", "W_inp", "b_inp", "W_out")}}
+    B, N = 48, 4
+    X, S, _ = _synth(B, N, 31)
+    S = (S * scale).astype(np.float32)
+    u0 = _u0(params, X)
+    o = run(params, X, u0, S, N, 20.0)
+    r64 = TT.loss_and_grads(params, X, u0, S, N, 20.0, dtype=torch.float64)
+    r32 = TT.loss_and_grads(params, X, u0, S, N, 20.0, dtype=torch.float32)
+    for k in FEATS + ("xhat",) + tuple(g for g, _ in GRADS):
+        assert np.isfinite(o[k]).all(), k
+        e_hip, e_t32 = relerr(o[k], r64[k]), relerr(r32[k], r64[k])
+        assert e_hip <= max(5e-5, 4 * e_t32), (k, e_hip, e_t32)
