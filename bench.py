@@ -259,6 +259,9 @@ def main():
     ap.add_argument("--precision", choices=("fp32", "f16", "f16fwd"), default="fp32",
                     help="fp32: reference-accurate (default, config 2); f16: gate products in f16 in both passes; "
                          "f16fwd: f16 forward, fp32-accurate backward (config 3)")
+    ap.add_argument("--small-limit", type=int, default=None,
+                    help="fcr_set_small_batch_limit: B at or below it runs the small-batch kernels (0 = never; "
+                         "default: the library's, 8192)")
     args = ap.parse_args()
 
     # --gpus N without a launcher: start N ranks (torchrun) as a child BEFORE anything touches the GPU
@@ -273,6 +276,10 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
         world = dist.get_world_size()
     B, N, H = args.batch, args.horizon, args.hidden
+    if args.small_limit is not None:
+        fca._native.set_small_batch_limit(args.small_limit)
+    # which kernel family runs (include/fcr.h, fcr_set_small_batch_limit)
+    small = args.precision == "fp32" and 17 <= H <= 52 and B <= fca._native.small_batch_limit()
 
     sim, ctrl = load_weights(dev, H)
     if world > 1:
@@ -331,7 +338,8 @@ def main():
         fl = flops_per_rollout_step(H)
         dom = ("bwd", b_ms) if b_ms >= f_ms else ("fwd", f_ms)
         narrow = H <= 52
-        kernel = f"fcr_{dom[0]}_kernel" if narrow else "wide path (split-f16 GEMMs + cell kernels)"
+        kernel = (f"fcr_s{dom[0]}_kernel" if small else f"fcr_{dom[0]}_kernel") if narrow else \
+            "wide path (split-f16 GEMMs + cell kernels)"
         achieved = B * N * fl[dom[0]] / (dom[1] * 1e-3) / 1e12
         hbm_roof = HBM_PEAK_GBS * 1e9 / hbm_bytes_per_rollout_step(N)
         default_cfg = (B, N, H, args.precision) == (65536, 10, 50, "fp32")

@@ -21,7 +21,7 @@ ERRORS = {-1: "FCR_EINVAL", -2: "FCR_EWORKSPACE", -3: "FCR_EHIP", -4: "FCR_EUNSU
 # Every symbol include/fcr.h declares (tests check the .so exports exactly these).
 EXPORTS = ("fcr_workspace_size", "fcr_forward", "fcr_backward", "fcr_lstm_workspace_size", "fcr_lstm_forward",
            "fcr_lstm_backward", "fcr_plant_rk4", "fcr_closed_loop_run", "fcr_window_gather", "fcr_fnn_workspace_size",
-           "fcr_fnn_forward", "fcr_fnn_backward", "fcr_last_error", "fcr_abi_version")
+           "fcr_fnn_forward", "fcr_fnn_backward", "fcr_set_small_batch_limit", "fcr_last_error", "fcr_abi_version")
 
 
 class FcrDims(ctypes.Structure):
@@ -107,6 +107,8 @@ def load() -> ctypes.CDLL:
         lib.fcr_fnn_forward.restype = i32
         lib.fcr_fnn_backward.argtypes = [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp]
         lib.fcr_fnn_backward.restype = i32
+        lib.fcr_set_small_batch_limit.argtypes = [i32]
+        lib.fcr_set_small_batch_limit.restype = i32
         lib.fcr_last_error.argtypes = []
         lib.fcr_last_error.restype = ctypes.c_char_p
         lib.fcr_abi_version.argtypes = []
@@ -121,6 +123,18 @@ def check(rc: int, what: str) -> None:
     if rc != FCR_OK:
         msg = load().fcr_last_error().decode(errors="replace")
         raise NativeError(f"{what} failed ({ERRORS.get(rc, rc)}): {msg}")
+
+
+def set_small_batch_limit(max_batch: int) -> int:
+    """fcr_set_small_batch_limit: B <= max_batch runs the small-batch kernels (0 = never); returns the old limit."""
+    return int(load().fcr_set_small_batch_limit(int(max_batch)))
+
+
+def small_batch_limit() -> int:
+    """The current small-batch limit (fcr_set_small_batch_limit's value)."""
+    cur = set_small_batch_limit(0)
+    set_small_batch_limit(cur)
+    return cur
 
 
 def workspace_bytes(dims: FcrDims, with_backward: bool) -> int:

@@ -19,6 +19,7 @@
 #include "fcr_img.h"
 #include "fcr_pack.h"
 #include "fcr_host.h"
+#include "fcr_small.h"
 #include "fcr_surrogate.h"
 #include "fcr_wide.h"
 
@@ -127,7 +128,9 @@ Layout make_layout(const fcr_dims *d, int with_backward) {
         L.cseq = take(sizeof(f32x4) * qcells);
         L.xw = take(sizeof(f32x2) * (size_t)L.nw_pad * d->N * kL * kWave);
         L.dseq = take(sizeof(f32x4) * (size_t)L.nw_pad * d->N * 2 * kL * HS * 16);
-        L.dxrow = take(sizeof(f32x2) * (size_t)L.nw_pad * d->N * kL * kWave);
+        // the small-batch backward keeps one copy per wave of its group (fcr_small.h)
+        const size_t rows_waves = L.nw_pad > 4 * L.nw ? L.nw_pad : 4 * L.nw;
+        L.dxrow = take(sizeof(f32x2) * rows_waves * d->N * kL * kWave);
     }
 #if FCR_STAMP
     L.stamp = take(sizeof(unsigned long long) * L.nw_pad * 16);   // [backward 8 | forward 8] per wave
@@ -187,6 +190,42 @@ int launch_bwd_t(const BwdArgs &ba, const Layout &L, hipStream_t s) {
 template <int HS>
 int launch_bwd(const BwdArgs &ba, const Layout &L, bool lp, hipStream_t s) {
     return lp ? launch_bwd_t<HS, true>(ba, L, s) : launch_bwd_t<HS, false>(ba, L, s);
+}
+
+// Small-batch kernels (fcr_small.h): one workgroup of ceil(HS/4) waves per 16-trajectory group.
+// Used for the fp32-accurate mode at HS = 8, 13 when B <= g_small_max_batch (fcr_set_small_batch_limit):
+// below one wave per SIMD the fused kernels run at one wave's sequential latency.
+int g_small_max_batch = 8192;
+bool use_small(const fcr_dims *d, const Layout &L) {
+    return d->precision == FCR_PRECISION_FP32 && (L.HS == 8 || L.HS == 13) && d->B <= g_small_max_batch;
+}
+
+template <int HS, bool STORE>
+int launch_sfwd_t(const FwdArgs &fa, const Layout &L, hipStream_t s) {
+    constexpr int lds = Small<HS>::LDS_FWD;
+    static bool attr_set = false;
+    if (!attr_set) {
+        const hipError_t e = hipFuncSetAttribute((const void *)fcr_sfwd_kernel<HS, STORE>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(sfwd): %s", hipGetErrorString(e));
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((fcr_sfwd_kernel<HS, STORE>), dim3(L.nw), dim3(Small<HS>::NQ * kWave), lds, s, fa);
+    return launch_check("fcr_sfwd_kernel");
+}
+
+template <int HS>
+int launch_sbwd_t(const BwdArgs &ba, const Layout &L, hipStream_t s) {
+    constexpr int lds = Small<HS>::LDS_BWD;
+    static bool attr_set = false;
+    if (!attr_set) {
+        const hipError_t e = hipFuncSetAttribute((const void *)fcr_sbwd_kernel<HS>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(sbwd): %s", hipGetErrorString(e));
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((fcr_sbwd_kernel<HS>), dim3(L.nw), dim3(Small<HS>::NQ * kWave), lds, s, ba);
+    return launch_check("fcr_sbwd_kernel");
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -762,6 +801,12 @@ const char *fcr_last_error(void) { return g_err; }
 
 int fcr_abi_version(void) { return FCR_ABI_VERSION; }
 
+int fcr_set_small_batch_limit(int32_t max_batch) {
+    const int prev = g_small_max_batch;
+    g_small_max_batch = max_batch < 0 ? 0 : max_batch;
+    return prev;
+}
+
 #if FCR_STAMP
 // diagnostic builds: byte offset (in ws) of the per-wave cycle sums [nw_pad][8] of the backward
 size_t fcr_debug_stamp_offset(const fcr_dims *d) { return make_layout(d, 1).stamp; }
@@ -857,15 +902,22 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
 #if FCR_STAMP
     fa.stamp = (unsigned long long *)(base + L.stamp) + (size_t)L.nw_pad * 8;
 #endif
-    switch (L.HS) {
-        case 4: rc = launch_fwd<4>(fa, L, d->precision != FCR_PRECISION_FP32, s); break;
-        case 8: rc = launch_fwd<8>(fa, L, d->precision != FCR_PRECISION_FP32, s); break;
-        case 13: rc = launch_fwd<13>(fa, L, d->precision != FCR_PRECISION_FP32, s); break;
-        default: rc = fail(FCR_EUNSUPPORTED, "H=%d", d->H);
+    const bool small = use_small(d, L);
+    if (small) {
+        if (L.HS == 8) rc = with_backward ? launch_sfwd_t<8, true>(fa, L, s) : launch_sfwd_t<8, false>(fa, L, s);
+        else rc = with_backward ? launch_sfwd_t<13, true>(fa, L, s) : launch_sfwd_t<13, false>(fa, L, s);
+    } else {
+        switch (L.HS) {
+            case 4: rc = launch_fwd<4>(fa, L, d->precision != FCR_PRECISION_FP32, s); break;
+            case 8: rc = launch_fwd<8>(fa, L, d->precision != FCR_PRECISION_FP32, s); break;
+            case 13: rc = launch_fwd<13>(fa, L, d->precision != FCR_PRECISION_FP32, s); break;
+            default: rc = fail(FCR_EUNSUPPORTED, "H=%d", d->H);
+        }
     }
     if (rc) return rc;
+    // the fused kernel writes a (zero) partial for every padded wave; the small one one per group
     hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(256), 0, s, (const float *)fa.loss_part,
-                       L.nw_pad, d->B, loss);
+                       small ? L.nw : L.nw_pad, d->B, loss);
     return launch_check("loss_reduce_kernel");
 }
 
@@ -909,11 +961,15 @@ int fcr_backward(const fcr_dims *d, const float *X, const float *states, const f
     ba.stamp = (unsigned long long *)(base + L.stamp);
 #endif
     ba.p = packed_ptrs(L, base);
-    switch (L.HS) {
-        case 4: rc = launch_bwd<4>(ba, L, d->precision == FCR_PRECISION_F16, s); break;
-        case 8: rc = launch_bwd<8>(ba, L, d->precision == FCR_PRECISION_F16, s); break;
-        case 13: rc = launch_bwd<13>(ba, L, d->precision == FCR_PRECISION_F16, s); break;
-        default: rc = fail(FCR_EUNSUPPORTED, "H=%d", d->H);
+    if (use_small(d, L)) {
+        rc = L.HS == 8 ? launch_sbwd_t<8>(ba, L, s) : launch_sbwd_t<13>(ba, L, s);
+    } else {
+        switch (L.HS) {
+            case 4: rc = launch_bwd<4>(ba, L, d->precision == FCR_PRECISION_F16, s); break;
+            case 8: rc = launch_bwd<8>(ba, L, d->precision == FCR_PRECISION_F16, s); break;
+            case 13: rc = launch_bwd<13>(ba, L, d->precision == FCR_PRECISION_F16, s); break;
+            default: rc = fail(FCR_EUNSUPPORTED, "H=%d", d->H);
+        }
     }
     if (rc) return rc;
     float *part = (float *)(base + L.fnn_part);

@@ -64,7 +64,9 @@ __device__ __forceinline__ void pace_cell(Pace &p) {
 #endif
 }
 
-template <int HS, bool L0, bool FIRST, bool LP>
+// R0, R1: the tile (unit slot) range this wave computes — the whole cell by default; the small-batch
+// kernels (fcr_small.h) split a cell's tiles over the waves of a workgroup (R0 even).
+template <int HS, bool L0, bool FIRST, bool LP, int R0 = 0, int R1 = HS>
 __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lane, float x0, float x1,
                                            const float (&x)[HS], const float (&hp)[HS], float (&c)[HS],
                                            float (&hout)[HS], Pace &turn) {
@@ -73,7 +75,8 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
     constexpr int KB = L0 ? G::KB0 : G::KB1;
     constexpr int KLO = (L0 && FIRST) ? G::XBLK : 0;
     constexpr int KHI = FIRST ? (L0 ? G::XBLK + 1 : G::KX1) : KB;
-    constexpr int NP = (HS + 1) / 2;   // tile pairs
+    constexpr int P0 = R0 / 2, P1 = (R1 + 1) / 2;   // tile pairs [P0, P1)
+    static_assert(R0 % 2 == 0 && R0 < R1 && R1 <= HS, "tile range");
     // packed tail block (fcr_f16.h): one MFMA on the tail fragment, no lo fragment
     constexpr bool TAIL = !L0 && G::TAIL1;
     constexpr int KT = TAIL ? KB - 1 : KB;   // lo fragments per tile
@@ -87,15 +90,15 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
         if (!LP && !(TAIL && kb == KB - 1)) l = lds_frag16(lw, HS * KB + r * KT + kb, lane);
     };
     f16x8 ah[2], al[2] = {};
-    rd(0, KLO, ah[0], al[0]);
-    if (HS > 1) rd(1, KLO, ah[1], al[1]);
+    rd(R0, KLO, ah[0], al[0]);
+    if (R0 + 1 < R1) rd(R0 + 1, KLO, ah[1], al[1]);
     f32x4 prev[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
     constexpr int R = KHI - KLO;   // regions per tile pair
     float po[2] = {0.0f, 0.0f};    // output gates of the previous pair between the pointwise stages
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {
+    for (int p = P0; p < P1; ++p) {
         const int r0 = 2 * p, r1 = 2 * p + 1;
-        const bool two = r1 < HS;
+        const bool two = r1 < R1;
         f32x4 acc[2][2];
 #pragma unroll
         for (int u = 0; u < 2; ++u) acc[u][0] = acc[u][1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -107,9 +110,9 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
             if (kb + 1 < KHI) {
                 rd(r0, kb + 1, nh[0], nl[0]);
                 if (two) rd(r1, kb + 1, nh[1], nl[1]);
-            } else if (p + 1 < NP) {
+            } else if (p + 1 < P1) {
                 rd(r0 + 2, KLO, nh[0], nl[0]);
-                if (r1 + 2 < HS) rd(r1 + 2, KLO, nh[1], nl[1]);
+                if (r1 + 2 < R1) rd(r1 + 2, KLO, nh[1], nl[1]);
             }
             const int ch = kOneAcc ? 0 : (kb - KLO) & 1;
 #if FCR_ABLATE == 1   // diagnostic: the fragment reads and operands stay, the MFMAs go
@@ -124,7 +127,7 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
                 if (two) acc[1][ch] = mma_p<LP>(ah[1], al[1], bh[kb], bl[kb], acc[1][ch]);
             }
 #endif
-            if (p > 0) {
+            if (p > P0) {
 #if FCR_FWD_SPREAD
                 // the previous pair's pointwise, spread over this pair's regions beside its MFMAs
                 // (R >= 3: gates of slot r0 | gates of slot r1 | both h; R = 2: both gates | both h)
@@ -154,8 +157,8 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
         prev[1] = kOneAcc ? acc[1][0] : acc[1][0] + acc[1][1];
     }
     sched_fence();
-    lstm_point<FIRST>(prev[0], c[2 * NP - 2], c[2 * NP - 2], hout[2 * NP - 2]);
-    if (2 * NP - 1 < HS) lstm_point<FIRST>(prev[1], c[2 * NP - 1], c[2 * NP - 1], hout[2 * NP - 1]);
+    lstm_point<FIRST>(prev[0], c[2 * P1 - 2], c[2 * P1 - 2], hout[2 * P1 - 2]);
+    if (2 * P1 - 1 < R1) lstm_point<FIRST>(prev[1], c[2 * P1 - 1], c[2 * P1 - 1], hout[2 * P1 - 1]);
 }
 
 #ifndef FCR_STAMP

@@ -223,6 +223,15 @@ int fcr_lstm_backward(const fcr_dims *dims, const fcr_weights *w, const float *d
                       float *const *g_w_ih, float *const *g_w_hh, float *g_fc_w, float *g_fc_b, float *g_x,
                       void *ws, size_t ws_bytes, void *stream);
 
+/*
+ * Kernel choice for small batches (fp32-accurate mode, H 17..52): B <= max_batch runs the small-batch
+ * kernels, which split each 16-trajectory group's cell over the four waves of a workgroup (the reference
+ * trains at B = 15, UL/Main.py:84,297); larger B runs the fused one-wave-per-group kernels. Default 8192;
+ * 0 = never. Process-wide; both kernel families keep the same workspace layout, so a change between a
+ * forward and its backward is harmless. Returns the previous limit.
+ */
+int fcr_set_small_batch_limit(int32_t max_batch);
+
 /* Thread-local description of the last error (never NULL). */
 const char *fcr_last_error(void);
 

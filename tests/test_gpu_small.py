@@ -1,0 +1,119 @@
+"""GPU parity of the small-batch kernels (csrc/fcr_small.h) against the oracle and the fused kernels.
+
+At B <= fcr_set_small_batch_limit (default 8192) the fp32 rollout of H 17..52 runs on workgroups of
+four waves per 16-trajectory group (each wave owns one record quad of unit slots); above it, on the
+fused one-wave-per-group kernels. Both must meet the 1e-5 bar against the fp64 oracle on every golden
+case, and agree with each other to ~1e-7 (the same per-tile MFMA chains and pointwise arithmetic, up to the
+compiler's fma contraction in each instance; the backward's cross-wave partial sums in another fp32 order). The two families share
+the workspace layout, so a forward of one and a backward of the other also pass.
+"""
+import contextlib
+
+import numpy as np
+import pytest
+import torch
+
+import forging_control_amd as fca
+from conftest import case_names, load_case, relerr
+from oracle import rollout_np as R
+from test_gpu_parity import DEV, FEATS, GRADS, TOL, _synth, _u0, modules, run
+
+pytestmark = pytest.mark.gpu
+native = fca._native
+BIG = 1 << 30
+
+
+@contextlib.contextmanager
+def small_limit(n):
+    prev = native.set_small_batch_limit(n)
+    try:
+        yield
+    finally:
+        native.set_small_batch_limit(prev)
+
+
+FUSED_CASES = [n for n in case_names() if load_case(n)[0]["H"] <= 52]
+
+
+def _check_oracle(o, c, name, tag):
+    for k in FEATS + ("xhat",):
+        assert relerr(o[k], c[f"{k}_64"]) <= TOL, (name, tag, k, relerr(o[k], c[f"{k}_64"]))
+    for k, _ in GRADS:
+        assert relerr(o[k], c[f"{k}_64"]) <= TOL, (name, tag, k, relerr(o[k], c[f"{k}_64"]))
+
+
+@pytest.mark.parametrize("name", FUSED_CASES)
+def test_small_and_fused_kernels_meet_oracle(name):
+    c, params = load_case(name)
+    outs = {}
+    for lim in (0, BIG):
+        with small_limit(lim):
+            o = run(params, c["X"], c["u0"], c["states"], c["N"], c["alpha"], c["noise"])
+        _check_oracle(o, c, name, "small" if lim else "fused")
+        outs[lim] = o
+    for k in FEATS + ("xhat",):
+        assert relerr(outs[BIG][k], outs[0][k]) <= 2e-6, (name, k, relerr(outs[BIG][k], outs[0][k]))
+    for k, _ in GRADS:
+        assert relerr(outs[BIG][k], outs[0][k]) <= 2e-6, (name, k, relerr(outs[BIG][k], outs[0][k]))
+
+
+def _run_mixed(params, X, u0, S, N, lim_fwd, lim_bwd):
+    sim, ctrl = modules(params)
+    d = lambda a: torch.as_tensor(np.asarray(a, np.float32), device=DEV)
+    u0_t = d(u0).reshape(-1, 1).requires_grad_(True)
+    with small_limit(lim_fwd):
+        loss, feats = fca.MPCLoss(prediction_horizon=N, alpha=20.0)(sim, ctrl, d(X), u0_t, d(S), DEV)
+    with small_limit(lim_bwd):
+        loss.backward()
+    torch.cuda.synchronize()
+    out = {"g_u0": u0_t.grad.reshape(-1).cpu().numpy()}
+    for k, name in GRADS[1:]:
+        mod, attr = name.split(".")
+        out[k] = getattr(getattr(ctrl, mod), attr).grad.cpu().numpy()
+    return out
+
+
+@pytest.mark.parametrize("lim_fwd,lim_bwd", [(BIG, 0), (0, BIG)])
+def test_forward_of_one_family_backward_of_the_other(lim_fwd, lim_bwd):
+    c, params = load_case("ref_b37_n25")
+    o = _run_mixed(params, c["X"], c["u0"], c["states"], c["N"], lim_fwd, lim_bwd)
+    for k, _ in GRADS:
+        assert relerr(o[k], c[f"{k}_64"]) <= TOL, (k, relerr(o[k], c[f"{k}_64"]))
+
+
+@pytest.mark.parametrize("H,B,N", [(50, 1000, 3), (32, 45, 4), (40, 8, 2), (50, 1, 5)])
+def test_small_kernels_ragged_and_hidden_sizes(H, B, N):
+    """Many groups with a partial last one, the HS = 8 tier (two waves per group), padded units, B = 1."""
+    from tests.golden.make_golden import synth_params
+    params = load_case("ref_b15_n10")[1] if H == 50 else synth_params(H, 500 + H)
+    X, S, _ = _synth(B, N, 600 + H + B)
+    u0 = _u0(params, X)
+    with small_limit(BIG):
+        o = run(params, X, u0, S, N, 20.0)
+    _, f, tape = R.rollout_forward(params, X, u0, S, N, 20.0)
+    g = R.rollout_backward(params, tape)
+    for k in FEATS:
+        assert relerr(o[k], f[k]) <= TOL, (H, B, k, relerr(o[k], f[k]))
+    assert relerr(o["xhat"], f["xhat"]) <= TOL
+    for k, _ in GRADS:
+        assert relerr(o[k], g[k]) <= TOL, (H, B, k, relerr(o[k], g[k]))
+
+
+def test_small_kernels_deterministic_and_dloss_linear():
+    params = load_case("ref_b15_n10")[1]
+    B, N = 300, 10
+    X, S, _ = _synth(B, N, 77)
+    u0 = _u0(params, X)
+    with small_limit(BIG):
+        a = run(params, X, u0, S, N, 20.0)
+        b = run(params, X, u0, S, N, 20.0)
+        c2 = run(params, X, u0, S, N, 20.0, dloss=2.0)
+    for k, _ in GRADS:
+        assert np.array_equal(a[k], b[k]), k
+        assert np.array_equal(2.0 * a[k], c2[k]), k
+
+
+def test_default_limit_routes_the_reference_batch_to_the_small_kernels():
+    prev = native.set_small_batch_limit(123)
+    assert native.set_small_batch_limit(prev) == 123
+    assert prev == 8192
