@@ -810,6 +810,8 @@ int fcr_set_small_batch_limit(int32_t max_batch) {
 #if FCR_STAMP
 // diagnostic builds: byte offset (in ws) of the per-wave cycle sums [nw_pad][8] of the backward
 size_t fcr_debug_stamp_offset(const fcr_dims *d) { return make_layout(d, 1).stamp; }
+size_t fcr_debug_dseq_offset(const fcr_dims *d) { return make_layout(d, 1).dseq; }
+size_t fcr_debug_dxrow_offset(const fcr_dims *d) { return make_layout(d, 1).dxrow; }
 #endif
 
 int fcr_workspace_size(const fcr_dims *dims, int with_backward, size_t *bytes) {

@@ -44,14 +44,15 @@ __device__ __forceinline__ void ld_quads(f32x4 (&dst)[Geo<HS>::HQ], __amdgpu_buf
     }
 }
 
-// DQ >= 0: only quad DQ of din (a small-batch wave's own slots, fcr_small.h); -1: all of it
+// quad k alone (a small-batch wave's own slots, fcr_small.h)
 template <int HS, int k>
 __device__ __forceinline__ void ld_quad(f32x4 (&dst)[Geo<HS>::HQ], __amdgpu_buffer_rsrc_t r, uint32_t off, int lane) {
     dst[k] = buf_ldq<quad_n<HS, k>()>(r, quad_voff<HS, k>(lane), off + quad_soff<HS, k>());
 }
 
-template <int HS, bool NX_L0, bool NX_HC, bool NX_DIN, int DQ = -1>
+template <int HS, bool NX_L0, bool NX_HC, bool NX_DIN>
 __device__ __forceinline__ void load_xhd(CellIn<HS> &ci, const NextIn &n, int lane) {
+    constexpr int HQ = Geo<HS>::HQ;
     if (NX_L0) {
         const f32x2 v = buf_ld2(n.rx, lane * 8, n.x);
         ci.x[0][0] = v[0];
@@ -60,10 +61,7 @@ __device__ __forceinline__ void load_xhd(CellIn<HS> &ci, const NextIn &n, int la
         ld_quads<HS>(ci.x, n.rh, n.x, lane);
     }
     if (NX_HC) ld_quads<HS>(ci.h, n.rh, n.h, lane);
-    if (NX_DIN) {
-        if constexpr (DQ >= 0) ld_quad<HS, DQ>(ci.d, n.rd, n.d, lane);
-        else ld_quads<HS>(ci.d, n.rd, n.d, lane);
-    }
+    if (NX_DIN) ld_quads<HS>(ci.d, n.rd, n.d, lane);
 }
 
 // inverse exp2 pre-scales of the packed gate rows (fcr_img.h), folded into the dgate scaling
@@ -98,17 +96,10 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 #endif
 }
 
-//
-// Small-batch split (fcr_small.h): R0, R1 = the unit slots [R0, R1) this wave owns (R0 even; the whole
-// cell by default). The wave recomputes only its tiles, forms only its dgate blocks and returns, with
-// PART, its partial transposed product over those gate rows (scaled back) in `part` for the workgroup's
-// reduction, instead of dxo / dh_prev; din is fetched for its own quad only.
-template <int HS, bool L0, bool DIN, bool FIRST, bool NX_L0, bool NX_HC, bool NX_DIN, bool LP, int R0 = 0,
-          int R1 = HS, bool PART = false>
+template <int HS, bool L0, bool DIN, bool FIRST, bool NX_L0, bool NX_HC, bool NX_DIN, bool LP>
 __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, const float (&ext)[HS],
                                          float (&dh)[HS], float (&dc)[HS], float (&dxo)[HS], float &dxq,
-                                         float &dx4, CellIn<HS> &ci, const NextIn &nx, Stamps &sp,
-                                         f32x4 *part = nullptr) {
+                                         float &dx4, CellIn<HS> &ci, const NextIn &nx, Stamps &sp) {
     const unsigned long long t0 = stamp_now();
 #if FCR_PRIO
     // the two waves of a SIMD take turns at the higher issue priority, cell by cell, so neither runs
@@ -119,15 +110,11 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
 #endif
     using I = Img<HS, L0>;
     using G = Geo16<HS>;
-    constexpr int KB = I::KB, NB = I::NB;
+    constexpr int KB = I::KB, NB = I::NB, KBB = I::KBB;
     constexpr uint32_t TILE = I::TILE;                  // one slot's 16 image rows
     constexpr uint32_t LO = I::HALF;                    // lo image
     constexpr int KLO = (L0 && FIRST) ? G::XBLK : 0;
     constexpr int KHI = FIRST ? (L0 ? G::XBLK + 1 : G::KX1) : KB;
-    constexpr int K0 = R0 / 2, K1 = (R1 + 1) / 2;   // dgate blocks (slot pairs) of this wave
-    static_assert(R0 % 2 == 0 && R0 < R1 && R1 <= HS, "slot range");
-    static_assert(!PART || (R0 % 4 == 0 && (R1 - R0 == 4 || R1 == HS)), "a split wave owns one record quad");
-    constexpr int DQ = PART ? R0 / 4 : -1;
 
     float up, down, sg0, sgg;   // the trajectory's power-of-two scale, set once the incoming dh is in
 
@@ -223,7 +210,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     auto fwd_pair = [&](int kbb, f32x4 (&fp)[2]) {
 #pragma unroll
         for (int u = 0; u < 2; ++u)
-            if (2 * kbb + u < R1) fwd_tile(2 * kbb + u, fp[u]);
+            if (2 * kbb + u < HS) fwd_tile(2 * kbb + u, fp[u]);
     };
     // dgate block kbb (B operand of the transposed product) from the pair's pre-activations
     auto dgate_block = [&](int kbb, const f32x4 (&fp)[2], f16x8 &gh, f16x8 &gl) {
@@ -231,7 +218,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int r = 2 * kbb + u;
-            if (r < R1) {
+            if (r < HS) {
                 slot_grad(r, fp[u], va + 4 * u, vb + 4 * u);
             } else {
 #pragma unroll
@@ -248,14 +235,14 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     for (int k = 0; k < NB; ++k) acc[k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     f32x4 fa[3][2];
     f16x8 gh[2], gl[2] = {};
-    fwd_pair(K0, fa[0]);
-    if (K1 - K0 > 1) fwd_pair(K0 + 1, fa[1]);
+    fwd_pair(0, fa[0]);
+    if (KBB > 1) fwd_pair(1, fa[1]);
     // ---- incoming dh, and the trajectory's power-of-two scale: issued behind the first forward MFMAs,
     // which only need this cell's (prefetched) inputs, so the previous cell's tail overlaps them ----
     {
         float m = 0.0f;
 #pragma unroll
-        for (int r = R0; r < R1; ++r) {
+        for (int r = 0; r < HS; ++r) {
             dh[r] += DIN ? ci.d[r >> 2][r & 3] : ext[r];
             m = fmaxf(m, fabsf(dh[r]) + fabsf(dc[r]));
         }
@@ -267,20 +254,20 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
         sg0 = up * kInvNegLog2e;   // dgate scale of the i, f, o rows
         sgg = sg0 * -0.5f;         // and of the g rows
     }
-    load_xhd<HS, NX_L0, NX_HC, NX_DIN, DQ>(ci, nx, lane);   // x, h, din of this cell are consumed
-    dgate_block(K0, fa[0], gh[0], gl[0]);
+    load_xhd<HS, NX_L0, NX_HC, NX_DIN>(ci, nx, lane);   // x, h, din of this cell are consumed
+    dgate_block(0, fa[0], gh[0], gl[0]);
     const unsigned long long t1 = stamp_now();
 #pragma unroll
-    for (int kbb = K0; kbb < K1; ++kbb) {
+    for (int kbb = 0; kbb < KBB; ++kbb) {
         sched_fence();
 #if FCR_BWD_LAUNDER
         asm volatile("" : "+v"(fb), "+v"(tb));
 #endif
         uint32_t tbl = tb + LO;   // lo image base (opaque: keeps the reads' offsets inside 16 bits)
         asm volatile("" : "+v"(tbl));
-        const int cu = (kbb - K0) & 1, nu = cu ^ 1;
-        const bool two = 2 * kbb + 1 < R1;
-        if (kbb + 2 < K1) fwd_pair(kbb + 2, fa[(kbb - K0 + 2) % 3]);
+        const int cu = kbb & 1, nu = cu ^ 1;
+        const bool two = 2 * kbb + 1 < HS;
+        if (kbb + 2 < KBB) fwd_pair(kbb + 2, fa[(kbb + 2) % 3]);
 #pragma unroll
         for (int tau = 0; tau < NB; ++tau) {
             const uint32_t ct = 8u * (2 * (tau >> 1) + (tau & 1)) + 2 * kbb * TILE;
@@ -301,7 +288,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
             // the products only feed the cell's outputs, so IR passes would sink every MFMA to the end
             // of the cell (all fragments live at once); naming the accumulator keeps block kb-1's
             // MFMAs ahead of this point (issued ~NB*3 MFMAs ago: no hazard wait)
-            if (kbb > K0) asm volatile("" : "+v"(acc[tau]));
+            if (kbb > 0) asm volatile("" : "+v"(acc[tau]));
 #if FCR_ABLATE == 1
             acc[tau][0] += (float)ah[0] + (float)gh[cu][0];
 #else
@@ -320,14 +307,11 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
             }
 #endif
         }
-        if (kbb + 1 < K1) dgate_block(kbb + 1, fa[(kbb - K0 + 1) % 3], gh[nu], gl[nu]);
+        if (kbb + 1 < KBB) dgate_block(kbb + 1, fa[(kbb + 1) % 3], gh[nu], gl[nu]);
     }
     sched_fence();
     const unsigned long long t2 = stamp_now();
-    if constexpr (PART) {
-#pragma unroll
-        for (int tau = 0; tau < NB; ++tau) part[tau] = acc[tau] * down;
-    } else if (L0) {
+    if (L0) {
 #pragma unroll
         for (int s = 0; s < HS; ++s) dh[s] = acc[s >> 2][s & 3] * down;
         dxq = acc[HS >> 2][HS & 3] * down;

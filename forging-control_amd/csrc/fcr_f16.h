@@ -68,6 +68,34 @@ __device__ __forceinline__ f16x8 lds_frag16(const float *lw, int idx, int lane) 
     return __builtin_bit_cast(f16x8, lds_quad(lw, idx, lane));
 }
 
+// The splits below write f16 halves with v_fma_mixlo/mixhi_f16. FCR_MIX_ASM = 1 emits them as inline asm
+// (2 instructions per value); the compiler's hazard recognizer does not look inside inline asm, so an
+// asm write may land on a VGPR that an MFMA issued just before still reads as its A/B operand (a WAR
+// hazard the compiler pads with s_nop for its own instructions). FCR_MIX_ASM = 0 writes the same
+// arithmetic as (_Float16)fmaf(a, b, c), which the backend selects as v_fma_mix* (~2.5 instructions per
+// value) with the hazard handled.
+#ifndef FCR_MIX_ASM
+#define FCR_MIX_ASM 0
+#endif
+// (hi, lo) of the products a·b for two values; hi = f16(a·b), lo = f16(a·b - hi), the product exact in the fma
+__device__ __forceinline__ void mix_pair(float a0, float b0, float a1, float b1, unsigned &hp, unsigned &lp) {
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    f16x2 h, l;
+    h[0] = (_Float16)__builtin_fmaf(a0, b0, 0.0f);
+    h[1] = (_Float16)__builtin_fmaf(a1, b1, 0.0f);
+    l[0] = (_Float16)__builtin_fmaf(a0, b0, -(float)h[0]);
+    l[1] = (_Float16)__builtin_fmaf(a1, b1, -(float)h[1]);
+    hp = __builtin_bit_cast(unsigned, h);
+    lp = __builtin_bit_cast(unsigned, l);
+}
+__device__ __forceinline__ unsigned mix_hi(float a0, float b0, float a1, float b1) {
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    f16x2 h;
+    h[0] = (_Float16)__builtin_fmaf(a0, b0, 0.0f);
+    h[1] = (_Float16)__builtin_fmaf(a1, b1, 0.0f);
+    return __builtin_bit_cast(unsigned, h);
+}
+
 // v -> (hi, lo) halves, 8 at a time
 __device__ __forceinline__ void split8(const float (&v)[8], f16x8 &hi, f16x8 &lo) {
 #pragma unroll
@@ -88,12 +116,16 @@ __device__ __forceinline__ void split8s(const float (&v)[8], float s, f16x8 &hi,
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         unsigned hp, lp;
+#if FCR_MIX_ASM
         asm("v_fma_mixlo_f16 %0, %1, %2, 0\n\t"
             "v_fma_mixhi_f16 %0, %3, %2, 0"
             : "=&v"(hp) : "v"(v[2 * p]), "v"(s), "v"(v[2 * p + 1]));
         asm("v_fma_mixlo_f16 %0, %1, %2, -%4 op_sel_hi:[0,0,1]\n\t"
             "v_fma_mixhi_f16 %0, %3, %2, -%4 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
             : "=&v"(lp) : "v"(v[2 * p]), "v"(s), "v"(v[2 * p + 1]), "v"(hp));
+#else
+        mix_pair(v[2 * p], s, v[2 * p + 1], s, hp, lp);
+#endif
         h[p] = hp;
         l[p] = lp;
     }
@@ -107,11 +139,15 @@ __device__ __forceinline__ void cvt8s(const float (&v)[8], float s, f16x8 &hi) {
     u32x4 h;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
+#if FCR_MIX_ASM
         unsigned hp;
         asm("v_fma_mixlo_f16 %0, %1, %2, 0\n\t"
             "v_fma_mixhi_f16 %0, %3, %2, 0"
             : "=&v"(hp) : "v"(v[2 * p]), "v"(s), "v"(v[2 * p + 1]));
         h[p] = hp;
+#else
+        h[p] = mix_hi(v[2 * p], s, v[2 * p + 1], s);
+#endif
     }
     hi = __builtin_bit_cast(f16x8, h);
 }
@@ -125,12 +161,16 @@ __device__ __forceinline__ void split8p(const float (&a)[8], const float (&b)[8]
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         unsigned hp, lp;
+#if FCR_MIX_ASM
         asm("v_fma_mixlo_f16 %0, %1, %2, 0\n\t"
             "v_fma_mixhi_f16 %0, %3, %4, 0"
             : "=&v"(hp) : "v"(a[2 * p]), "v"(b[2 * p]), "v"(a[2 * p + 1]), "v"(b[2 * p + 1]));
         asm("v_fma_mixlo_f16 %0, %1, %2, -%5 op_sel_hi:[0,0,1]\n\t"
             "v_fma_mixhi_f16 %0, %3, %4, -%5 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
             : "=&v"(lp) : "v"(a[2 * p]), "v"(b[2 * p]), "v"(a[2 * p + 1]), "v"(b[2 * p + 1]), "v"(hp));
+#else
+        mix_pair(a[2 * p], b[2 * p], a[2 * p + 1], b[2 * p + 1], hp, lp);
+#endif
         h[p] = hp;
         l[p] = lp;
     }
@@ -142,11 +182,15 @@ __device__ __forceinline__ void cvt8p(const float (&a)[8], const float (&b)[8], 
     u32x4 h;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
+#if FCR_MIX_ASM
         unsigned hp;
         asm("v_fma_mixlo_f16 %0, %1, %2, 0\n\t"
             "v_fma_mixhi_f16 %0, %3, %4, 0"
             : "=&v"(hp) : "v"(a[2 * p]), "v"(b[2 * p]), "v"(a[2 * p + 1]), "v"(b[2 * p + 1]));
         h[p] = hp;
+#else
+        h[p] = mix_hi(a[2 * p], b[2 * p], a[2 * p + 1], b[2 * p + 1]);
+#endif
     }
     hi = __builtin_bit_cast(f16x8, h);
 }

@@ -8,9 +8,9 @@
 //              their c, and the cell's h_t is exchanged through LDS (one barrier per cell) so every
 //              wave has the whole h_{t-1} for the next cell's B operand;
 //   backward — wave w recomputes its tiles, forms the dgates of its slots and the partial transposed
-//              product W[its gate rows]ᵀ·dgates for all output tiles (bwd_cell<..., PART>); the
-//              partials are summed through LDS in a fixed order (two barriers per cell), and each
-//              wave takes the dx / dh_prev of its own slots.
+//              product W[its gate rows]ᵀ·dgates for all output tiles (sb_atile, sb_slot, sb_ttile: bwd_cell's
+//              arithmetic); the partials are summed through LDS in a fixed order (two barriers per cell),
+//              and each wave takes the dx / dh_prev of its own slots.
 // Slab layout (hseq, cseq, xw, dseq) is that of the fused kernels — each wave writes its own quads
 // of a record, and a record is read whole only across a phase barrier — so a split forward and a fused
 // backward (or the reverse) are interchangeable; the backward's window-row gradients go to a per-wave
@@ -81,6 +81,35 @@ __device__ __forceinline__ void store_quad(f32x4 *dst, const float (&v)[HS], int
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 // before a barrier that hands global slab records between waves: this wave's stores are complete
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Per-phase image refill for a workgroup that is alone on its CU: with one workgroup per CU the LDS-DMA
+// refill (lds_fill, ~11 B/cycle) is fully exposed (~10 k cycles per 109 KB image at B = 15). Here each wave
+// loads its share of 1 KiB chunks into registers BEFORE the barrier that retires the old image (the
+// loads overlap the phase's tail skew), then writes them to LDS; the second barrier publishes the image.
+#ifndef FCR_SMALL_VFILL
+#define FCR_SMALL_VFILL 0
+#endif
+template <int NBYTES, int NWAVES>
+__device__ __forceinline__ void small_fill(float *lw, const float *__restrict__ src) {
+#if FCR_SMALL_VFILL
+    static_assert(NBYTES % 1024 == 0, "image must be whole 1 KiB chunks");
+    constexpr int NCH = NBYTES / 1024, PER = (NCH + NWAVES - 1) / NWAVES;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const f32x4 *s4 = reinterpret_cast<const f32x4 *>(src) + lane;
+    f32x4 v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+        if (wv + k * NWAVES < NCH) v[k] = s4[(wv + k * NWAVES) * kWave];
+    __syncthreads();
+    f32x4 *d4 = reinterpret_cast<f32x4 *>(lw) + lane;
+#pragma unroll
+    for (int k = 0; k < PER; ++k)
+        if (wv + k * NWAVES < NCH) d4[(wv + k * NWAVES) * kWave] = v[k];
+    __syncthreads();
+#else
+    lds_fill<NBYTES, NWAVES>(lw, src);
+#endif
+}
 
 // h exchange: wave W publishes its slots of h_t, every wave reads the whole vector back
 template <int HS, int W>
@@ -211,7 +240,7 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
         for (int l = 1; l < kLayers; ++l) {
             const bool keep_h = l == 1 || STORE;
             vm_drain();   // this wave's quads of the layer-below records are in memory before the barrier
-            lds_fill<G::FA1 * 4, NQ>(lw, a.p.fa[l]);
+            small_fill<G::FA1 * 4, NQ>(lw, a.p.fa[l]);
             load_quads<HS>(xc, SEQ_H(l - 1, 0), lane);
             for (int t = 0; t < kL; ++t) {
                 load_quads<HS>(xn, SEQ_H(l - 1, t + 1 < kL ? t + 1 : t), lane);
@@ -277,7 +306,11 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
 }
 
 // ---------------------------------------------------------------------------------------------------
-// backward: the fused backward kernel's program (fcr_bwd.h) with each cell's slots split over the waves
+// backward: the fused backward kernel's program (fcr_bwd.h) with each cell's slots split over the waves,
+// software-pipelined across cells: a cell is A (recompute its gate pre-activations from the stored
+// x_t, h_{t-1}) and B (cell gradients, dgates, the partial transposed product). A needs no gradient, so
+// A(t-1) is issued between B(t) and the reduction of cell t: its MFMAs run while the wave waits at the
+// reduction's barriers.
 // ---------------------------------------------------------------------------------------------------
 // Partial products of one cell -> the sums this wave needs: dh_prev of its slots (L0: combined slots σ =
 // s; else σ = HS + s), dx of its slots (layers >= 1: σ = s, into its dseq quad) and, for L0, the window
@@ -322,19 +355,355 @@ __device__ __forceinline__ void small_reduce(f32x4 *red, const f32x4 (&part)[Sma
     }
 }
 
-template <int HS, bool L0, bool DIN, bool FIRST, bool NX_L0, bool NX_HC, bool NX_DIN>
-__device__ __forceinline__ void sbwd_cell(int w, uint32_t fb, uint32_t tb, int lane, const float (&ext)[HS],
-                                          float (&dh)[HS], float (&dc)[HS], float (&dxo)[HS], float &dxq, float &dx4,
-                                          CellIn<HS> &ci, const NextIn &nx, Stamps &sp, f32x4 *red, f32x4 *dseq_cell) {
-    by_quad<HS>(w, [&](auto Wc) {
-        constexpr int W = decltype(Wc)::v;
-        using Q = QR<HS, W>;
-        f32x4 part[Small<HS>::NB];
-        bwd_cell<HS, L0, DIN, FIRST, NX_L0, NX_HC, NX_DIN, false, Q::R0, Q::R1, true>(fb, tb, lane, ext, dh, dc, dxo, dxq,
-                                                                                     dx4, ci, nx, sp, part);
-        small_reduce<HS, L0, W>(red, part, lane, dh, dxo, dxq, dx4);
-        if (!L0) store_quad<HS, W>(dseq_cell, dxo, lane);
-    });
+// A's operands: the recomputation's B operand (x_t, h_{t-1} of the cell, split into f16 halves)
+template <int HS, bool L0>
+struct AOps {
+    f16x8 bh[Img<HS, L0>::KB], bl[Img<HS, L0>::KB];
+};
+template <int HS, bool L0, bool FIRST>
+struct ARange {
+    using Gm = Geo16<HS>;
+    static constexpr int KB = Img<HS, L0>::KB;
+    static constexpr int KLO = (L0 && FIRST) ? Gm::XBLK : 0;
+    static constexpr int KHI = FIRST ? (L0 ? Gm::XBLK + 1 : Gm::KX1) : KB;
+    static constexpr bool TAIL = !L0 && Gm::TAIL1;
+};
+template <int HS, bool L0, bool FIRST>
+__device__ __forceinline__ void sb_split(const CellIn<HS> &ci, AOps<HS, L0> &o) {
+    using A = ARange<HS, L0, FIRST>;
+    float xv[HS], hv[HS];
+#pragma unroll
+    for (int s = 0; s < HS; ++s) {
+        xv[s] = L0 ? 0.0f : ci.x[s >> 2][s & 3];
+        hv[s] = FIRST ? 0.0f : ci.h[s >> 2][s & 3];
+    }
+    const float x0 = ci.x[0][0], x1 = ci.x[0][1];
+#pragma unroll
+    for (int kb = 0; kb < A::KB; ++kb) o.bh[kb] = o.bl[kb] = f16x8{};
+#pragma unroll
+    for (int kb = A::KLO; kb < A::KHI; ++kb) fwd_operand<HS, L0, FIRST, false>(kb, x0, x1, xv, hv, o.bh[kb], o.bl[kb]);
+    if (A::TAIL && A::KHI == A::KB) o.bh[A::KB - 1] = tail_operand<false>(o.bh[A::KB - 1], o.bl[A::KB - 1]);
+}
+// A: gate pre-activations of this wave's tiles (the forward's products, the same k order), one tile at a
+// time: its image rows (hi, lo per k-block) are read a chunk ahead of its MFMAs
+template <int HS, bool L0>
+struct AFrag {
+    f16x8 h[Img<HS, L0>::KB], l[Img<HS, L0>::KB];
+};
+template <int HS, bool L0, bool FIRST>
+__device__ __forceinline__ void sb_aread(uint32_t fb, int r, AFrag<HS, L0> &f) {
+    using A = ARange<HS, L0, FIRST>;
+    using I = Img<HS, L0>;
+    constexpr uint32_t TILE = I::TILE, LO = I::HALF;
+    uint32_t fbl = fb + LO;
+    asm volatile("" : "+v"(fbl));
+#pragma unroll
+    for (int kb = A::KLO; kb < A::KHI; ++kb) {
+        const f16x4 h0 = lds_b64_f16(fb + 8u * (2 * kb) + r * TILE), h1 = lds_b64_f16(fb + 8u * (2 * kb + 1) + r * TILE);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            f.h[kb][k] = h0[k];
+            f.h[kb][4 + k] = h1[k];
+        }
+        if (!(A::TAIL && kb == A::KB - 1)) {
+            const f16x4 l0 = lds_b64_f16(fbl + 8u * (2 * kb) + r * TILE), l1 = lds_b64_f16(fbl + 8u * (2 * kb + 1) + r * TILE);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                f.l[kb][k] = l0[k];
+                f.l[kb][4 + k] = l1[k];
+            }
+        }
+    }
+}
+template <int HS, bool L0, bool FIRST>
+__device__ __forceinline__ f32x4 sb_atile(const AFrag<HS, L0> &f, const AOps<HS, L0> &o) {
+    using A = ARange<HS, L0, FIRST>;
+    f32x4 g = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int kb = A::KLO; kb < A::KHI; ++kb) {
+        if (A::TAIL && kb == A::KB - 1) g = mfma16(f.h[kb], o.bh[kb], g);
+        else g = mma3(f.h[kb], f.l[kb], o.bh[kb], o.bl[kb], g);
+    }
+    return g;
+}
+
+// B's scale: the incoming dh (+ din or ext) of this wave's slots and the power of two for the f16 split of
+// its dgates (as in bwd_cell: 2^(13-e), e = exponent of the largest |dh| + |dc| of the trajectory's slots)
+struct BScale {
+    float sg0, sgg, down;
+};
+template <int HS, bool DIN, int R0, int R1>
+__device__ __forceinline__ BScale sb_scale(const CellIn<HS> &ci, const float (&ext)[HS], float (&dh)[HS],
+                                           const float (&dc)[HS]) {
+    float m = 0.0f;
+#pragma unroll
+    for (int r = R0; r < R1; ++r) {
+        dh[r] += DIN ? ci.d[r >> 2][r & 3] : ext[r];
+        m = fmaxf(m, fabsf(dh[r]) + fabsf(dc[r]));
+    }
+    m = fmaxf(m, __shfl_xor(m, 16));
+    m = fmaxf(m, __shfl_xor(m, 32));
+    const int e = max(__builtin_amdgcn_frexp_expf(m), -100);   // m < 2^e; all-zero -> e = 0
+    BScale b;
+    b.sg0 = __builtin_amdgcn_ldexpf(1.0f, 13 - e) * kInvNegLog2e;
+    b.sgg = b.sg0 * -0.5f;
+    b.down = __builtin_amdgcn_ldexpf(1.0f, e - 13);
+    return b;
+}
+// cell gradient of slot r from its pre-activations: the 4 dgates as (scaled factor, local derivative)
+// pairs at va/vb[0..3] (multiplied inside the split, split8p)
+template <int HS, bool FIRST>
+__device__ __forceinline__ void sb_slot(int r, f32x4 g, const CellIn<HS> &ci, const BScale &sc, float (&dh)[HS],
+                                        float (&dc)[HS], float *va, float *vb) {
+    f32x4 P;
+    f32x2 Q;
+    lstm_point_grad<FIRST>(g, FIRST ? 0.0f : ci.c[r >> 2][r & 3], P, Q);
+    const float dcv = fmaf(dh[r], P[0], dc[r]);   // dc = dc_carried + dh dh/dc
+    dc[r] = dcv * Q[1];
+    const float dcs = dcv * sc.sg0;
+    va[0] = dcs;
+    vb[0] = P[2];
+    va[1] = dcs;
+    vb[1] = P[3];
+    va[2] = dcv * sc.sgg;
+    vb[2] = Q[0];
+    va[3] = dh[r] * sc.sg0;
+    vb[3] = P[1];
+}
+
+// B's transposed product Wᵀ·dgates over THIS wave's gate rows for output tile tau: the image columns of
+// its blocks (read a tile ahead) and 3 MFMAs per block (2 for a half block)
+template <int HS, bool L0, int R0, int R1>
+struct TFrag {
+    static constexpr int NK = (R1 + 1) / 2 - R0 / 2;
+    f16x4 h0[NK], l0[NK], h1[NK], l1[NK];
+};
+template <int HS, bool L0, int R0, int R1>
+__device__ __forceinline__ void sb_tread(uint32_t tb, int tau, TFrag<HS, L0, R0, R1> &f) {
+    using I = Img<HS, L0>;
+    constexpr uint32_t TILE = I::TILE, LO = I::HALF;
+    constexpr int K0 = R0 / 2, K1 = (R1 + 1) / 2;
+    uint32_t tbl = tb + LO;
+    asm volatile("" : "+v"(tbl));
+#pragma unroll
+    for (int kbb = K0; kbb < K1; ++kbb) {
+        const uint32_t ct = 8u * (2 * (tau >> 1) + (tau & 1)) + 2 * kbb * TILE;
+        f.h0[kbb - K0] = lds_tr_f16(tb + ct);
+        f.l0[kbb - K0] = lds_tr_f16(tbl + ct);
+        if (2 * kbb + 1 < R1) {
+            f.h1[kbb - K0] = lds_tr_f16(tb + ct + TILE);
+            f.l1[kbb - K0] = lds_tr_f16(tbl + ct + TILE);
+        }
+    }
+}
+template <int HS, bool L0, int R0, int R1>
+__device__ __forceinline__ f32x4 sb_ttile(const TFrag<HS, L0, R0, R1> &f, const f16x8 (&gh)[2], const f16x8 (&gl)[2]) {
+    constexpr int K0 = R0 / 2, K1 = (R1 + 1) / 2;
+    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int kbb = K0; kbb < K1; ++kbb) {
+        const int i = kbb - K0;
+        if (2 * kbb + 1 >= R1) {
+            // half block (its second slot is padding): hi·hi and hi·lo in ONE MFMA, then lo·hi
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 h = __builtin_bit_cast(u32x4, gh[i]), l = __builtin_bit_cast(u32x4, gl[i]);
+            f16x8 a2, al2 = {};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                a2[k] = a2[4 + k] = f.h0[i][k];
+                al2[k] = f.l0[i][k];
+            }
+            acc = mfma16(a2, __builtin_bit_cast(f16x8, u32x4{h[0], h[1], l[0], l[1]}), acc);
+            acc = mfma16(al2, gh[i], acc);
+        } else {
+            f16x8 ah, al;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                ah[k] = f.h0[i][k];
+                ah[4 + k] = f.h1[i][k];
+                al[k] = f.l0[i][k];
+                al[4 + k] = f.l1[i][k];
+            }
+            acc = mma3(ah, al, gh[i], gl[i], acc);
+        }
+    }
+    return acc;
+}
+
+template <int HS>
+struct SbCtx {
+    NextIn nb;                        // this group's slab descriptors
+    f32x4 *dseq_w;                    // this group's dseq
+    __amdgpu_buffer_rsrc_t rr;        // this wave's copy of the window-row gradients
+    f32x4 *red;                       // LDS partial products
+    uint32_t fb1, tb1, fb0, tb0;      // image lane addresses (layers >= 1 / layer 0 geometry)
+    float scq, sc4;
+    int lane, N;
+    Stamps *sp;                       // FCR_STAMP diagnostic builds: [grad, recompute, reduce, cells, total, head+fills]
+    __device__ uint32_t hoff(int j, int l, int t) const {
+        return (uint32_t)(((size_t)(j * kLayers + l) * kL + t) * Geo<HS>::QC * 16);
+    }
+    __device__ size_t doff(int j, int lfrom, int t) const { return ((size_t)(j * 2 + (2 - lfrom)) * kL + t) * Geo<HS>::QC; }
+    __device__ NextIn next_of(int j, int l, int t) const {   // the cell processed after (j, l, t)
+        NextIn n = nb;
+        int nj = j, nl = l, nt = t - 1;
+        if (t == 0) {
+            nt = kL - 1;
+            nl = l - 1;
+            if (l == 0) { nl = 2; nj = j - 1; }
+        }
+        if (nj < 0) { nj = 0; nl = 2; nt = 9; }   // past the last cell: a valid one (harmless)
+        n.x = nl == 0 ? (uint32_t)((nj * kL + nt) * kWave * 8) : hoff(nj, nl > 0 ? nl - 1 : 0, nt);
+        n.h = hoff(nj, nl, nt > 0 ? nt - 1 : 0);
+        n.c = n.h;
+        n.d = (uint32_t)((nl < 2 ? doff(nj, nl + 1, nt) : 0) * 16);
+        return n;
+    }
+};
+
+// inputs of the next A (x_t, h_{t-1}: whole records) and of the next B (c_{t-1}, din: this wave's quad)
+template <int HS, bool NX_L0, bool NX_HC>
+__device__ __forceinline__ void sb_load_a(CellIn<HS> &ci, const NextIn &n, int lane) {
+    load_xhd<HS, NX_L0, NX_HC, false>(ci, n, lane);
+}
+template <int HS, int W, bool NX_HC, bool NX_DIN>
+__device__ __forceinline__ void sb_load_b(CellIn<HS> &ci, const NextIn &n, int lane) {
+    if (NX_HC) ld_quad<HS, W>(ci.c, n.rc, n.c, lane);
+    if (NX_DIN) ld_quad<HS, W>(ci.d, n.rd, n.d, lane);
+}
+
+// One pipeline step of layer LAYER at cell t (t = 9 .. 0), in chunks that pair independent work so the
+// MFMA pipe and the vector ALU overlap (one wave per SIMD: nothing else fills the MFMA shadows):
+//   region 1, per own slot r: A(t-1)'s tile r (DO_A; FA: cell t-1 is the first) beside B(t)'s cell gradient
+//             of slot r (FB: t = 0), the dgate split after each slot pair;
+//   region 2, per output tile: B(t)'s transposed products beside a share of the operand split of A(t-2)
+//             (DO_S; FS: t-2 = 0);
+//   then the reduction of cell t and this wave's stores. Loads: B's next inputs (c, din of the cell after
+//   t) after region 1, A's (x, h of the cell after t-2) after region 2 — a step ahead of their use.
+template <int HS, int LAYER, int W, bool FB, bool DO_A, bool FA, bool DO_S, bool FS, bool S_NX_L0, bool S_NX_HC,
+          bool B_NX_HC, bool B_NX_DIN>
+__device__ __forceinline__ void sb_step(const SbCtx<HS> &x, int j, int t, const float (&ext)[HS], CellIn<HS> &ci,
+                                        f32x4 (&G)[4], AOps<HS, LAYER == 0> &ops, float (&dh)[HS], float (&dc)[HS]) {
+    using Q = QR<HS, W>;
+    constexpr int R0 = Q::R0, R1 = Q::R1, NS = R1 - R0;
+    constexpr bool L0 = LAYER == 0, DIN = LAYER < 2;
+    constexpr int NB = Img<HS, L0>::NB;
+    const uint32_t fb = L0 ? x.fb0 : x.fb1, tb = L0 ? x.tb0 : x.tb1;
+    const unsigned long long s0 = stamp_now();
+    // ---- region 1 ----
+    sched_fence();
+    AFrag<HS, L0> fa[2];
+    if constexpr (DO_A) sb_aread<HS, L0, FA>(fb, R0, fa[0]);
+    const BScale sc = sb_scale<HS, DIN, R0, R1>(ci, ext, dh, dc);
+    f32x4 Gn[4];
+    f16x8 gh[2], gl[2];
+    float va[8], vb[8];
+#pragma unroll
+    for (int u = 0; u < NS; ++u) {
+        sched_fence();
+        if constexpr (DO_A) {
+            if (u + 1 < NS) sb_aread<HS, L0, FA>(fb, R0 + u + 1, fa[(u + 1) & 1]);
+            Gn[u] = sb_atile<HS, L0, FA>(fa[u & 1], ops);
+        }
+        sb_slot<HS, FB>(R0 + u, G[u], ci, sc, dh, dc, va + 4 * (u & 1), vb + 4 * (u & 1));
+        if ((u & 1) || u + 1 == NS) {
+            if (!(u & 1)) {
+#pragma unroll
+                for (int k = 4; k < 8; ++k) va[k] = vb[k] = 0.0f;
+            }
+            split8p(va, vb, gh[u >> 1], gl[u >> 1]);
+        }
+    }
+    sched_fence();
+    sb_load_b<HS, W, B_NX_HC, B_NX_DIN>(ci, x.next_of(j, LAYER, t), x.lane);
+    const unsigned long long s1 = stamp_now();
+    // ---- region 2 ----
+    TFrag<HS, L0, R0, R1> tf[2];
+    sb_tread<HS, L0, R0, R1>(tb, 0, tf[0]);
+    f32x4 acc[Small<HS>::NB];
+    // A(t-2)'s operand split spread over the output tiles: k-block kb goes with tile tau = kb * NB / KB
+    using AR = ARange<HS, L0, FS>;
+    float xv[HS], hv[HS];
+#pragma unroll
+    for (int s = 0; s < HS; ++s) {
+        xv[s] = L0 ? 0.0f : ci.x[s >> 2][s & 3];
+        hv[s] = FS ? 0.0f : ci.h[s >> 2][s & 3];
+    }
+    const float x0 = ci.x[0][0], x1 = ci.x[0][1];
+#pragma unroll
+    for (int tau = 0; tau < NB; ++tau) {
+        sched_fence();
+        if (tau + 1 < NB) sb_tread<HS, L0, R0, R1>(tb, tau + 1, tf[(tau + 1) & 1]);
+        acc[tau] = sb_ttile<HS, L0, R0, R1>(tf[tau & 1], gh, gl);
+        if constexpr (DO_S) {
+#pragma unroll
+            for (int kb = 0; kb < AR::KB; ++kb) {
+                if (kb * NB / AR::KB != tau) continue;
+                if (kb >= AR::KLO && kb < AR::KHI) fwd_operand<HS, L0, FS, false>(kb, x0, x1, xv, hv, ops.bh[kb], ops.bl[kb]);
+                else ops.bh[kb] = ops.bl[kb] = f16x8{};
+                if (AR::TAIL && AR::KHI == AR::KB && kb == AR::KB - 1)
+                    ops.bh[kb] = tail_operand<false>(ops.bh[kb], ops.bl[kb]);
+            }
+        }
+    }
+    sched_fence();
+    if constexpr (DO_S) sb_load_a<HS, S_NX_L0, S_NX_HC>(ci, x.next_of(j, LAYER, t - 2), x.lane);
+    if constexpr (DO_A) {
+#pragma unroll
+        for (int r = 0; r < NS; ++r) G[r] = Gn[r];
+    }
+    const unsigned long long s2 = stamp_now();
+    f32x4 part[Small<HS>::NB];
+#pragma unroll
+    for (int tau = 0; tau < NB; ++tau) part[tau] = acc[tau] * sc.down;
+    float dxo[HS], dxq = 0.0f, dx4 = 0.0f;
+    small_reduce<HS, L0, W>(x.red, part, x.lane, dh, dxo, dxq, dx4);
+    if (FCR_STAMP) {
+        const unsigned long long s3 = stamp_now();
+        x.sp->t[0] += s1 - s0;
+        x.sp->t[1] += s2 - s1;
+        x.sp->t[2] += s3 - s2;
+        x.sp->t[3] += 1;
+    }
+    if (L0) buf_st2(x.rr, x.lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{dxq * x.scq, dx4 * x.sc4});   // row j+t
+    else store_quad<HS, W>(x.dseq_w + x.doff(j, LAYER, t), dxo, x.lane);
+}
+
+template <int HS, int LAYER, int W>
+__device__ __forceinline__ void sb_phase(const SbCtx<HS> &x, int j, const float (&dh_out)[HS], CellIn<HS> &ci,
+                                         float (&dh)[HS], float (&dc)[HS]) {
+    using Q = QR<HS, W>;
+    constexpr bool L0 = LAYER == 0, DIN = LAYER < 2;
+    constexpr bool NEXT_L0 = LAYER == 1, NEXT_DIN = LAYER >= 1;   // the next phase's first cell
+    float zero[HS];
+#pragma unroll
+    for (int r = 0; r < HS; ++r) zero[r] = 0.0f;
+#pragma unroll
+    for (int r = Q::R0; r < Q::R1; ++r) dh[r] = dc[r] = 0.0f;
+    const unsigned long long p0 = stamp_now();
+    // prologue: A(9), and A(8)'s operands (ci holds cell 9's x, h on entry)
+    AOps<HS, L0> ops;
+    f32x4 G[4];
+    sb_split<HS, L0, false>(ci, ops);
+    sb_load_a<HS, L0, true>(ci, x.next_of(j, LAYER, kL - 1), x.lane);
+#pragma unroll
+    for (int r = Q::R0; r < Q::R1; ++r) {
+        AFrag<HS, L0> f;
+        sb_aread<HS, L0, false>(L0 ? x.fb0 : x.fb1, r, f);
+        G[r - Q::R0] = sb_atile<HS, L0, false>(f, ops);
+    }
+    sb_split<HS, L0, false>(ci, ops);
+    sb_load_a<HS, L0, true>(ci, x.next_of(j, LAYER, kL - 2), x.lane);
+    if (FCR_STAMP) x.sp->t[6] += stamp_now() - p0;
+    //      <HS, LAYER, W, FB,   DO_A, FA,   DO_S, FS,   S_NX_L0, S_NX_HC, B_NX_HC, B_NX_DIN>
+    sb_step<HS, LAYER, W, false, true, false, true, false, L0, true, true, DIN>(x, j, kL - 1, LAYER == 2 ? dh_out : zero, ci,
+                                                                             G, ops, dh, dc);
+    for (int t = kL - 2; t >= 4; --t)
+        sb_step<HS, LAYER, W, false, true, false, true, false, L0, true, true, DIN>(x, j, t, zero, ci, G, ops, dh, dc);
+    sb_step<HS, LAYER, W, false, true, false, true, false, L0, false, true, DIN>(x, j, 3, zero, ci, G, ops, dh, dc);
+    sb_step<HS, LAYER, W, false, true, false, true, true, NEXT_L0, true, true, DIN>(x, j, 2, zero, ci, G, ops, dh, dc);
+    sb_step<HS, LAYER, W, false, true, true, false, false, false, false, false, DIN>(x, j, 1, zero, ci, G, ops, dh, dc);
+    sb_step<HS, LAYER, W, true, false, false, false, false, false, false, true, NEXT_DIN>(x, j, 0, zero, ci, G, ops, dh, dc);
 }
 
 template <int HS>
@@ -346,7 +715,6 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sbwd_kernel(BwdA
     extern __shared__ __attribute__((aligned(16))) float lw[];
     float *lfnp = lw + LD::REGION / 4;
     float *lfcp = lfnp + LD::FNP;
-    f32x4 *red = reinterpret_cast<f32x4 *>(lw + LD::BYTES / 4);
     lds_copy(lfnp, a.p.fnp, LD::FNP);
     lds_copy(lfcp, a.p.fcp, LD::FCP);
     __syncthreads();
@@ -362,66 +730,63 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sbwd_kernel(BwdA
     const float alpha = a.alpha;
     const float wgt = valid ? a.dloss[0] / ((float)a.B * (float)N) : 0.0f;   // Functions.py:1458, 1463
     const float ref = a.X[(size_t)bc * kCtrlIn + 2];
-    const float scq = a.p.wsc[q], sc4 = a.p.wsc[4];
     const float s84 = a.states[(size_t)bc * kL * kIn + (kL - 2) * kIn + 4];
     const float *pred = a.prediction + (size_t)bc * N;
     const float *xh = a.xhat + (size_t)bc * N * kOut;
-    const ImgLane<I1::U> L1 = img_lane<I1::U>(lds_offset(lw), lane);
-    const ImgLane<I0::U> L0 = img_lane<I0::U>(lds_offset(lw), lane);
 
+    SbCtx<HS> x;
+    {
+        const ImgLane<I1::U> L1 = img_lane<I1::U>(lds_offset(lw), lane);
+        const ImgLane<I0::U> L0 = img_lane<I0::U>(lds_offset(lw), lane);
+        x.fb1 = L1.fb;
+        x.tb1 = L1.tb;
+        x.fb0 = L0.fb;
+        x.tb0 = L0.tb;
+    }
+    x.lane = lane;
+    x.N = N;
+    Stamps sp = {{0, 0, 0, 0, 0, 0, 0, 0}};
+    x.sp = &sp;
+    const unsigned long long tk0 = stamp_now();
+    x.scq = a.p.wsc[q];
+    x.sc4 = a.p.wsc[4];
+    x.red = reinterpret_cast<f32x4 *>(lw + LD::BYTES / 4);
     // this wave's own copy of the window-row gradients (dxrow holds NQ copies per group)
-    const __amdgpu_buffer_rsrc_t rr =
-        wave_rsrc(a.dxrow + ((size_t)grp * NQ + w) * N * kL * kWave, (size_t)N * kL * kWave * 8);
-    auto row_grad = [&](int rho) {
-        f32x2 acc2 = {0.0f, 0.0f};
-        const int w_hi = rho < N - 1 ? rho : N - 1;
-        const int w_lo = rho - (kL - 1) > 0 ? rho - (kL - 1) : 0;
-        for (int v = w_hi; v >= w_lo; --v) acc2 += buf_ld2(rr, lane * 8, (uint32_t)((v * kL + (rho - v)) * kWave * 8));
-        return acc2;
-    };
-    float dh[HS], dc[HS], dxo[HS], dab[HS];
-#pragma unroll
-    for (int r = 0; r < HS; ++r) dh[r] = dc[r] = dxo[r] = dab[r] = 0.0f;
-
+    x.rr = wave_rsrc(a.dxrow + ((size_t)grp * NQ + w) * N * kL * kWave, (size_t)N * kL * kWave * 8);
     const size_t qcell = (size_t)Geo<HS>::QC;
     const size_t seq_sz = (size_t)N * kLayers * kL * qcell;
     const size_t dseq_sz = (size_t)N * 2 * kL * qcell;
-    NextIn nb;
-    nb.rh = wave_rsrc(a.hseq + (size_t)grp * seq_sz, seq_sz * 16);
-    nb.rc = wave_rsrc(a.cseq + (size_t)grp * seq_sz, seq_sz * 16);
-    nb.rx = wave_rsrc(a.xw + (size_t)grp * N * kL * kWave, (size_t)N * kL * kWave * 8);
-    nb.rd = wave_rsrc(a.dseq + (size_t)grp * dseq_sz, dseq_sz * 16);
-    f32x4 *dseq_w = a.dseq + (size_t)grp * dseq_sz;
-    auto hoff = [&](int j, int l, int t) { return (uint32_t)(((size_t)(j * kLayers + l) * kL + t) * qcell * 16); };
-    auto doff = [&](int j, int lfrom, int t) { return ((size_t)(j * 2 + (2 - lfrom)) * kL + t) * qcell; };
-    auto next_of = [&](int j, int l, int t) {   // the cell processed after (j, l, t)
-        NextIn n = nb;
-        int nj = j, nl = l, nt = t - 1;
-        if (t == 0) {
-            nt = kL - 1;
-            nl = l - 1;
-            if (l == 0) { nl = 2; nj = j - 1; }
-        }
-        if (nj < 0) { nj = 0; nl = 2; nt = 9; }
-        n.x = nl == 0 ? (uint32_t)((nj * kL + nt) * kWave * 8) : hoff(nj, nl > 0 ? nl - 1 : 0, nt);
-        n.h = hoff(nj, nl, nt > 0 ? nt - 1 : 0);
-        n.c = n.h;
-        n.d = (uint32_t)((nl < 2 ? doff(nj, nl + 1, nt) : 0) * 16);
-        return n;
+    x.nb.rh = wave_rsrc(a.hseq + (size_t)grp * seq_sz, seq_sz * 16);
+    x.nb.rc = wave_rsrc(a.cseq + (size_t)grp * seq_sz, seq_sz * 16);
+    x.nb.rx = wave_rsrc(a.xw + (size_t)grp * N * kL * kWave, (size_t)N * kL * kWave * 8);
+    x.nb.rd = wave_rsrc(a.dseq + (size_t)grp * dseq_sz, dseq_sz * 16);
+    x.dseq_w = a.dseq + (size_t)grp * dseq_sz;
+    auto row_grad = [&](int rho) {   // sum over windows v = max(0, rho-9) .. min(N-1, rho) of dx(v, rho-v)
+        f32x2 acc2 = {0.0f, 0.0f};
+        const int w_hi = rho < N - 1 ? rho : N - 1;
+        const int w_lo = rho - (kL - 1) > 0 ? rho - (kL - 1) : 0;
+        for (int v = w_hi; v >= w_lo; --v) acc2 += buf_ld2(x.rr, lane * 8, (uint32_t)((v * kL + (rho - v)) * kWave * 8));
+        return acc2;
     };
-    Stamps sp = {{0, 0, 0, 0, 0, 0, 0, 0}};
+    float dh[HS], dc[HS];
+#pragma unroll
+    for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
     CellIn<HS> ci;
     {
-        const NextIn f = next_of(N - 1, 2, kL);
-        load_xhd<HS, false, true, false>(ci, f, lane);
-        ld_quads<HS>(ci.c, f.rc, f.c, lane);
+        const NextIn f = x.next_of(N - 1, 2, kL);   // t = kL -> (N-1, 2, 9)
+        by_quad<HS>(w, [&](auto Wc) {
+            constexpr int W = decltype(Wc)::v;
+            sb_load_a<HS, false, true>(ci, f, lane);
+            sb_load_b<HS, W, true, false>(ci, f, lane);
+        });
     }
-    float dxq = 0.0f, dx4 = 0.0f;
 
     for (int j = N - 1; j >= 0; --j) {
         const float *lfnp_j = opaque(lfnp), *lfcp_j = opaque(lfcp);
-        // layer 2's image; the barriers also order the previous window's row-gradient stores
-        lds_fill<I1::BYTES, NQ>(lw, a.p.img[2]);
+        // layer 2's image (the barriers also retire layer 0's reads of the previous window)
+        const unsigned long long th0 = stamp_now();
+        small_fill<I1::BYTES, NQ>(lw, a.p.img[2]);
+        const unsigned long long th1 = stamp_now();
         const float x0 = xh[j * kOut + 0], x1 = xh[j * kOut + 1], x2 = xh[j * kOut + 2], x3 = xh[j * kOut + 3];
         float d0 = wgt * 2.0f * (x0 - ref);                             // Functions.py:1443-1452
         float d1 = wgt * ((-x1 > 0.0f ? -1.0f : 0.0f) + (x1 - kP1Max > 0.0f ? 1.0f : 0.0f));
@@ -461,47 +826,30 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sbwd_kernel(BwdA
             const float *fp = lfcp_j + r * 4 + q;
             dh_out[r] = fp[0] * d0 + fp[HS * 4] * d1 + fp[2 * HS * 4] * d2 + fp[3 * HS * 4] * d3;
         }
-        // ---- layer 2 ----
-#pragma unroll
-        for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
-        for (int t = kL - 1; t >= 2; --t) {
-#pragma unroll
-            for (int r = 0; r < HS; ++r) dab[r] = (t == kL - 1) ? dh_out[r] : 0.0f;
-            sbwd_cell<HS, false, false, false, false, true, false>(w, L1.fb, L1.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
-                                                                   next_of(j, 2, t), sp, red, dseq_w + doff(j, 2, t));
+        const unsigned long long th2 = stamp_now();
+        by_quad<HS>(w, [&](auto Wc) { sb_phase<HS, 2, decltype(Wc)::v>(x, j, dh_out, ci, dh, dc); });
+        const unsigned long long tf0 = stamp_now();
+        small_fill<I1::BYTES, NQ>(lw, a.p.img[1]);
+        const unsigned long long tf1 = stamp_now();
+        by_quad<HS>(w, [&](auto Wc) { sb_phase<HS, 1, decltype(Wc)::v>(x, j, dh_out, ci, dh, dc); });
+        const unsigned long long tf2 = stamp_now();
+        small_fill<I0::BYTES, NQ>(lw, a.p.img[0]);
+        if (FCR_STAMP) {
+            sp.t[5] += (th1 - th0) + (tf1 - tf0) + (stamp_now() - tf2);   // three refills
+            sp.t[7] += th2 - th1;                                         // window head
         }
-#pragma unroll
-        for (int r = 0; r < HS; ++r) dab[r] = 0.0f;
-        sbwd_cell<HS, false, false, false, false, false, false>(w, L1.fb, L1.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
-                                                                next_of(j, 2, 1), sp, red, dseq_w + doff(j, 2, 1));
-        sbwd_cell<HS, false, false, true, false, true, true>(w, L1.fb, L1.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
-                                                             next_of(j, 2, 0), sp, red, dseq_w + doff(j, 2, 0));
-        // ---- layer 1 ----
-        lds_fill<I1::BYTES, NQ>(lw, a.p.img[1]);
-#pragma unroll
-        for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
-        for (int t = kL - 1; t >= 2; --t)
-            sbwd_cell<HS, false, true, false, false, true, true>(w, L1.fb, L1.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
-                                                                 next_of(j, 1, t), sp, red, dseq_w + doff(j, 1, t));
-        sbwd_cell<HS, false, true, false, false, false, true>(w, L1.fb, L1.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
-                                                              next_of(j, 1, 1), sp, red, dseq_w + doff(j, 1, 1));
-        sbwd_cell<HS, false, true, true, true, true, true>(w, L1.fb, L1.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
-                                                           next_of(j, 1, 0), sp, red, dseq_w + doff(j, 1, 0));
-        // ---- layer 0: dx -> window-row gradients (this wave's copy) ----
-        lds_fill<I0::BYTES, NQ>(lw, a.p.img[0]);
-#pragma unroll
-        for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
-        for (int t = kL - 1; t >= 2; --t) {
-            sbwd_cell<HS, true, true, false, true, true, true>(w, L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
-                                                               next_of(j, 0, t), sp, red, nullptr);
-            buf_st2(rr, lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{dxq * scq, dx4 * sc4});   // row j+t
-        }
-        sbwd_cell<HS, true, true, false, true, false, true>(w, L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
-                                                            next_of(j, 0, 1), sp, red, nullptr);
-        buf_st2(rr, lane * 8, (uint32_t)((j * kL + 1) * kWave * 8), f32x2{dxq * scq, dx4 * sc4});       // row j+1
-        sbwd_cell<HS, true, true, true, false, true, false>(w, L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
-                                                            next_of(j, 0, 0), sp, red, nullptr);
-        buf_st2(rr, lane * 8, (uint32_t)((j * kL) * kWave * 8), f32x2{dxq * scq, dx4 * sc4});           // row j
+        by_quad<HS>(w, [&](auto Wc) { sb_phase<HS, 0, decltype(Wc)::v>(x, j, dh_out, ci, dh, dc); });
+    }
+    if (FCR_STAMP && lane == 0) {   // diagnostic builds: per (group, wave) cycle sums
+        unsigned long long *o = a.stamp + ((size_t)grp * NQ + w) * 8;
+        o[0] = sp.t[0];
+        o[1] = sp.t[1];
+        o[2] = sp.t[2];
+        o[3] = sp.t[3];
+        o[4] = stamp_now() - tk0;
+        o[5] = sp.t[5];
+        o[6] = sp.t[6];
+        o[7] = sp.t[7];
     }
     const float g_u0_rows = row_grad(kL - 1)[1];   // row 9, col 4 = u0 (Functions.py:1396)
     float du0 = 2.0f * alpha * wgt * (pred[0] - s84);
