@@ -4,7 +4,7 @@
 //
 // Recompute, not store: each cell rebuilds its gate pre-activations from (x_t, h_{t-1}, c_{t-1}) —
 // the forward kept h and c (8 B per unit slot) — with the very products and pointwise arithmetic of
-// the forward kernel (fwd_operand, mma3 in the same k order, lstm_point_grad), and feeds the local
+// the forward kernel (rec_operand on the stored split records, mma3 in the same k order, lstm_point_grad), and feeds the local
 // derivatives straight into the gradient product [dx ; dh_prev] = Wᵀ·dgates. Both products read the
 // same LDS image: row reads for W·[x;h], ds_read_b64_tr_b16 for Wᵀ·dgates. Against storing the
 // derivatives (24 B per slot written by the forward, read here), this halves the HBM traffic of
@@ -20,8 +20,8 @@ namespace fcr {
 // cell right after this cell consumed it (x, h_{t-1}, din at the top, c_{t-1} quad by quad).
 template <int HS>
 struct CellIn {
-    f32x4 x[Geo<HS>::HQ];   // layer >= 1: layer-below h_t; layer 0: x[0] = (column q, column 4, -, -)
-    f32x4 h[Geo<HS>::HQ];   // h_{t-1}
+    f32x4 x[Geo<HS>::HQ];   // layer >= 1: split record of the layer-below h_t; layer 0: x[0] = (column q, column 4, -, -)
+    f32x4 h[Geo<HS>::HQ];   // split record of h_{t-1} (fcr_f16.h)
     f32x4 c[Geo<HS>::HQ];   // c_{t-1}
     f32x4 d[Geo<HS>::HQ];   // din = dx of the layer above at t (layers 0, 1)
 };
@@ -131,7 +131,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
         }
         const float x0 = ci.x[0][0], x1 = ci.x[0][1];
 #pragma unroll
-        for (int kb = KLO; kb < KHI; ++kb) fwd_operand<HS, L0, FIRST, LP>(kb, x0, x1, xv, hv, bh[kb], bl[kb]);
+        for (int kb = KLO; kb < KHI; ++kb) rec_operand<HS, L0, FIRST, LP>(kb, x0, x1, xv, hv, bh[kb], bl[kb]);
         if (TAIL && KHI == KB) bh[KB - 1] = tail_operand<LP>(bh[KB - 1], bl[KB - 1]);
     }
 

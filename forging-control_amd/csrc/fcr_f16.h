@@ -113,6 +113,10 @@ __device__ __forceinline__ void split8(const float (&v)[8], f16x8 &hi, f16x8 &lo
 __device__ __forceinline__ void split8s(const float (&v)[8], float s, f16x8 &hi, f16x8 &lo) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     u32x4 h, l;
+#if !FCR_MIX_ASM
+    // a constant s = 1 would fold the fma away and lose the v_fma_mix form (cvt/sub/cvt instead)
+    asm("" : "+v"(s));
+#endif
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         unsigned hp, lp;
@@ -241,6 +245,101 @@ __device__ __forceinline__ void fwd_operand(int kb, float x0, float x1, const fl
         v[j] = e;
     }
     split_p<LP>(v, 1.0f, bh, bl);
+}
+
+// ---- split records ----
+// A cell's h leaves the cell already split into the f16 halves every consumer multiplies with (the next
+// cell's h_{t-1}, the layer above's x_t, the backward's recompute of both): its record (the compact slab
+// record of fcr_common.h, HS 32-bit values per lane) holds the half array [hi(slot 0..HS-1) | lo(slot
+// 0..HS-1)], hi = f16(h), lo = f16(h - hi), dword d = halves 2d (low) and 2d+1 (high). The B operands are
+// then assembled from record dwords with alignbit / perm (compile-time selects) instead of re-splitting fp32
+// values — the same halves, so the products are bit for bit those of a split at the consumer.
+template <int HS>
+__device__ __forceinline__ void split_rec(const float (&h)[HS], float (&r)[HS]) {
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    float one = 1.0f;
+    asm("" : "+v"(one));   // keeps the v_fma_mix form (a constant 1 folds the fma away)
+    _Float16 hh[HS], ll[HS];
+#pragma unroll
+    for (int k = 0; k < HS; ++k) {
+        hh[k] = (_Float16)__builtin_fmaf(h[k], one, 0.0f);
+        ll[k] = (_Float16)__builtin_fmaf(h[k], one, -(float)hh[k]);
+    }
+#pragma unroll
+    for (int d = 0; d < HS; ++d) {
+        f16x2 v;
+        v[0] = 2 * d < HS ? hh[2 * d < HS ? 2 * d : 0] : ll[2 * d >= HS ? 2 * d - HS : 0];
+        v[1] = 2 * d + 1 < HS ? hh[2 * d + 1 < HS ? 2 * d + 1 : 0] : ll[2 * d + 1 >= HS ? 2 * d + 1 - HS : 0];
+        r[d] = __builtin_bit_cast(float, v);
+    }
+}
+
+// One 32-bit word of an operand from two halves, each (source, half index) with the source a record
+// (1: x record, 2: h record) or the on-the-fly split window pair (3: hi pair, 4: lo pair), 0 = zero.
+// Compile-time arguments: one alignbit or perm (or a plain register) per word.
+struct HalfRef {
+    int src, k;
+};
+template <int HS>
+__device__ __forceinline__ uint32_t rec_word(HalfRef a, HalfRef b, const float (&xr)[HS], const float (&hr)[HS],
+                                             uint32_t wh, uint32_t wl) {
+    auto dw = [&](HalfRef h) -> uint32_t {
+        if (h.src == 1) return __builtin_bit_cast(uint32_t, xr[h.k >> 1]);
+        if (h.src == 2) return __builtin_bit_cast(uint32_t, hr[h.k >> 1]);
+        return h.src == 3 ? wh : wl;
+    };
+    if (a.src == 0 && b.src == 0) return 0u;
+    if (b.src == 0) return (a.k & 1) ? dw(a) >> 16 : dw(a) & 0xffffu;
+    if (a.src == 0) return (b.k & 1) ? dw(b) & 0xffff0000u : dw(b) << 16;
+    if (a.src == b.src && (b.k >> 1) == (a.k >> 1) && (a.k & 1) == 0 && (b.k & 1) == 1) return dw(a);
+    if (a.src == b.src && (a.k & 1) == 1 && b.k == a.k + 1) return __builtin_amdgcn_alignbit(dw(b), dw(a), 16);
+    // perm: bytes 0-3 select from the second source, 4-7 from the first
+    const uint32_t sel = (uint32_t)(2 * (a.k & 1)) | (uint32_t)(2 * (a.k & 1) + 1) << 8 | (uint32_t)(4 + 2 * (b.k & 1)) << 16 |
+                         (uint32_t)(5 + 2 * (b.k & 1)) << 24;
+    return __builtin_amdgcn_perm(dw(b), dw(a), sel);
+}
+
+// B operand (8 combined slots of k-block kb) of a cell from the split records: layer >= 1 — x record (the
+// layer below's h_t, σ < HS) and h record (h_{t-1}, σ - HS); layer 0 — h record (σ < HS) and the window
+// columns x0 (σ = HS), x1 (σ = HS + 1), split here. FIRST: h_{t-1} = 0. Identical in the forward kernels
+// and the backward's recomputation.
+template <int HS, bool L0, bool FIRST, bool LP>
+__device__ __forceinline__ void rec_operand(int kb, float x0, float x1, const float (&xr)[HS], const float (&hr)[HS],
+                                            f16x8 &bh, f16x8 &bl) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    uint32_t wh = 0u, wl = 0u;
+    if (L0 && 8 * kb <= HS + 1 && HS < 8 * kb + 8) {   // the window columns fall in this block
+        float one = 1.0f;
+        asm("" : "+v"(one));
+        f16x2 h, l;
+        h[0] = (_Float16)__builtin_fmaf(x0, one, 0.0f);
+        h[1] = (_Float16)__builtin_fmaf(x1, one, 0.0f);
+        l[0] = (_Float16)__builtin_fmaf(x0, one, -(float)h[0]);
+        l[1] = (_Float16)__builtin_fmaf(x1, one, -(float)h[1]);
+        wh = __builtin_bit_cast(uint32_t, h);
+        wl = __builtin_bit_cast(uint32_t, l);
+    }
+    auto ref = [&](int sg, bool lo) -> HalfRef {
+        if (L0) {
+            if (sg < HS) return FIRST ? HalfRef{0, 0} : HalfRef{2, lo ? HS + sg : sg};
+            if (sg == HS) return HalfRef{lo ? 4 : 3, 0};
+            if (sg == HS + 1) return HalfRef{lo ? 4 : 3, 1};
+            return HalfRef{0, 0};
+        }
+        if (sg < HS) return HalfRef{1, lo ? HS + sg : sg};
+        if (sg < 2 * HS) return FIRST ? HalfRef{0, 0} : HalfRef{2, lo ? sg : sg - HS};
+        return HalfRef{0, 0};
+    };
+    u32x4 H, L;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int s0 = 8 * kb + 2 * p;
+        H[p] = rec_word<HS>(ref(s0, false), ref(s0 + 1, false), xr, hr, wh, wl);
+        L[p] = LP ? 0u : rec_word<HS>(ref(s0, true), ref(s0 + 1, true), xr, hr, wh, wl);
+    }
+    bh = __builtin_bit_cast(f16x8, H);
+    bl = __builtin_bit_cast(f16x8, L);
 }
 
 // Cell update of one unit slot from its pre-activations a = (i, f, g, o), pre-scaled for exp2 (the

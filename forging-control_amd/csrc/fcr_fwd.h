@@ -22,7 +22,8 @@ __device__ __forceinline__ void rot_left(float (&w)[kL]) {
 
 // One LSTM cell for 16 trajectories on the f16 matrix cores (fcr_f16.h): fragments
 // [r][kb][hi|lo][lane][8 halves]. L0: input is the window row (x0: column q in lane group q, x1:
-// column 4 in lane group 0); otherwise x = the layer-below h_t. FIRST: t = 0 (h_{t-1} = 0: those
+// column 4 in lane group 0); otherwise x = the split record of the layer-below h_t. hp = the split
+// record of h_{t-1} (fcr_f16.h, split_rec); hout = this cell's h (fp32). FIRST: t = 0 (h_{t-1} = 0: those
 // k-blocks are skipped). The B operands are split once per cell and shared by all tiles. Tiles go in
 // pairs, each with two accumulators over alternate k-blocks: four independent MFMA chains per
 // scheduling region (one region per k-block, the next block's four fragment reads in flight), and the
@@ -82,7 +83,7 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
     constexpr int KT = TAIL ? KB - 1 : KB;   // lo fragments per tile
     f16x8 bh[KB], bl[KB] = {};
 #pragma unroll
-    for (int kb = KLO; kb < KHI; ++kb) fwd_operand<HS, L0, FIRST, LP>(kb, x0, x1, x, hp, bh[kb], bl[kb]);
+    for (int kb = KLO; kb < KHI; ++kb) rec_operand<HS, L0, FIRST, LP>(kb, x0, x1, x, hp, bh[kb], bl[kb]);
     if (TAIL && KHI == KB) bh[KB - 1] = tail_operand<LP>(bh[KB - 1], bl[KB - 1]);
     // fragment reads of (tile r, block kb): hi, lo
     auto rd = [&](int r, int kb, f16x8 &h, f16x8 &l) {   // split-major fragments (pack_fwd16_kernel)
@@ -218,9 +219,9 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
     float cmd_sum = 0.0f, err_sum = 0.0f, tot_sum = 0.0f;
     float xh0 = 0.0f, xh1 = 0.0f, xh2 = 0.0f, xh3 = 0.0f;
 
-    float c[HS], hout[HS], hp[HS], xc[HS], xn[HS];
-    // sequence slabs [wave][j][layer][t][quad][64]: h of every cell (layers 0, 1: the next phase's
-    // input; with STORE also layer 2) and, with STORE, c; plus the window rows [wave][j][t][64]
+    float c[HS], hout[HS], hp[HS], xc[HS], xn[HS];   // hp, xc, xn: split records (fcr_f16.h)
+    // sequence slabs [wave][j][layer][t][quad][64]: the split record of h of every cell (layers 0, 1: the
+    // next phase's input; with STORE also layer 2) and, with STORE, c; plus the window rows [wave][j][t][64]
     const size_t qcell = (size_t)Geo<HS>::QC;    // one cell of a sequence slab, in 16-B units
     const size_t wseq = (size_t)wave * N * kLayers * kL * qcell;
     f32x4 *hs_wave = a.hseq + wseq;
@@ -278,26 +279,24 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             rot_left(w0);
             rot_left(w1);
             fwd16_cell<HS, true, true, LP>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
-            store_quads<HS>(SEQ_H(0, 0), hout, lane);
+            split_rec<HS>(hout, hp);
+            store_quads<HS>(SEQ_H(0, 0), hp, lane);
             if (STORE) {
                 if (FCR_ABLATE != 3) xw_wave[(size_t)j * kL * kWave + lane] = f32x2{x0, x1};
                 store_quads<HS>(SEQ_C(0, 0), c, lane);
             }
-#pragma unroll
-            for (int r = 0; r < HS; ++r) hp[r] = hout[r];
         }
         for (int t = 1; t < kL; ++t) {
             const float x0 = w0[0], x1 = w1[0];
             rot_left(w0);
             rot_left(w1);
             fwd16_cell<HS, true, false, LP>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
-            store_quads<HS>(SEQ_H(0, t), hout, lane);
+            split_rec<HS>(hout, hp);
+            store_quads<HS>(SEQ_H(0, t), hp, lane);
             if (STORE) {
                 if (FCR_ABLATE != 3) xw_wave[((size_t)j * kL + t) * kWave + lane] = f32x2{x0, x1};
                 if (t + 1 < kL) store_quads<HS>(SEQ_C(0, t), c, lane);   // c_9 is never a c_{t-1}
             }
-#pragma unroll
-            for (int r = 0; r < HS; ++r) hp[r] = hout[r];
         }
         // ---- layers 1, 2: input sequence streamed back from the slab, one cell ahead ----
 #pragma unroll
@@ -336,23 +335,21 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             load_quads<HS>(xc, SEQ_H(l - 1, 0), lane);
             load_quads<HS>(xn, SEQ_H(l - 1, 1), lane);
             fwd16_cell<HS, false, true, LP>(lwc, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
-            if (keep_h) store_quads<HS>(SEQ_H(l, 0), hout, lane);
+            split_rec<HS>(hout, hp);
+            if (keep_h) store_quads<HS>(SEQ_H(l, 0), hp, lane);
             if (STORE) store_quads<HS>(SEQ_C(l, 0), c, lane);
 #pragma unroll
-            for (int r = 0; r < HS; ++r) {
-                hp[r] = hout[r];
-                xc[r] = xn[r];
-            }
+            for (int r = 0; r < HS; ++r) xc[r] = xn[r];
             for (int t = 1; t < kL; ++t) {
                 load_quads<HS>(xn, SEQ_H(l - 1, t + 1 < kL ? t + 1 : t), lane);
                 fwd16_cell<HS, false, false, LP>(lwc, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
-                if (keep_h && !(l == 2 && t + 1 == kL)) store_quads<HS>(SEQ_H(l, t), hout, lane);
+                if (!(l == 2 && t + 1 == kL)) {   // h_9 of layer 2 only feeds the readout (fp32 hout)
+                    split_rec<HS>(hout, hp);
+                    if (keep_h) store_quads<HS>(SEQ_H(l, t), hp, lane);
+                }
                 if (STORE && t + 1 < kL) store_quads<HS>(SEQ_C(l, t), c, lane);
 #pragma unroll
-                for (int r = 0; r < HS; ++r) {
-                    hp[r] = hout[r];
-                    xc[r] = xn[r];
-                }
+                for (int r = 0; r < HS; ++r) xc[r] = xn[r];
             }
         }
 #undef SEQ_H
@@ -363,7 +360,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
         for (int o = 0; o < kOut; ++o) {
             float p = 0.0f;
 #pragma unroll
-            for (int r = 0; r < HS; ++r) p += lfcp_j[(o * HS + r) * 4 + q] * hp[r];
+            for (int r = 0; r < HS; ++r) p += lfcp_j[(o * HS + r) * 4 + q] * hout[r];
             xo[o] = xor_sum_q(p) + lfcb_j[o];
         }
         if (a.noise) {                                                 // Functions.py:1400-1402

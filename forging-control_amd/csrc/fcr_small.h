@@ -25,12 +25,13 @@ namespace fcr {
 template <int HS>
 struct Small {
     static constexpr int NQ = (HS + 3) / 4;                       // waves per workgroup = record quads
-    static constexpr int XBUF = 2 * NQ * kWave * 16;              // h exchange, double-buffered
+    static constexpr int XBUF = 2 * NQ * kWave * 16;              // h exchange (split record), double-buffered
     static constexpr int LDS_FWD = Geo16<HS>::LDS_FWD + XBUF;
     static constexpr int NB = Img<HS, false>::NB > Img<HS, true>::NB ? Img<HS, false>::NB : Img<HS, true>::NB;
     static constexpr int RED = NQ * NB * kWave * 16;              // partial transposed products
     static constexpr int LDS_BWD = BwdLds<HS, false>::BYTES + RED;
     static_assert(LDS_FWD <= 163840 && LDS_BWD <= 163840, "small-batch LDS exceeds 160 KiB");
+    static_assert(XBUF >= 2 * Geo<HS>::QC * 16, "two split records fit the exchange buffer");
     static_assert(Geo16<HS>::LDS_FWD % 16 == 0 && BwdLds<HS, false>::BYTES % 16 == 0, "16-B aligned buffers");
 };
 
@@ -121,6 +122,29 @@ __device__ __forceinline__ void xchg_put(f32x4 *xb, const float (&h)[HS], int la
         if (Q::R0 + e < Q::R1) v[e] = h[Q::R0 + e];
     xb[W * kWave + lane] = v;
 }
+// split-record exchange: wave W writes the f16 halves of its slots (hi at half s, lo at half HS + s of the
+// record, fcr_f16.h) into an LDS record laid out like a slab record (store_quads); every wave reads it whole
+template <int HS>
+__device__ __forceinline__ int rec_half_byte(int k, int lane) {   // byte of half k of this lane's record
+    constexpr int FQ = HS / 4, TS = HS % 4;
+    const int d = k >> 1;
+    const int dw = d < 4 * FQ ? ((d >> 2) * kWave + lane) * 16 + (d & 3) * 4 : FQ * kWave * 16 + (lane * TS + d - 4 * FQ) * 4;
+    return dw + 2 * (k & 1);
+}
+template <int HS, int W>
+__device__ __forceinline__ void xrec_put(char *xb, const float (&h)[HS], int lane) {
+    using Q = QR<HS, W>;
+    float one = 1.0f;
+    asm("" : "+v"(one));
+#pragma unroll
+    for (int s = Q::R0; s < Q::R1; ++s) {
+        const _Float16 hi = (_Float16)__builtin_fmaf(h[s], one, 0.0f);
+        const _Float16 lo = (_Float16)__builtin_fmaf(h[s], one, -(float)hi);
+        *reinterpret_cast<_Float16 *>(xb + rec_half_byte<HS>(s, lane)) = hi;
+        *reinterpret_cast<_Float16 *>(xb + rec_half_byte<HS>(HS + s, lane)) = lo;
+    }
+}
+
 template <int HS>
 __device__ __forceinline__ void xchg_get(const f32x4 *xb, float (&h)[HS], int lane) {
 #pragma unroll
@@ -146,6 +170,7 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
     float *lfcp = lfnp + G::FNP;
     float *lfcb = lfcp + G::FCP;
     f32x4 *xbuf = reinterpret_cast<f32x4 *>(lw + G::LDS_FWD / 4);
+    constexpr int RECB = Geo<HS>::QC * 16;   // one split record (bytes); two of them double-buffer the exchange
     lds_copy(lw0, a.p.fa[0], G::FA0);
     lds_copy(lfnp, a.p.fnp, G::FNP);
     lds_copy(lfcp, a.p.fcp, G::FCP);
@@ -177,7 +202,7 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
     float cmd_sum = 0.0f, err_sum = 0.0f, tot_sum = 0.0f;
     float xh0 = 0.0f, xh1 = 0.0f, xh2 = 0.0f, xh3 = 0.0f;
 
-    float c[HS], hout[HS], hp[HS], xc[HS], xn[HS];
+    float c[HS], hout[HS], hp[HS], xc[HS], xn[HS];   // hp, xc, xn: split records (fcr_f16.h)
 #pragma unroll
     for (int r = 0; r < HS; ++r) c[r] = hout[r] = hp[r] = xc[r] = xn[r] = 0.0f;
     const size_t qcell = (size_t)Geo<HS>::QC;
@@ -220,43 +245,46 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
             const float x0 = w0[0], x1 = w1[0];
             rot_left(w0);
             rot_left(w1);
+            char *xb = reinterpret_cast<char *>(xbuf) + (t & 1) * RECB;
             by_quad<HS>(w, [&](auto Wc) {
                 constexpr int W = decltype(Wc)::v;
                 using Q = QR<HS, W>;
                 if (t == 0) fwd16_cell<HS, true, true, false, Q::R0, Q::R1>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
                 else fwd16_cell<HS, true, false, false, Q::R0, Q::R1>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
-                store_quad<HS, W>(SEQ_H(0, t), hout, lane);
                 if (STORE && t + 1 < kL) store_quad<HS, W>(SEQ_C(0, t), c, lane);   // c_9 is never a c_{t-1}
-                if (t + 1 < kL) xchg_put<HS, W>(xbuf + (t & 1) * NQ * kWave, hout, lane);
+                xrec_put<HS, W>(xb, hout, lane);
             });
             if (STORE && lead) xw_wave[((size_t)j * kL + t) * kWave + lane] = f32x2{x0, x1};
-            if (t + 1 < kL) {
-                lds_barrier();
-                xchg_get<HS>(xbuf + (t & 1) * NQ * kWave, hp, lane);
-            }
+            lds_barrier();
+            load_quads<HS>(hp, reinterpret_cast<const f32x4 *>(xb), lane);   // the whole split record of h_t
+            by_quad<HS>(w, [&](auto Wc) { store_quad<HS, decltype(Wc)::v>(SEQ_H(0, t), hp, lane); });
         }
         // ---- layers 1, 2: input sequence from the slab records the workgroup wrote ----
 #pragma unroll
         for (int l = 1; l < kLayers; ++l) {
             const bool keep_h = l == 1 || STORE;
-            vm_drain();   // this wave's quads of the layer-below records are in memory before the barrier
+            vm_drain();   // this wave's chunks of the layer-below records are in memory before the barrier
             small_fill<G::FA1 * 4, NQ>(lw, a.p.fa[l]);
             load_quads<HS>(xc, SEQ_H(l - 1, 0), lane);
             for (int t = 0; t < kL; ++t) {
                 load_quads<HS>(xn, SEQ_H(l - 1, t + 1 < kL ? t + 1 : t), lane);
-                const bool xch = t + 1 < kL || l == kLayers - 1;   // the readout needs the whole h_9 of layer 2
+                const bool last = l == kLayers - 1 && t + 1 == kL;   // h_9 of layer 2: the readout's, in fp32
+                char *xb = reinterpret_cast<char *>(xbuf) + (t & 1) * RECB;
                 by_quad<HS>(w, [&](auto Wc) {
                     constexpr int W = decltype(Wc)::v;
                     using Q = QR<HS, W>;
                     if (t == 0) fwd16_cell<HS, false, true, false, Q::R0, Q::R1>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
                     else fwd16_cell<HS, false, false, false, Q::R0, Q::R1>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
-                    if (keep_h && !(l == 2 && t + 1 == kL)) store_quad<HS, W>(SEQ_H(l, t), hout, lane);
                     if (STORE && t + 1 < kL) store_quad<HS, W>(SEQ_C(l, t), c, lane);
-                    if (xch) xchg_put<HS, W>(xbuf + (t & 1) * NQ * kWave, hout, lane);
+                    if (last) xchg_put<HS, W>(reinterpret_cast<f32x4 *>(xb), hout, lane);
+                    else xrec_put<HS, W>(xb, hout, lane);
                 });
-                if (xch) {
-                    lds_barrier();
-                    xchg_get<HS>(xbuf + (t & 1) * NQ * kWave, hp, lane);
+                lds_barrier();
+                if (last) {
+                    xchg_get<HS>(reinterpret_cast<const f32x4 *>(xb), hout, lane);
+                } else {
+                    load_quads<HS>(hp, reinterpret_cast<const f32x4 *>(xb), lane);
+                    if (keep_h) by_quad<HS>(w, [&](auto Wc) { store_quad<HS, decltype(Wc)::v>(SEQ_H(l, t), hp, lane); });
                 }
 #pragma unroll
                 for (int r = 0; r < HS; ++r) xc[r] = xn[r];
@@ -270,7 +298,7 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
         for (int o = 0; o < kOut; ++o) {
             float p = 0.0f;
 #pragma unroll
-            for (int r = 0; r < HS; ++r) p += lfcp_j[(o * HS + r) * 4 + q] * hp[r];
+            for (int r = 0; r < HS; ++r) p += lfcp_j[(o * HS + r) * 4 + q] * hout[r];
             xo[o] = xor_sum_q(p) + lfcb_j[o];
         }
         if (a.noise) {                                                 // Functions.py:1400-1402
@@ -381,7 +409,7 @@ __device__ __forceinline__ void sb_split(const CellIn<HS> &ci, AOps<HS, L0> &o) 
 #pragma unroll
     for (int kb = 0; kb < A::KB; ++kb) o.bh[kb] = o.bl[kb] = f16x8{};
 #pragma unroll
-    for (int kb = A::KLO; kb < A::KHI; ++kb) fwd_operand<HS, L0, FIRST, false>(kb, x0, x1, xv, hv, o.bh[kb], o.bl[kb]);
+    for (int kb = A::KLO; kb < A::KHI; ++kb) rec_operand<HS, L0, FIRST, false>(kb, x0, x1, xv, hv, o.bh[kb], o.bl[kb]);
     if (A::TAIL && A::KHI == A::KB) o.bh[A::KB - 1] = tail_operand<false>(o.bh[A::KB - 1], o.bl[A::KB - 1]);
 }
 // A: gate pre-activations of this wave's tiles (the forward's products, the same k order), one tile at a
@@ -639,7 +667,7 @@ __device__ __forceinline__ void sb_step(const SbCtx<HS> &x, int j, int t, const 
 #pragma unroll
             for (int kb = 0; kb < AR::KB; ++kb) {
                 if (kb * NB / AR::KB != tau) continue;
-                if (kb >= AR::KLO && kb < AR::KHI) fwd_operand<HS, L0, FS, false>(kb, x0, x1, xv, hv, ops.bh[kb], ops.bl[kb]);
+                if (kb >= AR::KLO && kb < AR::KHI) rec_operand<HS, L0, FS, false>(kb, x0, x1, xv, hv, ops.bh[kb], ops.bl[kb]);
                 else ops.bh[kb] = ops.bl[kb] = f16x8{};
                 if (AR::TAIL && AR::KHI == AR::KB && kb == AR::KB - 1)
                     ops.bh[kb] = tail_operand<false>(ops.bh[kb], ops.bl[kb]);
