@@ -259,6 +259,9 @@ def main():
     ap.add_argument("--precision", choices=("fp32", "f16", "f16fwd"), default="fp32",
                     help="fp32: reference-accurate (default, config 2); f16: gate products in f16 in both passes; "
                          "f16fwd: f16 forward, fp32-accurate backward (config 3)")
+    ap.add_argument("--graphed", action="store_true",
+                    help="time the step as NeuralNetwork.captured_step replays it (one HIP graph per step; the "
+                         "launch-bound small batches, e.g. the reference's B = 15); 1 GPU")
     ap.add_argument("--small-limit", type=int, default=None,
                     help="fcr_set_small_batch_limit: B at or below it runs the small-batch kernels (0 = never; "
                          "default: the library's, 8192)")
@@ -270,6 +273,8 @@ def main():
     rank, local, world = fca.launch.rank_env()
     if world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.graphed and world > 1:
+        sys.exit("bench.py: --graphed times the 1-GPU captured step")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)            # before the process group: RCCL binds each rank to its own GPU
     if world > 1:
@@ -307,8 +312,15 @@ def main():
         opt.step()
         return loss
 
-    for _ in range(args.warmup):
-        step()
+    captured = None
+    if args.graphed:
+        # the product's captured step (graphed.CapturedStep): warm-up steps, capture, then one replay per step
+        captured = fca.NeuralNetwork.captured_step(sim, ctrl, loss_fn, opt, dev)
+        for _ in range(max(args.warmup, 3)):
+            captured(X, S)
+    else:
+        for _ in range(args.warmup):
+            step()
     torch.cuda.synchronize()
 
     # timed region: K steps; HIP events on the launching stream bracket the fused forward and backward of
@@ -319,7 +331,10 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        loss = step(marks[k])
+        if captured is not None:
+            loss = captured(X, S)[0]
+        else:
+            loss = step(marks[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -330,6 +345,12 @@ def main():
         dt = float(t.item())
     ms = 1000.0 * dt / args.steps
     value = world * B * N / (dt / args.steps)
+    if captured is not None:
+        # graph replays carry no events between kernels: time the same kernels in a few eager steps after
+        marks = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(5)]
+        for k in range(len(marks)):
+            step(marks[k])
+        torch.cuda.synchronize()
     fwd_ms = [e[0].elapsed_time(e[1]) for e in marks]
     bwd_ms = [e[1].elapsed_time(e[2]) for e in marks]
 
@@ -371,10 +392,14 @@ def main():
             "dtype": {"fp32": "f32", "f16": "f16", "f16fwd": "f16fwd/f32bwd"}[args.precision],
             "data": "synthetic (SURVEY §8d distribution); reference-trained LSTM/controller weights",
             "config": {"workload": f"unsupervised-MPC rollout train step, B={B}/GPU, N={N}, H={H}, 3-layer LSTM, "
-                                   f"ctrl 3-50-1, {prec_label}", "batch_per_gpu": B, "global_batch": B * world,
+                                   f"ctrl 3-50-1, {prec_label}" + (", HIP-graph replay" if captured is not None else ""),
+                       "batch_per_gpu": B, "global_batch": B * world,
                        "horizon": N, "hidden": H, "parallelism": f"dp{world}", "world_size": world},
             "roofline": roof,
-            "kernels_ms": {"fwd": f_ms, "bwd": b_ms, "source": "HIP events on the launching stream, every timed step"},
+            "kernels_ms": {"fwd": f_ms, "bwd": b_ms,
+                           "source": ("HIP events on the launching stream, 5 eager steps after the graphed timed region"
+                                      if captured is not None else
+                                      "HIP events on the launching stream, every timed step")},
             # the design's own HBM traffic (activation records and hand-off slabs, PMC-measured) against
             # 8 TB/s: how close the dominant kernel runs to the bandwidth its data movement needs
             "hbm_traffic_frac": (traffic / (dom[1] * 1e-3) / (HBM_PEAK_GBS * 1e9)) if traffic else None,

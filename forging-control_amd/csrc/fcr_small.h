@@ -215,6 +215,8 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
     turn.me = w;
     turn.cnt = turn.other = 0;
     turn.prog = nullptr;
+    unsigned long long sc[6] = {0, 0, 0, 0, 0, 0};   // FCR_STAMP: cells, exchanges, refills, count, -, head+readout
+    const unsigned long long sk0 = fstamp();
     __syncthreads();
 
     for (int j = 0; j < N; ++j) {
@@ -246,6 +248,7 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
             rot_left(w0);
             rot_left(w1);
             char *xb = reinterpret_cast<char *>(xbuf) + (t & 1) * RECB;
+            const unsigned long long s0 = fstamp();
             by_quad<HS>(w, [&](auto Wc) {
                 constexpr int W = decltype(Wc)::v;
                 using Q = QR<HS, W>;
@@ -255,21 +258,30 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
                 xrec_put<HS, W>(xb, hout, lane);
             });
             if (STORE && lead) xw_wave[((size_t)j * kL + t) * kWave + lane] = f32x2{x0, x1};
+            const unsigned long long s1 = fstamp();
             lds_barrier();
             load_quads<HS>(hp, reinterpret_cast<const f32x4 *>(xb), lane);   // the whole split record of h_t
             by_quad<HS>(w, [&](auto Wc) { store_quad<HS, decltype(Wc)::v>(SEQ_H(0, t), hp, lane); });
+            if (FCR_STAMP) {
+                sc[0] += s1 - s0;
+                sc[1] += fstamp() - s1;
+                sc[3] += 1;
+            }
         }
         // ---- layers 1, 2: input sequence from the slab records the workgroup wrote ----
 #pragma unroll
         for (int l = 1; l < kLayers; ++l) {
             const bool keep_h = l == 1 || STORE;
+            const unsigned long long sf0 = fstamp();
             vm_drain();   // this wave's chunks of the layer-below records are in memory before the barrier
             small_fill<G::FA1 * 4, NQ>(lw, a.p.fa[l]);
+            if (FCR_STAMP) sc[2] += fstamp() - sf0;
             load_quads<HS>(xc, SEQ_H(l - 1, 0), lane);
             for (int t = 0; t < kL; ++t) {
                 load_quads<HS>(xn, SEQ_H(l - 1, t + 1 < kL ? t + 1 : t), lane);
                 const bool last = l == kLayers - 1 && t + 1 == kL;   // h_9 of layer 2: the readout's, in fp32
                 char *xb = reinterpret_cast<char *>(xbuf) + (t & 1) * RECB;
+                const unsigned long long s0 = fstamp();
                 by_quad<HS>(w, [&](auto Wc) {
                     constexpr int W = decltype(Wc)::v;
                     using Q = QR<HS, W>;
@@ -279,12 +291,18 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
                     if (last) xchg_put<HS, W>(reinterpret_cast<f32x4 *>(xb), hout, lane);
                     else xrec_put<HS, W>(xb, hout, lane);
                 });
+                const unsigned long long s1 = fstamp();
                 lds_barrier();
                 if (last) {
                     xchg_get<HS>(reinterpret_cast<const f32x4 *>(xb), hout, lane);
                 } else {
                     load_quads<HS>(hp, reinterpret_cast<const f32x4 *>(xb), lane);
                     if (keep_h) by_quad<HS>(w, [&](auto Wc) { store_quad<HS, decltype(Wc)::v>(SEQ_H(l, t), hp, lane); });
+                }
+                if (FCR_STAMP) {
+                    sc[0] += s1 - s0;
+                    sc[1] += fstamp() - s1;
+                    sc[3] += 1;
                 }
 #pragma unroll
                 for (int r = 0; r < HS; ++r) xc[r] = xn[r];
@@ -331,6 +349,14 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) part += __shfl_xor(part, m);
     if (lead && lane == 0) a.loss_part[grp] = part;
+    if (FCR_STAMP && lane == 0) {   // diagnostic builds: per (group, wave) cycle sums
+        unsigned long long *o = a.stamp + ((size_t)grp * NQ + w) * 8;
+        o[0] = sc[0];
+        o[1] = sc[1];
+        o[2] = sc[2];
+        o[3] = sc[3];
+        o[4] = fstamp() - sk0;
+    }
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -813,23 +839,24 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sbwd_kernel(BwdA
         const float *lfnp_j = opaque(lfnp), *lfcp_j = opaque(lfcp);
         // layer 2's image (the barriers also retire layer 0's reads of the previous window)
         const unsigned long long th0 = stamp_now();
+        // the window head's global loads go out before the refill's barriers, which cover their latency
+        const float x0 = xh[j * kOut + 0], x1 = xh[j * kOut + 1], x2 = xh[j * kOut + 2], x3 = xh[j * kOut + 3];
+        const float uj = pred[j], uj1 = pred[j + 1 < N ? j + 1 : j], uj2 = pred[j + 2 < N ? j + 2 : j];
+        const f32x2 Gr = j <= N - 2 ? row_grad(kL + j) : f32x2{0.0f, 0.0f};
         small_fill<I1::BYTES, NQ>(lw, a.p.img[2]);
         const unsigned long long th1 = stamp_now();
-        const float x0 = xh[j * kOut + 0], x1 = xh[j * kOut + 1], x2 = xh[j * kOut + 2], x3 = xh[j * kOut + 3];
         float d0 = wgt * 2.0f * (x0 - ref);                             // Functions.py:1443-1452
         float d1 = wgt * ((-x1 > 0.0f ? -1.0f : 0.0f) + (x1 - kP1Max > 0.0f ? 1.0f : 0.0f));
         float d2 = wgt * ((-x2 > 0.0f ? -1.0f : 0.0f) + (x2 - kP2Max > 0.0f ? 1.0f : 0.0f));
         float d3 = 0.0f;
         if (j <= N - 2) {
-            const f32x2 Gr = row_grad(kL + j);
             d0 += __shfl(Gr[0], sl);
             d1 += __shfl(Gr[0], sl + 16);
             d2 += __shfl(Gr[0], sl + 32);
             d3 += __shfl(Gr[0], sl + 48);
             const float g4 = __shfl(Gr[1], sl);
-            const float uj = pred[j], uj1 = pred[j + 1];
             float du = 2.0f * alpha * wgt * (uj1 - uj);
-            if (j + 2 < N) du += 2.0f * alpha * wgt * (uj1 - pred[j + 2]);
+            if (j + 2 < N) du += 2.0f * alpha * wgt * (uj1 - uj2);
             du += g4;
             float z[kMS];                                               // Functions.py:1424-1430
             const float v = fnn_pre(lfnp_j, q, x0, x3, ref, z);

@@ -33,3 +33,12 @@ for w in range(nq):
     print(f"wave {w}: cells {c:.0f}  B {st[w, 0] / c:7.0f}  A {st[w, 1] / c:7.0f}  reduce {st[w, 2] / c:7.0f}  "
           f"per cell total {(st[w, 0] + st[w, 1] + st[w, 2]) / c:7.0f}  lifetime {st[w, 4]:.3e} ({st[w, 4] / c:.0f}/cell)")
     print(f"        per window: 3 refills {st[w, 5] / 10:7.0f}  head {st[w, 7] / 10:7.0f}  3 phase prologues (A(9)) {st[w, 6] / 10:7.0f}")
+
+nw_pad = (a.batch + 15) // 16
+nw_pad = (nw_pad + 7) // 8 * 8
+fo = off + nw_pad * 64
+fw = ws[fo:fo + nq * 64].view(torch.int64).reshape(nq, 8).cpu().numpy().astype(np.float64)
+for w in range(nq):
+    c = fw[w, 3]
+    print(f"forward wave {w}: cells {c:.0f}  cell {fw[w, 0] / c:7.0f}  exchange {fw[w, 1] / c:7.0f}  "
+          f"refills/window {fw[w, 2] / 10:7.0f}  lifetime {fw[w, 4]:.3e} ({fw[w, 4] / c:.0f}/cell)")
