@@ -54,12 +54,12 @@ def pmc_traffic(kernel):
     import re
     pick = []
     for f in glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")):
-        m = re.fullmatch(r"(round|r)(\d+)_pmc\.json", os.path.basename(f))   # the rollout's, not the plant's
+        m = re.fullmatch(r"(round|r)(\d+)([a-z]?)_pmc\.json", os.path.basename(f))   # the rollout's, not the plant's
         if m:
-            pick.append((m.group(1) == "round", int(m.group(2)), f))
+            pick.append((m.group(1) == "round", int(m.group(2)), m.group(3), f))
     if not pick:
         return None, None
-    f = max(pick)[2]
+    f = max(pick)[-1]
     d = json.load(open(f))
     if kernel not in d or not d[kernel].get("hbm_bytes_corrected"):
         return None, None
