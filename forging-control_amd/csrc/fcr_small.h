@@ -83,33 +83,12 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // before a barrier that hands global slab records between waves: this wave's stores are complete
 __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Per-phase image refill for a workgroup that is alone on its CU: with one workgroup per CU the LDS-DMA
-// refill (lds_fill, ~11 B/cycle) is fully exposed (~10 k cycles per 109 KB image at B = 15). Here each wave
-// loads its share of 1 KiB chunks into registers BEFORE the barrier that retires the old image (the
-// loads overlap the phase's tail skew), then writes them to LDS; the second barrier publishes the image.
-#ifndef FCR_SMALL_VFILL
-#define FCR_SMALL_VFILL 0
-#endif
+// Per-phase image refill: LDS-DMA (lds_fill). With one workgroup per CU it is exposed (~2.7 k cycles per
+// 109 KB image at B = 15); staging the image through registers with the global loads issued before the
+// retiring barrier measured slower (round 2), so the DMA form stays.
 template <int NBYTES, int NWAVES>
 __device__ __forceinline__ void small_fill(float *lw, const float *__restrict__ src) {
-#if FCR_SMALL_VFILL
-    static_assert(NBYTES % 1024 == 0, "image must be whole 1 KiB chunks");
-    constexpr int NCH = NBYTES / 1024, PER = (NCH + NWAVES - 1) / NWAVES;
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const f32x4 *s4 = reinterpret_cast<const f32x4 *>(src) + lane;
-    f32x4 v[PER];
-#pragma unroll
-    for (int k = 0; k < PER; ++k)
-        if (wv + k * NWAVES < NCH) v[k] = s4[(wv + k * NWAVES) * kWave];
-    __syncthreads();
-    f32x4 *d4 = reinterpret_cast<f32x4 *>(lw) + lane;
-#pragma unroll
-    for (int k = 0; k < PER; ++k)
-        if (wv + k * NWAVES < NCH) d4[(wv + k * NWAVES) * kWave] = v[k];
-    __syncthreads();
-#else
     lds_fill<NBYTES, NWAVES>(lw, src);
-#endif
 }
 
 // h exchange: wave W publishes its slots of h_t, every wave reads the whole vector back
@@ -215,11 +194,12 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
     turn.me = w;
     turn.cnt = turn.other = 0;
     turn.prog = nullptr;
-    unsigned long long sc[6] = {0, 0, 0, 0, 0, 0};   // FCR_STAMP: cells, exchanges, refills, count, -, head+readout
+    unsigned long long sc[6] = {0, 0, 0, 0, 0, 0};   // FCR_STAMP: cells, exchanges, refills, count, head+readout, refill+first load
     const unsigned long long sk0 = fstamp();
     __syncthreads();
 
     for (int j = 0; j < N; ++j) {
+        const unsigned long long sw0 = fstamp();
         const float *lfnp_j = opaque(lfnp), *lfcp_j = opaque(lfcp), *lfcb_j = opaque(lfcb);
         float pred = u0;
         if (j > 0) {                                                   // Functions.py:1421-1434
@@ -242,6 +222,7 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
         f32x4 *csj = cs_wave + (size_t)j * kLayers * kL * qcell;
 #define SEQ_H(l, t) (hsj + (size_t)((l) * kL + (t)) * qcell)
 #define SEQ_C(l, t) (csj + (size_t)((l) * kL + (t)) * qcell)
+        if (FCR_STAMP) sc[4] += fstamp() - sw0;   // window head
         // ---- layer 0 (Functions.py:374) ----
         for (int t = 0; t < kL; ++t) {
             const float x0 = w0[0], x1 = w1[0];
@@ -277,6 +258,10 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
             small_fill<G::FA1 * 4, NQ>(lw, a.p.fa[l]);
             if (FCR_STAMP) sc[2] += fstamp() - sf0;
             load_quads<HS>(xc, SEQ_H(l - 1, 0), lane);
+            if (FCR_STAMP) {   // diagnostic: the first record's latency (the cell would wait for it anyway)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                sc[5] += fstamp() - sf0;
+            }
             for (int t = 0; t < kL; ++t) {
                 load_quads<HS>(xn, SEQ_H(l - 1, t + 1 < kL ? t + 1 : t), lane);
                 const bool last = l == kLayers - 1 && t + 1 == kL;   // h_9 of layer 2: the readout's, in fp32
@@ -310,6 +295,7 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
         }
 #undef SEQ_H
 #undef SEQ_C
+        const unsigned long long sr0 = fstamp();
         // ---- readout fc(h_9 of layer 2) (Functions.py:377), identical in every wave ----
         float xo[kOut];
 #pragma unroll
@@ -338,6 +324,7 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
         tot_sum += (err + cmd_j) + con;
         err_sum += err;
         cmd_sum += cmd_j;
+        if (FCR_STAMP) sc[4] += fstamp() - sr0;   // readout and costs
     }
     const float cost = tot_sum / (float)N;                             // Functions.py:1458-1460
     if (lead && valid && q == 0) {
@@ -356,6 +343,8 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
         o[2] = sc[2];
         o[3] = sc[3];
         o[4] = fstamp() - sk0;
+        o[5] = sc[4];
+        o[6] = sc[5];
     }
 }
 

@@ -42,3 +42,4 @@ for w in range(nq):
     c = fw[w, 3]
     print(f"forward wave {w}: cells {c:.0f}  cell {fw[w, 0] / c:7.0f}  exchange {fw[w, 1] / c:7.0f}  "
           f"refills/window {fw[w, 2] / 10:7.0f}  lifetime {fw[w, 4]:.3e} ({fw[w, 4] / c:.0f}/cell)")
+    print(f"        per window: head+readout {fw[w, 5] / 10:7.0f}  refills incl. first record load {fw[w, 6] / 10:7.0f}")
