@@ -195,7 +195,8 @@ int launch_bwd(const BwdArgs &ba, const Layout &L, bool lp, hipStream_t s) {
 // Small-batch kernels (fcr_small.h): one workgroup of ceil(HS/4) waves per 16-trajectory group.
 // Used for the fp32-accurate mode at HS = 8, 13 when B <= g_small_max_batch (fcr_set_small_batch_limit):
 // below one wave per SIMD the fused kernels run at one wave's sequential latency.
-int g_small_max_batch = 8192;
+// thread-local like the last-error text: the ABI keeps no process-wide mutable state
+thread_local int g_small_max_batch = 8192;
 bool use_small(const fcr_dims *d, const Layout &L) {
     return d->precision == FCR_PRECISION_FP32 && (L.HS == 8 || L.HS == 13) && d->B <= g_small_max_batch;
 }

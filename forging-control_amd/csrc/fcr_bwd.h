@@ -101,7 +101,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
                                          float (&dh)[HS], float (&dc)[HS], float (&dxo)[HS], float &dxq,
                                          float &dx4, CellIn<HS> &ci, const NextIn &nx, Stamps &sp) {
     const unsigned long long t0 = stamp_now();
-#if FCR_PRIO
+#if FCR_PRIO == 1
     // the two waves of a SIMD take turns at the higher issue priority, cell by cell, so neither runs
     // ahead of the other between the phase barriers (oldest-first arbitration otherwise skews them)
     if (sp.t[4] & 1) __builtin_amdgcn_s_setprio(1);
@@ -422,6 +422,9 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         return n;
     };
     Stamps sp = {{0, 0, 0, 0, (unsigned long long)((threadIdx.x >> 8) & 1), 0, 0, 0}};
+#if FCR_PRIO == 2   // diagnostic: static priority for the second-dispatched half (MI355X_MICROARCH.md item 4)
+    if ((threadIdx.x >> 8) & 1) __builtin_amdgcn_s_setprio(1);
+#endif
     const unsigned long long tk0 = stamp_now();
     CellIn<HS> ci;
     {

@@ -227,8 +227,8 @@ int fcr_lstm_backward(const fcr_dims *dims, const fcr_weights *w, const float *d
  * Kernel choice for small batches (fp32-accurate mode, H 17..52): B <= max_batch runs the small-batch
  * kernels, which split each 16-trajectory group's cell over the four waves of a workgroup (the reference
  * trains at B = 15, UL/Main.py:84,297); larger B runs the fused one-wave-per-group kernels. Default 8192;
- * 0 = never. Process-wide; both kernel families keep the same workspace layout, so a change between a
- * forward and its backward is harmless. Returns the previous limit.
+ * 0 = never. Per calling thread (like fcr_last_error); both kernel families keep the same workspace
+ * layout, so a change between a forward and its backward is harmless. Returns the previous limit.
  */
 int fcr_set_small_batch_limit(int32_t max_batch);
 

@@ -104,3 +104,21 @@ def test_fnn_model_on_cpu_is_the_torch_module():
     assert not hip_shape_ok(m, x)
     ref = torch.nn.functional.hardtanh(m.fc_out(torch.relu(m.fc_inp(x))))
     assert torch.equal(m(x), ref)
+
+
+def test_small_batch_limit_is_per_thread():
+    """fcr_set_small_batch_limit (the kernel-family choice) keeps no process-wide state: a setting made on
+    one thread is not seen by another (no global mutable state but the thread-local error)."""
+    import threading
+    n = fca._native
+    prev = n.set_small_batch_limit(77)
+    try:
+        assert n.small_batch_limit() == 77
+        seen = {}
+        th = threading.Thread(target=lambda: seen.setdefault("other", n.small_batch_limit()))
+        th.start()
+        th.join()
+        assert seen["other"] == 8192
+        assert n.set_small_batch_limit(-5) == 77 and n.small_batch_limit() == 0   # negative clamps to 0 = never
+    finally:
+        n.set_small_batch_limit(prev)

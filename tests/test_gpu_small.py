@@ -116,4 +116,4 @@ def test_small_kernels_deterministic_and_dloss_linear():
 def test_default_limit_routes_the_reference_batch_to_the_small_kernels():
     prev = native.set_small_batch_limit(123)
     assert native.set_small_batch_limit(prev) == 123
-    assert prev == 8192
+    assert prev == 8192   # per thread (tests/test_abi.py)
