@@ -22,6 +22,7 @@
 #include "fcr_small.h"
 #include "fcr_surrogate.h"
 #include "fcr_wide.h"
+#include "fcr_wgemm.h"
 
 namespace fcr {
 
@@ -463,6 +464,26 @@ int launch_cell_bwd(int B, int H, hipStream_t s, const float *act, const float *
     return launch_check("wide_cell_bwd_kernel");
 }
 
+// Layers >= 1 of the split path: the cell's GEMM and update as one hand-written kernel (fcr_wgemm.h).
+// Off by default: its one-barrier 256 x 128 mainloop runs a cell in ~485 us where rocBLAS's GEMM + the cell
+// kernel take ~300 us (round 2, B = 65 536, H = 256; DESIGN.md §4 "Config 5"). Parity-tested when on.
+#ifndef FCR_WIDE_FUSED
+#define FCR_WIDE_FUSED 0
+#endif
+bool wide_fused_ok(int H) { return FCR_WIDE_FUSED && H % kWgU == 0; }
+int launch_wgemm_cell(const WgArgs &wa, hipStream_t s) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        const hipError_t e = hipFuncSetAttribute((const void *)wide_gemm_cell_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kWgLds);
+        if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(wgemm): %s", hipGetErrorString(e));
+        attr_set = true;
+    }
+    const int nx = (wa.B + kWgN - 1) / kWgN, ny = wa.H / kWgU;
+    hipLaunchKernelGGL(wide_gemm_cell_kernel, dim3((unsigned)(nx * ny)), dim3(kWgThreads), kWgLds, s, wa);
+    return launch_check("wide_gemm_cell_kernel");
+}
+
 // One window's cells, forward: 3 layers x 10 steps of [GEMM x_t W_ih^T, GEMM h_{t-1} W_hh^T, cell].
 // sp != nullptr (the rollout): the H-wide products as ONE K-concatenated split-f16 GEMM per cell (gemm16_fwd) — ~3x the fp32
 // GEMM rate at equal accuracy; sp == nullptr (the surrogate's training step): fp32 rocBLAS throughout.
@@ -481,6 +502,25 @@ int wide_cells(rocblas_handle h, const WideArgs &a, const float *const *w_ih, co
             // split path with keep_act (the backward's recompute): the gate pre-activations stay per cell in
             // the Act slab (wide_cell_bwd_kernel<true> rebuilds the activations) instead of a second array
             float *G = (sp && keep_act) ? a.Act + ((size_t)l * kL + t) * cell * 4 : a.G;
+            if (sp && l > 0 && wide_fused_ok(H)) {   // GEMM + cell update in one kernel
+                WgArgs wa{};
+                wa.A = sp->fa[l];
+                wa.XB = xb(l, t);
+                wa.lda = wa.ldb = 6 * H;
+                wa.K = t > 0 ? 6 * H : 3 * H;
+                wa.B = B;
+                wa.H = H;
+                wa.c_prev = t > 0 ? a.Cs + ((size_t)l * kL + t - 1) * cell : nullptr;
+                wa.c_out = a.Cs + ((size_t)l * kL + t) * cell;
+                wa.h_out = (l == kLayers - 1 && t == kL - 1) ? a.Hs + ((size_t)l * kL + t) * cell : nullptr;
+                wa.preact = keep_act ? G : nullptr;
+                wa.xb_h = t + 1 < kL ? xb(l, t + 1) + 3 * H : nullptr;
+                wa.sh = ldx(l);
+                wa.xb_x = l + 1 < kLayers ? xb(l + 1, t) : nullptr;
+                wa.sx = ldx(l + 1 < kLayers ? l + 1 : l);
+                if ((rc = launch_wgemm_cell(wa, s))) return rc;
+                continue;
+            }
             if (sp) {
                 if (l == 0) {   // [h part | window-row part] (wide_window_kernel writes the latter); t = 0: no h
                     const int k0 = t > 0 ? 0 : 3 * H;

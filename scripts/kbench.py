@@ -39,17 +39,18 @@ def main(return_state=False):
     ap.add_argument("libs", nargs="+")
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--horizon", type=int, default=10)
+    ap.add_argument("--hidden", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--sustain", type=int, default=0, help="then time this many back-to-back launches per lib")
     ap.add_argument("--precision", type=int, default=0, help="0 = fp32-accurate, 1 = f16 (config 3)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    B, N = a.batch, a.horizon
-    sim, ctrl = load_weights(dev, 50)
+    B, N, H = a.batch, a.horizon, a.hidden
+    sim, ctrl = load_weights(dev, H)
     X, S = synth_batch(B, dev, 7)
     with torch.no_grad():
         u0 = ctrl(X).contiguous()
-    dims = fca.rollout.make_dims(B, N, 50, 3, 50, 20.0, precision=a.precision)
+    dims = fca.rollout.make_dims(B, N, H, 3, 50, 20.0, precision=a.precision)
     w = _n.FcrWeights()
     params = [ctrl.fc_inp.weight, ctrl.fc_inp.bias, ctrl.fc_out.weight]
     w.ctrl_w_inp, w.ctrl_b_inp, w.ctrl_w_out = (p.data_ptr() for p in params)
