@@ -24,11 +24,17 @@ namespace fcr {
 constexpr int kWgU = 64;                  // units per workgroup
 constexpr int kWgM = 4 * kWgU;            // A rows per workgroup
 constexpr int kWgN = 128;                 // trajectories per workgroup
-constexpr int kWgK = 64;                  // K per step
+#ifndef FCR_WG_K
+#define FCR_WG_K 32
+#endif
+constexpr int kWgK = FCR_WG_K;            // K per step: 32 keeps the workgroup at 72 KB of LDS, two per CU
+constexpr int kWgC = kWgK / 8;            // 16-B chunks per LDS row
 constexpr int kWgThreads = 512;
 constexpr int kWgStageA = kWgM * kWgK * 2;   // bytes
 constexpr int kWgStageB = kWgN * kWgK * 2;
-constexpr int kWgLds = 2 * (kWgStageA + kWgStageB);
+constexpr int kWgEpi = kWgN * ((kWgU + 4) * 4 + 2 * (kWgU + 8) * 2);   // the epilogue's c / hi / lo tiles
+constexpr int kWgLds = 2 * (kWgStageA + kWgStageB) > kWgEpi ? 2 * (kWgStageA + kWgStageB) : kWgEpi;
+static_assert(kWgK == 32 || kWgK == 64, "K step");
 
 struct WgArgs {
     const _Float16 *A;     // [4H][lda]
@@ -43,8 +49,12 @@ struct WgArgs {
     int sh, sx;
 };
 
-// byte offset of 16-B chunk c (0..7) of LDS row r in a stage
-__device__ __forceinline__ uint32_t wg_off(int r, int c) { return (uint32_t)(r * 128 + ((c ^ (r & 7)) << 4)); }
+// byte offset of 16-B chunk c of LDS row r in a stage; the swizzle puts the 8 rows of a fragment read's
+// 8-lane phase on the 8 distinct 16-B slots of a 128-B bank line
+__device__ __forceinline__ uint32_t wg_off(int r, int c) {
+    if constexpr (kWgC == 8) return (uint32_t)(r * 128 + ((c ^ (r & 7)) << 4));
+    else return (uint32_t)(r * 64 + ((c ^ ((r >> 1) & 3)) << 4));
+}
 
 __global__ __launch_bounds__(kWgThreads, 2) void wide_gemm_cell_kernel(WgArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -62,41 +72,42 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_gemm_cell_kernel(WgArgs a)
     const int b0 = (wg / ny) * kWgN;                   // first trajectory
     const int nk = a.K / kWgK;
 
-    // global -> register chunk assignment: A 256 rows x 8 chunks (4 per thread), XB 128 rows x 8 chunks (2)
+    // global -> register chunk assignment: A 256 rows x kWgC chunks, XB 128 rows x kWgC chunks
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const int cch = tid & 7;
-    const _Float16 *gA[4];
-    uint32_t oA[4];
+    constexpr int NA = kWgM * kWgC / kWgThreads, NB = kWgN * kWgC / kWgThreads, RS = kWgThreads / kWgC;
+    const int cch = tid % kWgC;
+    const _Float16 *gA[NA];
+    uint32_t oA[NA];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = (tid >> 3) + 64 * i;            // LDS row = 4 * unit + gate
+    for (int i = 0; i < NA; ++i) {
+        const int r = tid / kWgC + RS * i;            // LDS row = 4 * unit + gate
         const int grow = (r & 3) * H + u0 + (r >> 2);  // torch row gate * H + unit
         gA[i] = a.A + (size_t)grow * a.lda + cch * 8;
         oA[i] = wg_off(r, cch);
     }
-    const _Float16 *gB[2];
-    uint32_t oB[2];
+    const _Float16 *gB[NB];
+    uint32_t oB[NB];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int r = (tid >> 3) + 64 * i;
+    for (int i = 0; i < NB; ++i) {
+        const int r = tid / kWgC + RS * i;
         int b = b0 + r;
         if (b >= a.B) b = a.B - 1;                     // tail rows recompute the last trajectory (not stored)
         gB[i] = a.XB + (size_t)b * a.ldb + cch * 8;
         oB[i] = (uint32_t)kWgStageA + wg_off(r, cch);
     }
-    u32x4 ra[4], rb[2];
+    u32x4 ra[NA], rb[NB];
     auto gload = [&](int ks) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ra[i] = *reinterpret_cast<const u32x4 *>(gA[i] + ks * kWgK);
+        for (int i = 0; i < NA; ++i) ra[i] = *reinterpret_cast<const u32x4 *>(gA[i] + ks * kWgK);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) rb[i] = *reinterpret_cast<const u32x4 *>(gB[i] + ks * kWgK);
+        for (int i = 0; i < NB; ++i) rb[i] = *reinterpret_cast<const u32x4 *>(gB[i] + ks * kWgK);
     };
     auto lstore = [&](int buf) {
         char *base = lds + buf * (kWgStageA + kWgStageB);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4 *>(base + oA[i]) = ra[i];
+        for (int i = 0; i < NA; ++i) *reinterpret_cast<u32x4 *>(base + oA[i]) = ra[i];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4 *>(base + oB[i]) = rb[i];
+        for (int i = 0; i < NB; ++i) *reinterpret_cast<u32x4 *>(base + oB[i]) = rb[i];
     };
 
     f32x4 acc[8][2];
@@ -113,7 +124,7 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_gemm_cell_kernel(WgArgs a)
         if (ks + 1 < nk) gload(ks + 1);
         const char *base = lds + buf * (kWgStageA + kWgStageB);
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
+        for (int kb = 0; kb < kWgK / 32; ++kb) {
             f16x8 bf[2];
 #pragma unroll
             for (int n = 0; n < 2; ++n) {
@@ -132,42 +143,89 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_gemm_cell_kernel(WgArgs a)
         __syncthreads();
     }
 
-    // ---- epilogue: the cell update (wide_cell_kernel's arithmetic) on the accumulators ----
+#ifdef FCR_WG_NOEPI   // diagnostic: the mainloop alone (one store per tile keeps it live)
+    if (a.B < 0) for (int m = 0; m < 8; ++m) a.c_out[m] = acc[m][0][0] + acc[m][1][0];
+    return;
+#endif
+    // ---- epilogue: the cell update (wide_cell_kernel's arithmetic) on the accumulators, through LDS ----
+    // A lane holds (trajectory, unit) pairs scattered over 16 rows; the slabs want whole rows. So the c_prev
+    // tile comes in by rows, each lane updates its pairs in LDS tiles [trajectory][unit] (rows padded by 16 B:
+    // 2-way bank conflicts at most, chunks stay 16-B aligned), and c, the operand halves and (keep_act) the
+    // pre-activations go out by rows again.
+    constexpr int CSTR = kWgU + 4;            // floats per c row
+    constexpr int HSTR = kWgU + 8;            // halves per hi / lo row
+    float *cs = reinterpret_cast<float *>(lds);                                   // [128][CSTR]
+    _Float16 *hs = reinterpret_cast<_Float16 *>(lds + kWgN * CSTR * 4);           // [128][HSTR]
+    _Float16 *ls = hs + kWgN * HSTR;                                              // [128][HSTR]
+    const int er = tid >> 4, ec = tid & 15;   // row-wise passes: 32 rows x 16 chunks per 512 threads
+    auto row_b = [&](int r) { return b0 + r; };
+    if (a.c_prev) {
+#pragma unroll
+        for (int p = 0; p < kWgN / 32; ++p) {
+            const int r = er + 32 * p, b = row_b(r);
+            if (b < a.B)
+                *reinterpret_cast<f32x4 *>(cs + r * CSTR + 4 * ec) =
+                    *reinterpret_cast<const f32x4 *>(a.c_prev + (size_t)b * H + u0 + 4 * ec);
+        }
+    }
+    __syncthreads();
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
-        const int b = b0 + 32 * wc + 16 * n + fr;
-        if (b >= a.B) continue;
+        const int r = 32 * wc + 16 * n + fr;
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
-            const int u = u0 + 32 * wr + 4 * m + fq;
+            const int ul = 32 * wr + 4 * m + fq;
             const f32x4 g4 = acc[m][n];
-            const size_t idx = (size_t)b * H + u;
-            const float cp = a.c_prev ? a.c_prev[idx] : 0.0f;
+            const float cp = a.c_prev ? cs[r * CSTR + ul] : 0.0f;
             const float i = sigm(g4[0]), f = sigm(g4[1]), g = tanhf(g4[2]), o = sigm(g4[3]);
             const float c = (a.c_prev ? f * cp : 0.0f) + i * g;
             const float h = o * tanhf(c);
             const _Float16 hi = (_Float16)h;
-            const _Float16 lo = (_Float16)(h - (float)hi);
-            a.c_out[idx] = c;
-            if (a.h_out) a.h_out[idx] = h;
+            cs[r * CSTR + ul] = c;
+            hs[r * HSTR + ul] = hi;
+            ls[r * HSTR + ul] = (_Float16)(h - (float)hi);
+            const int b = b0 + r;
+            if (a.h_out && b < a.B) a.h_out[(size_t)b * H + u0 + ul] = h;   // the readout's cell only
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < kWgN / 32; ++p) {
+        const int r = er + 32 * p, b = row_b(r);
+        if (b >= a.B) continue;
+        *reinterpret_cast<f32x4 *>(a.c_out + (size_t)b * H + u0 + 4 * ec) = *reinterpret_cast<const f32x4 *>(cs + r * CSTR + 4 * ec);
+        if (ec < 8) {   // 8 chunks of 8 halves per row: the hi and lo halves of 64 units
+            const u32x4 hv = *reinterpret_cast<const u32x4 *>(hs + r * HSTR + 8 * ec);
+            const u32x4 lv = *reinterpret_cast<const u32x4 *>(ls + r * HSTR + 8 * ec);
             if (a.xb_h) {
-                _Float16 *p = a.xb_h + (size_t)b * a.sh + u;
-                p[0] = hi;
-                p[H] = lo;
-                p[2 * H] = hi;
+                _Float16 *q = a.xb_h + (size_t)b * a.sh + u0 + 8 * ec;
+                *reinterpret_cast<u32x4 *>(q) = hv;
+                *reinterpret_cast<u32x4 *>(q + H) = lv;
+                *reinterpret_cast<u32x4 *>(q + 2 * H) = hv;
             }
             if (a.xb_x) {
-                _Float16 *p = a.xb_x + (size_t)b * a.sx + u;
-                p[0] = hi;
-                p[H] = lo;
-                p[2 * H] = hi;
+                _Float16 *q = a.xb_x + (size_t)b * a.sx + u0 + 8 * ec;
+                *reinterpret_cast<u32x4 *>(q) = hv;
+                *reinterpret_cast<u32x4 *>(q + H) = lv;
+                *reinterpret_cast<u32x4 *>(q + 2 * H) = hv;
             }
-            if (a.preact) {
-                float *p = a.preact + (size_t)b * 4 * H + u;
-                p[0] = g4[0];
-                p[H] = g4[1];
-                p[2 * H] = g4[2];
-                p[3 * H] = g4[3];
+        }
+    }
+    if (a.preact) {   // gate by gate through the c tile: rows of 64 pre-activations
+#pragma unroll
+        for (int gt = 0; gt < 4; ++gt) {
+            __syncthreads();
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+#pragma unroll
+                for (int m = 0; m < 8; ++m) cs[(32 * wc + 16 * n + fr) * CSTR + 32 * wr + 4 * m + fq] = acc[m][n][gt];
+            __syncthreads();
+#pragma unroll
+            for (int p = 0; p < kWgN / 32; ++p) {
+                const int r = er + 32 * p, b = row_b(r);
+                if (b < a.B)
+                    *reinterpret_cast<f32x4 *>(a.preact + (size_t)b * 4 * H + gt * H + u0 + 4 * ec) =
+                        *reinterpret_cast<const f32x4 *>(cs + r * CSTR + 4 * ec);
             }
         }
     }
