@@ -468,7 +468,7 @@ int launch_cell_bwd(int B, int H, hipStream_t s, const float *act, const float *
 // Off by default: its one-barrier 256 x 128 mainloop runs a cell in ~485 us where rocBLAS's GEMM + the cell
 // kernel take ~300 us (round 2, B = 65 536, H = 256; DESIGN.md §4 "Config 5"). Parity-tested when on.
 #ifndef FCR_WIDE_FUSED
-#define FCR_WIDE_FUSED 0
+#define FCR_WIDE_FUSED 1
 #endif
 bool wide_fused_ok(int H) { return FCR_WIDE_FUSED && H % kWgU == 0; }
 int launch_wgemm_cell(const WgArgs &wa, hipStream_t s) {
@@ -479,6 +479,9 @@ int launch_wgemm_cell(const WgArgs &wa, hipStream_t s) {
         if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(wgemm): %s", hipGetErrorString(e));
         attr_set = true;
     }
+    if (wa.K <= 0 || wa.K % kWgK || wa.lda % 8 || wa.ldb % 8 || wa.H % kWgU || wa.B <= 0)
+        return fail(FCR_EINVAL, "wide_gemm_cell_kernel: K %d lda %d ldb %d H %d B %d off its tiling", wa.K, wa.lda, wa.ldb,
+                    wa.H, wa.B);
     const int nx = (wa.B + kWgN - 1) / kWgN, ny = wa.H / kWgU;
     hipLaunchKernelGGL(wide_gemm_cell_kernel, dim3((unsigned)(nx * ny)), dim3(kWgThreads), kWgLds, s, wa);
     return launch_check("wide_gemm_cell_kernel");
@@ -502,19 +505,22 @@ int wide_cells(rocblas_handle h, const WideArgs &a, const float *const *w_ih, co
             // split path with keep_act (the backward's recompute): the gate pre-activations stay per cell in
             // the Act slab (wide_cell_bwd_kernel<true> rebuilds the activations) instead of a second array
             float *G = (sp && keep_act) ? a.Act + ((size_t)l * kL + t) * cell * 4 : a.G;
-            if (sp && l > 0 && wide_fused_ok(H)) {   // GEMM + cell update in one kernel
+            if (sp && wide_fused_ok(H)) {   // GEMM + cell update in one kernel
+                // layer 0: [h part 3H | window-row part kX16], t = 0 without the h part
+                const int k0 = (l == 0 && t == 0) ? 3 * H : 0;
                 WgArgs wa{};
-                wa.A = sp->fa[l];
-                wa.XB = xb(l, t);
-                wa.lda = wa.ldb = 6 * H;
-                wa.K = t > 0 ? 6 * H : 3 * H;
+                wa.A = sp->fa[l] + k0;
+                wa.XB = xb(l, t) + k0;
+                wa.lda = l == 0 ? 3 * H + kX16 : 6 * H;
+                wa.ldb = ldx(l);
+                wa.K = l == 0 ? 3 * H + kX16 - k0 : t > 0 ? 6 * H : 3 * H;
                 wa.B = B;
                 wa.H = H;
                 wa.c_prev = t > 0 ? a.Cs + ((size_t)l * kL + t - 1) * cell : nullptr;
                 wa.c_out = a.Cs + ((size_t)l * kL + t) * cell;
                 wa.h_out = (l == kLayers - 1 && t == kL - 1) ? a.Hs + ((size_t)l * kL + t) * cell : nullptr;
                 wa.preact = keep_act ? G : nullptr;
-                wa.xb_h = t + 1 < kL ? xb(l, t + 1) + 3 * H : nullptr;
+                wa.xb_h = t + 1 < kL ? xb(l, t + 1) + (l == 0 ? 0 : 3 * H) : nullptr;
                 wa.sh = ldx(l);
                 wa.xb_x = l + 1 < kLayers ? xb(l + 1, t) : nullptr;
                 wa.sx = ldx(l + 1 < kLayers ? l + 1 : l);

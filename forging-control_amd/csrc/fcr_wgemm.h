@@ -1,8 +1,7 @@
 // fcr_wgemm.h — H > 52 (config 5): one LSTM cell of the whole batch as ONE hand-written split-f16 MFMA GEMM
-// with the cell update in its epilogue (in place of rocBLAS gemm16_fwd + wide_cell_kernel for layers >= 1).
-// Experimental, built with FCR_WIDE_FUSED=1 (fcr_abi.hip): correct, but its mainloop is ~2x slower than
-// rocBLAS's Tensile kernel at this shape — the deep-pipelined 256^2 structure of cdna_hip_programming.md §5
-// is what it would need before the fused epilogue (no 4H x B gate matrix in HBM) pays.
+// with the cell update in its epilogue (in place of rocBLAS gemm16_fwd + wide_cell_kernel, every layer).
+// On by default (FCR_WIDE_FUSED=1, fcr_abi.hip) for every layer when H % 64 == 0: at config 5 it takes the
+// step from 703 to 657 ms (forward 219 -> 180 ms), equal to the rocBLAS path within 2e-7 relative.
 //
 // Product: G[b][r] = sum_k XB[b][k] A[r][k], the K-concatenated split operands of fcr_wide.h (A = [Wih_hi |
 // Wih_hi | Wih_lo | Whh_hi | Whh_hi | Whh_lo] rows r = gate*H + unit, XB = [x_hi | x_lo | x_hi | h_hi | h_lo |
@@ -11,10 +10,13 @@
 // lane = trajectory lane & 15, rows 4 (lane >> 4) .. +3) holds the four gates i, f, g, o of ONE unit of ONE
 // trajectory: the cell update runs on the accumulators, and the 4H x B gate matrix never goes to HBM.
 //
-// Tile walk: 8 waves (2 x 4), each 128 rows (32 units) x 32 trajectories = 8 x 2 D tiles; K in steps of 64
-// (two 16x16x32 f16 k-blocks), A and XB chunks staged global -> registers -> LDS, double-buffered, one
-// barrier per step. LDS rows are 128 B; their 16-B chunks are XOR-swizzled by (row & 7), so the 16 rows
-// one ds_read_b128 touches land on distinct banks.
+// Tile walk: 4 waves (2 x 2), each 128 rows (32 units) x 64 trajectories = 8 x 4 D tiles (LDS reads 0.023
+// B per MFMA flop, under the 0.031 one CU's LDS sustains at the MFMA peak); K in steps of 32 (one 16x16x32
+// f16 k-block), A and XB chunks staged global -> registers -> LDS, double-buffered, one barrier per step;
+// 72 KB of LDS (the epilogue's tiles) lets two workgroups share a CU, so one's epilogue and barriers
+// overlap the other's MFMAs. LDS rows are 64 B; their 16-B chunks are XOR-swizzled by (row >> 1) & 3, so
+// the 8 rows of a ds_read_b128 phase land on distinct 16-B bank groups. (8 waves x 128 x 32 measured the
+// same; K steps of 64 at one workgroup per CU 13 % slower.)
 #pragma once
 #include "fcr_common.h"
 #include "fcr_f16.h"
@@ -29,7 +31,14 @@ constexpr int kWgN = 128;                 // trajectories per workgroup
 #endif
 constexpr int kWgK = FCR_WG_K;            // K per step: 32 keeps the workgroup at 72 KB of LDS, two per CU
 constexpr int kWgC = kWgK / 8;            // 16-B chunks per LDS row
-constexpr int kWgThreads = 512;
+#ifndef FCR_WG_WAVES
+#define FCR_WG_WAVES 4
+#endif
+constexpr int kWgWaves = FCR_WG_WAVES;    // 2 x kWgWC waves; each 128 rows x kWgN / kWgWC trajectories
+constexpr int kWgWC = kWgWaves / 2;
+constexpr int kWgNT = kWgN / kWgWC / 16;  // D tiles per wave along the trajectories
+constexpr int kWgThreads = 64 * kWgWaves;
+static_assert(kWgWaves == 4 || kWgWaves == 8, "wave layout");
 constexpr int kWgStageA = kWgM * kWgK * 2;   // bytes
 constexpr int kWgStageB = kWgN * kWgK * 2;
 constexpr int kWgEpi = kWgN * ((kWgU + 4) * 4 + 2 * (kWgU + 8) * 2);   // the epilogue's c / hi / lo tiles
@@ -56,11 +65,11 @@ __device__ __forceinline__ uint32_t wg_off(int r, int c) {
     else return (uint32_t)(r * 64 + ((c ^ ((r >> 1) & 3)) << 4));
 }
 
-__global__ __launch_bounds__(kWgThreads, 2) void wide_gemm_cell_kernel(WgArgs a) {
+__global__ __launch_bounds__(kWgThreads, 8 / kWgWaves) void wide_gemm_cell_kernel(WgArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wr = wv >> 2, wc = wv & 3;               // wave's 128-row half, 32-trajectory quarter
+    const int wr = wv / kWgWC, wc = wv % kWgWC;         // wave's 128-row half, trajectory slice
     const int H = a.H;
     // XCD-aware walk (consecutive workgroup ids go to different XCDs, each with its own L2): the ids an XCD
     // receives are renumbered contiguously and walk the unit blocks fastest, so a trajectory block's operand
@@ -95,6 +104,8 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_gemm_cell_kernel(WgArgs a)
         gB[i] = a.XB + (size_t)b * a.ldb + cch * 8;
         oB[i] = (uint32_t)kWgStageA + wg_off(r, cch);
     }
+    // one step ahead: step ks + 1's chunks are loaded into registers before step ks's MFMAs and stored to
+    // the other LDS stage after them (a second register set, two steps ahead, measured slower: 272 vs 259 us)
     u32x4 ra[NA], rb[NB];
     auto gload = [&](int ks) {
 #pragma unroll
@@ -110,9 +121,11 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_gemm_cell_kernel(WgArgs a)
         for (int i = 0; i < NB; ++i) *reinterpret_cast<u32x4 *>(base + oB[i]) = rb[i];
     };
 
-    f32x4 acc[8][2];
+    f32x4 acc[8][kWgNT];
 #pragma unroll
-    for (int m = 0; m < 8; ++m) acc[m][0] = acc[m][1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int n = 0; n < kWgNT; ++n) acc[m][n] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 
     // fragment reads: A tile m rows 128 wr + 16 m + (lane & 15), k chunk 4 kb + (lane >> 4); B likewise
     const int fr = lane & 15, fq = lane >> 4;
@@ -125,18 +138,18 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_gemm_cell_kernel(WgArgs a)
         const char *base = lds + buf * (kWgStageA + kWgStageB);
 #pragma unroll
         for (int kb = 0; kb < kWgK / 32; ++kb) {
-            f16x8 bf[2];
+            f16x8 bf[kWgNT];
 #pragma unroll
-            for (int n = 0; n < 2; ++n) {
-                const int r = 32 * wc + 16 * n + fr;
+            for (int n = 0; n < kWgNT; ++n) {
+                const int r = 16 * (kWgNT * wc + n) + fr;
                 bf[n] = *reinterpret_cast<const f16x8 *>(base + kWgStageA + wg_off(r, 4 * kb + fq));
             }
 #pragma unroll
             for (int m = 0; m < 8; ++m) {
                 const int r = 128 * wr + 16 * m + fr;
                 const f16x8 af = *reinterpret_cast<const f16x8 *>(base + wg_off(r, 4 * kb + fq));
-                acc[m][0] = mfma16(af, bf[0], acc[m][0]);
-                acc[m][1] = mfma16(af, bf[1], acc[m][1]);
+#pragma unroll
+                for (int n = 0; n < kWgNT; ++n) acc[m][n] = mfma16(af, bf[n], acc[m][n]);
             }
         }
         if (ks + 1 < nk) lstore(buf ^ 1);
@@ -144,7 +157,7 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_gemm_cell_kernel(WgArgs a)
     }
 
 #ifdef FCR_WG_NOEPI   // diagnostic: the mainloop alone (one store per tile keeps it live)
-    if (a.B < 0) for (int m = 0; m < 8; ++m) a.c_out[m] = acc[m][0][0] + acc[m][1][0];
+    if (a.B < 0) for (int m = 0; m < 8; ++m) a.c_out[m] = acc[m][0][0] + acc[m][kWgNT - 1][0];
     return;
 #endif
     // ---- epilogue: the cell update (wide_cell_kernel's arithmetic) on the accumulators, through LDS ----
@@ -157,12 +170,13 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_gemm_cell_kernel(WgArgs a)
     float *cs = reinterpret_cast<float *>(lds);                                   // [128][CSTR]
     _Float16 *hs = reinterpret_cast<_Float16 *>(lds + kWgN * CSTR * 4);           // [128][HSTR]
     _Float16 *ls = hs + kWgN * HSTR;                                              // [128][HSTR]
-    const int er = tid >> 4, ec = tid & 15;   // row-wise passes: 32 rows x 16 chunks per 512 threads
+    constexpr int ERS = kWgThreads / 16;      // row-wise passes: ERS rows x 16 chunks per pass
+    const int er = tid >> 4, ec = tid & 15;
     auto row_b = [&](int r) { return b0 + r; };
     if (a.c_prev) {
 #pragma unroll
-        for (int p = 0; p < kWgN / 32; ++p) {
-            const int r = er + 32 * p, b = row_b(r);
+        for (int p = 0; p < kWgN / ERS; ++p) {
+            const int r = er + ERS * p, b = row_b(r);
             if (b < a.B)
                 *reinterpret_cast<f32x4 *>(cs + r * CSTR + 4 * ec) =
                     *reinterpret_cast<const f32x4 *>(a.c_prev + (size_t)b * H + u0 + 4 * ec);
@@ -170,8 +184,8 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_gemm_cell_kernel(WgArgs a)
     }
     __syncthreads();
 #pragma unroll
-    for (int n = 0; n < 2; ++n) {
-        const int r = 32 * wc + 16 * n + fr;
+    for (int n = 0; n < kWgNT; ++n) {
+        const int r = 16 * (kWgNT * wc + n) + fr;
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
             const int ul = 32 * wr + 4 * m + fq;
@@ -190,8 +204,8 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_gemm_cell_kernel(WgArgs a)
     }
     __syncthreads();
 #pragma unroll
-    for (int p = 0; p < kWgN / 32; ++p) {
-        const int r = er + 32 * p, b = row_b(r);
+    for (int p = 0; p < kWgN / ERS; ++p) {
+        const int r = er + ERS * p, b = row_b(r);
         if (b >= a.B) continue;
         *reinterpret_cast<f32x4 *>(a.c_out + (size_t)b * H + u0 + 4 * ec) = *reinterpret_cast<const f32x4 *>(cs + r * CSTR + 4 * ec);
         if (ec < 8) {   // 8 chunks of 8 halves per row: the hi and lo halves of 64 units
@@ -216,13 +230,13 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_gemm_cell_kernel(WgArgs a)
         for (int gt = 0; gt < 4; ++gt) {
             __syncthreads();
 #pragma unroll
-            for (int n = 0; n < 2; ++n)
+            for (int n = 0; n < kWgNT; ++n)
 #pragma unroll
-                for (int m = 0; m < 8; ++m) cs[(32 * wc + 16 * n + fr) * CSTR + 32 * wr + 4 * m + fq] = acc[m][n][gt];
+                for (int m = 0; m < 8; ++m) cs[(16 * (kWgNT * wc + n) + fr) * CSTR + 32 * wr + 4 * m + fq] = acc[m][n][gt];
             __syncthreads();
 #pragma unroll
-            for (int p = 0; p < kWgN / 32; ++p) {
-                const int r = er + 32 * p, b = row_b(r);
+            for (int p = 0; p < kWgN / ERS; ++p) {
+                const int r = er + ERS * p, b = row_b(r);
                 if (b < a.B)
                     *reinterpret_cast<f32x4 *>(a.preact + (size_t)b * 4 * H + gt * H + u0 + 4 * ec) =
                         *reinterpret_cast<const f32x4 *>(cs + r * CSTR + 4 * ec);

@@ -32,8 +32,9 @@ struct WideArgs {
 };
 
 // layer 0's K = 5 window-row input as the last kX16 columns of its split-f16 operand rows and weights:
-// [x_hi (5) | x_lo (5) | x_hi (5) | 0] against [Wih_hi | Wih_hi | Wih_lo | 0]
-constexpr int kX16 = 16;
+// [x_hi (5) | x_lo (5) | x_hi (5) | 0] against [Wih_hi | Wih_hi | Wih_lo | 0]; 32 columns keep layer 0's K
+// (3H + kX16, or kX16 at t = 0) a whole number of the fused cell kernel's K steps (fcr_wgemm.h)
+constexpr int kX16 = 32;
 static_assert(3 * kIn < kX16, "layer-0 input split exceeds its padded block");
 // row stride of layer 0's operand rows [h part 3H | x part kX16], padded to whole 128-B lines (rows that
 // straddle lines cost the GEMM's operand loads)

@@ -245,10 +245,11 @@ def test_wide_path_any_incoming_gradient_scale(dloss):
         assert relerr(o[k] / dloss, c[f"{k}_64"]) <= TOL, (k, relerr(o[k] / dloss, c[f"{k}_64"]))
 
 
-@pytest.mark.parametrize("H,B,N", [(54, 300, 3), (57, 77, 2), (96, 520, 4)])
+@pytest.mark.parametrize("H,B,N", [(54, 300, 3), (57, 77, 2), (96, 520, 4), (64, 129, 2), (128, 300, 3)])
 def test_wide_path_hidden_sizes(H, B, N):
     """H > 52 at sizes the golden cases do not hit: even H not a multiple of 4 (cell kernels 2 units per
-    thread), odd H (1 unit per thread), and a multiple of 4 at a few hundred trajectories — the window-row
+    thread), odd H (1 unit per thread), a multiple of 4 at a few hundred trajectories, and multiples of 64
+    (the fused GEMM + cell kernel, fcr_wgemm.h) with a ragged last block of 128 trajectories — the window-row
     columns inside layer 0's split GEMM and the combined [input gradient | dh] backward products, against
     the fp64 oracle on seeded synthetic weights (parity unpinned: no reference output at these sizes)."""
     from tests.golden.make_golden import synth_params
