@@ -359,8 +359,12 @@ def main():
         fl = flops_per_rollout_step(H)
         dom = ("bwd", b_ms) if b_ms >= f_ms else ("fwd", f_ms)
         narrow = H <= 52
-        kernel = (f"fcr_s{dom[0]}_kernel" if small else f"fcr_{dom[0]}_kernel") if narrow else \
-            "wide path (split-f16 GEMMs + cell kernels)"
+        wide_label = {   # H > 52 (fcr_wide.h / fcr_wgemm.h); the fused cell kernel needs H % 64 == 0
+            "fwd": "wide_gemm_cell_kernel (hand-written split-f16 GEMM + cell update)" if H % 64 == 0 else
+                   "rocBLAS split-f16 gate GEMM + wide_cell_kernel",
+            "bwd": ("recompute wide_gemm_cell_kernel" if H % 64 == 0 else "recompute rocBLAS gate GEMM + wide_cell_kernel")
+                   + " + wide_cell_bwd_kernel + rocBLAS split-f16 [input grad | dh] and weight-gradient products"}
+        kernel = (f"fcr_s{dom[0]}_kernel" if small else f"fcr_{dom[0]}_kernel") if narrow else wide_label[dom[0]]
         achieved = B * N * fl[dom[0]] / (dom[1] * 1e-3) / 1e12
         hbm_roof = HBM_PEAK_GBS * 1e9 / hbm_bytes_per_rollout_step(N)
         default_cfg = (B, N, H, args.precision) == (65536, 10, 50, "fp32")

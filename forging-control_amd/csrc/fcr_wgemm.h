@@ -16,7 +16,10 @@
 // 72 KB of LDS (the epilogue's tiles) lets two workgroups share a CU, so one's epilogue and barriers
 // overlap the other's MFMAs. LDS rows are 64 B; their 16-B chunks are XOR-swizzled by (row >> 1) & 3, so
 // the 8 rows of a ds_read_b128 phase land on distinct 16-B bank groups. (8 waves x 128 x 32 measured the
-// same; K steps of 64 at one workgroup per CU 13 % slower.)
+// same; K steps of 64 at one workgroup per CU 13 % slower; B fragments loaded straight from global memory
+// into registers (64-B row pieces) 22 % slower; a second register set for a two-step prefetch 5 % slower.
+// Diagnostic builds bound the loop: cache-hot operand loads gain 6 %, no loads and LDS stores at all 33 %:
+// the staging (LDS write traffic and the wait before it), not HBM, is what the loop loses to.)
 #pragma once
 #include "fcr_common.h"
 #include "fcr_f16.h"
