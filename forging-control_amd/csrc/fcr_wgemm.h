@@ -19,7 +19,9 @@
 // same; K steps of 64 at one workgroup per CU 13 % slower; B fragments loaded straight from global memory
 // into registers (64-B row pieces) 22 % slower; a second register set for a two-step prefetch 5 % slower.
 // Diagnostic builds bound the loop: cache-hot operand loads gain 6 %, no loads and LDS stores at all 33 %:
-// the staging (LDS write traffic and the wait before it), not HBM, is what the loop loses to.)
+// the staging (LDS write traffic and the wait before it), not HBM, is what the loop loses to. The stages
+// are filled by LDS-DMA (global_load_lds, FCR_WG_DMA): 2 % faster than the register round trip; a 3-stage
+// ring with the next step's fragment reads overlapping the MFMAs measured 5 % slower.)
 #pragma once
 #include "fcr_common.h"
 #include "fcr_f16.h"
@@ -37,7 +39,10 @@ constexpr int kWgC = kWgK / 8;            // 16-B chunks per LDS row
 #ifndef FCR_WG_WAVES
 #define FCR_WG_WAVES 4
 #endif
-constexpr int kWgWaves = FCR_WG_WAVES;    // 2 x kWgWC waves; each 128 rows x kWgN / kWgWC trajectories
+constexpr int kWgWaves = FCR_WG_WAVES;
+#ifndef FCR_WG_DMA
+#define FCR_WG_DMA 1
+#endif    // 2 x kWgWC waves; each 128 rows x kWgN / kWgWC trajectories
 constexpr int kWgWC = kWgWaves / 2;
 constexpr int kWgNT = kWgN / kWgWC / 16;  // D tiles per wave along the trajectories
 constexpr int kWgThreads = 64 * kWgWaves;
@@ -45,8 +50,11 @@ static_assert(kWgWaves == 4 || kWgWaves == 8, "wave layout");
 constexpr int kWgStageA = kWgM * kWgK * 2;   // bytes
 constexpr int kWgStageB = kWgN * kWgK * 2;
 constexpr int kWgEpi = kWgN * ((kWgU + 4) * 4 + 2 * (kWgU + 8) * 2);   // the epilogue's c / hi / lo tiles
-constexpr int kWgLds = 2 * (kWgStageA + kWgStageB) > kWgEpi ? 2 * (kWgStageA + kWgStageB) : kWgEpi;
+constexpr int kWgStages = 2;
+constexpr int kWgLds = kWgStages * (kWgStageA + kWgStageB) > kWgEpi ? kWgStages * (kWgStageA + kWgStageB) : kWgEpi;
 static_assert(kWgK == 32 || kWgK == 64, "K step");
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 struct WgArgs {
     const _Float16 *A;     // [4H][lda]
@@ -84,8 +92,68 @@ __global__ __launch_bounds__(kWgThreads, 8 / kWgWaves) void wide_gemm_cell_kerne
     const int b0 = (wg / ny) * kWgN;                   // first trajectory
     const int nk = a.K / kWgK;
 
+#if FCR_WG_DMA
+    // LDS-DMA staging (global_load_lds, 16 B per lane): one wave instruction fills one 1 KB piece of a stage
+    // = 16 rows x 64 B; lane i lands at +16 i, i.e. row i >> 2, slot i & 3, so it fetches the global chunk
+    // that the row's swizzle puts in that slot. A stage is 16 A pieces + 8 B pieces, 6 per wave.
+    constexpr int NPC = (kWgStageA + kWgStageB) / 1024 / kWgWaves;
+    static_assert(kWgC == 4 && (kWgStageA + kWgStageB) % (1024 * kWgWaves) == 0, "DMA pieces");
+    const _Float16 *gsrc[NPC];
+    uint32_t ldst[NPC];
+#pragma unroll
+    for (int q = 0; q < NPC; ++q) {
+        const int j = wv + kWgWaves * q;                  // piece of the stage
+        const bool isA = j < kWgStageA / 1024;
+        const int r = 16 * (isA ? j : j - kWgStageA / 1024) + (lane >> 2);
+        const int c = (lane & 3) ^ ((r >> 1) & 3);
+        if (isA) {
+            gsrc[q] = a.A + (size_t)((r & 3) * H + u0 + (r >> 2)) * a.lda + 8 * c;
+        } else {
+            int b = b0 + r;
+            if (b >= a.B) b = a.B - 1;                     // tail rows recompute the last trajectory (not stored)
+            gsrc[q] = a.XB + (size_t)b * a.ldb + 8 * c;
+        }
+        ldst[q] = (uint32_t)j * 1024;
+    }
+    auto dma = [&](int ks, int buf) {
+#pragma unroll
+        for (int q = 0; q < NPC; ++q)
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(gsrc[q] + ks * kWgK),
+                (__attribute__((address_space(3))) void *)((__attribute__((address_space(3))) char *)lds +
+                                                           buf * (kWgStageA + kWgStageB) + ldst[q]),
+                16, 0, 0);
+    };
+
+    f32x4 acc[8][kWgNT];
+#pragma unroll
+    for (int m = 0; m < 8; ++m)
+#pragma unroll
+        for (int n = 0; n < kWgNT; ++n) acc[m][n] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    const int fr = lane & 15, fq = lane >> 4;
+    dma(0, 0);
+    for (int ks = 0; ks < nk; ++ks) {
+        const int buf = ks & 1;
+        // stage ks landed (every wave drains its own DMA; the barrier publishes them all), stage ks - 1
+        // retired. The wait is explicit: the compiler's LDS-DMA tracking is not relied on for it
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const char *base = lds + buf * (kWgStageA + kWgStageB);
+        f16x8 af[8], bf[kWgNT];
+#pragma unroll
+        for (int n = 0; n < kWgNT; ++n)
+            bf[n] = *reinterpret_cast<const f16x8 *>(base + kWgStageA + wg_off(16 * (kWgNT * wc + n) + fr, fq));
+#pragma unroll
+        for (int m = 0; m < 8; ++m) af[m] = *reinterpret_cast<const f16x8 *>(base + wg_off(128 * wr + 16 * m + fr, fq));
+        if (ks + 1 < nk) dma(ks + 1, buf ^ 1);   // after this step's reads: they need not wait for it
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+#pragma unroll
+            for (int n = 0; n < kWgNT; ++n) acc[m][n] = mfma16(af[m], bf[n], acc[m][n]);
+    }
+    __syncthreads();
+#else
     // global -> register chunk assignment: A 256 rows x kWgC chunks, XB 128 rows x kWgC chunks
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     constexpr int NA = kWgM * kWgC / kWgThreads, NB = kWgN * kWgC / kWgThreads, RS = kWgThreads / kWgC;
     const int cch = tid % kWgC;
     const _Float16 *gA[NA];
@@ -159,6 +227,7 @@ __global__ __launch_bounds__(kWgThreads, 8 / kWgWaves) void wide_gemm_cell_kerne
         __syncthreads();
     }
 
+#endif
 #ifdef FCR_WG_NOEPI   // diagnostic: the mainloop alone (one store per tile keeps it live)
     if (a.B < 0) for (int m = 0; m < 8; ++m) a.c_out[m] = acc[m][0][0] + acc[m][kWgNT - 1][0];
     return;
