@@ -45,8 +45,14 @@ int launch_check(const char *what) {
 // window-column scales of the f16 split's range guard (fcr_pack.h) -> wsc[8], from the call's inputs
 int launch_range(const fcr_dims *d, const float *states, const float *u0, const float *noise, const float *fcw,
                  const float *fcb, float *part, float *wsc, hipStream_t s) {
+    const size_t rows = (size_t)d->B * (d->N > kL ? d->N : kL);
+    if (rows <= 16 * kRangeThreads) {   // small batch: one block, the final step inside (one launch)
+        hipLaunchKernelGGL(range_partial_kernel, dim3(1), dim3(kRangeThreads), 0, s, states, u0, noise, d->B, d->N,
+                           part, fcw, fcb, d->H, wsc);
+        return launch_check("range_partial_kernel");
+    }
     hipLaunchKernelGGL(range_partial_kernel, dim3(kRangeBlocks), dim3(kRangeThreads), 0, s, states, u0, noise, d->B,
-                       d->N, part);
+                       d->N, part, nullptr, nullptr, 0, nullptr);
     int rc = launch_check("range_partial_kernel");
     if (rc) return rc;
     hipLaunchKernelGGL(range_final_kernel, dim3(1), dim3(64), 0, s, (const float *)part, kRangeBlocks, fcw, fcb, d->H,
@@ -467,6 +473,28 @@ int launch_cell_bwd(int B, int H, hipStream_t s, const float *act, const float *
 // Layers >= 1 of the split path: the cell's GEMM and update as one hand-written kernel (fcr_wgemm.h).
 // Off by default: its one-barrier 256 x 128 mainloop runs a cell in ~485 us where rocBLAS's GEMM + the cell
 // kernel take ~300 us (round 2, B = 65 536, H = 256; DESIGN.md §4 "Config 5"). Parity-tested when on.
+// The per-call weight packs (pack_fwd16_item, pack_img_item, pack_misc_item) as jobs of one launch:
+// block ranges in job order, 256 threads each, the same items the separate kernels ran
+enum { kPackFwd16 = 0, kPackImg = 1, kPackMisc = 2 };
+struct PackJob {
+    int kind, l, blocks;
+    _Float16 *dst;
+};
+struct PackAllArgs {
+    PackArgs a;
+    int njobs;
+    PackJob job[2 * kLayers + 1];
+};
+__global__ __launch_bounds__(256) void pack_all_kernel(PackAllArgs p) {
+    int b = blockIdx.x, j = 0;
+    while (j + 1 < p.njobs && b >= p.job[j].blocks) b -= p.job[j++].blocks;
+    const int idx = b * 256 + (int)threadIdx.x;
+    const PackJob &jb = p.job[j];
+    if (jb.kind == kPackFwd16) pack_fwd16_item(p.a, jb.l, jb.dst, idx);
+    else if (jb.kind == kPackImg) pack_img_item(p.a, jb.l, jb.dst, idx);
+    else pack_misc_item(p.a, idx);
+}
+
 #ifndef FCR_WIDE_FUSED
 #define FCR_WIDE_FUSED 1
 #endif
@@ -694,9 +722,12 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
     hipLaunchKernelGGL(wide_gu0_kernel, dim3(nb), dim3(256), 0, s, a, g_u0);
     if ((rc = launch_check("wide_gu0_kernel"))) return rc;
     float *part = (float *)(base + L.fnn_part);
+    const bool one = L.ctrl_blocks == 1;   // one block writes the gradients itself (grad_out5)
     hipLaunchKernelGGL(ctrl_grad_kernel, dim3(L.ctrl_blocks), dim3(kCtrlBlock), 0, s, X, (const float *)a.xhat,
-                       (const float *)a.dv, (const float *)(base + L.fnp), d->B, d->N, d->ctrl_hidden, part);
+                       (const float *)a.dv, (const float *)(base + L.fnp), d->B, d->N, d->ctrl_hidden, part,
+                       one ? g_w_inp : nullptr, one ? g_b_inp : nullptr, one ? g_w_out : nullptr);
     if ((rc = launch_check("ctrl_grad_kernel"))) return rc;
+    if (one) return FCR_OK;
     hipLaunchKernelGGL(grad_reduce_kernel, dim3(d->ctrl_hidden * 5), dim3(256), 0, s, (const float *)part,
                        L.ctrl_blocks, d->ctrl_hidden, g_w_inp, g_b_inp, g_w_out);
     return launch_check("grad_reduce_kernel");
@@ -914,20 +945,22 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
     pa.wsc = (const float *)(base + L.wsc);
     if ((rc = launch_range(d, states, u0, noise, w->fc_w, w->fc_b, (float *)(base + L.rng), (float *)(base + L.wsc), s)))
         return rc;
-    for (int l = 0; l < kLayers; ++l) {
-        const int nf = L.HS * (l == 0 ? (L.HS + 2 + 7) / 8 : (2 * L.HS + 7) / 8) * kWave * 8;   // per (tile, block, lane, k)
-        hipLaunchKernelGGL(pack_fwd16_kernel, dim3((nf + 255) / 256), dim3(256), 0, s, pa, l,
-                           (_Float16 *)(base + L.fa[l]));
-        if ((rc = launch_check("pack_fwd16_kernel"))) return rc;
-        if (with_backward) {
-            const int ni = img_pack_threads(L.HS, l);
-            hipLaunchKernelGGL(pack_img_kernel, dim3((ni + 255) / 256), dim3(256), 0, s, pa, l,
-                               (_Float16 *)(base + L.img[l]));
-            if ((rc = launch_check("pack_img_kernel"))) return rc;
+    {   // every weight pack of the call in ONE launch (seven launches of ~4 us each were a step's overhead
+        // at the reference's B = 15)
+        PackAllArgs pk{};
+        pk.a = pa;
+        for (int l = 0; l < kLayers; ++l) {
+            const int nf = L.HS * (l == 0 ? (L.HS + 2 + 7) / 8 : (2 * L.HS + 7) / 8) * kWave * 8;   // per (tile, block, lane, k)
+            pk.job[pk.njobs++] = PackJob{kPackFwd16, l, (nf + 255) / 256, (_Float16 *)(base + L.fa[l])};
+            if (with_backward)
+                pk.job[pk.njobs++] = PackJob{kPackImg, l, (img_pack_threads(L.HS, l) + 255) / 256, (_Float16 *)(base + L.img[l])};
         }
+        pk.job[pk.njobs++] = PackJob{kPackMisc, 0, 2, nullptr};
+        int blocks = 0;
+        for (int j = 0; j < pk.njobs; ++j) blocks += pk.job[j].blocks;
+        hipLaunchKernelGGL(pack_all_kernel, dim3(blocks), dim3(256), 0, s, pk);
+        if ((rc = launch_check("pack_all_kernel"))) return rc;
     }
-    hipLaunchKernelGGL(pack_misc_kernel, dim3(2), dim3(256), 0, s, pa);
-    if ((rc = launch_check("pack_misc_kernel"))) return rc;
 
     FwdArgs fa{};
     fa.B = d->B;
@@ -1022,9 +1055,12 @@ int fcr_backward(const fcr_dims *d, const float *X, const float *states, const f
     }
     if (rc) return rc;
     float *part = (float *)(base + L.fnn_part);
+    const bool one = L.ctrl_blocks == 1;   // one block writes the gradients itself (grad_out5)
     hipLaunchKernelGGL(ctrl_grad_kernel, dim3(L.ctrl_blocks), dim3(kCtrlBlock), 0, s, X, ba.xhat,
-                       (const float *)ba.dv, ba.p.fnp, d->B, d->N, d->ctrl_hidden, part);
+                       (const float *)ba.dv, ba.p.fnp, d->B, d->N, d->ctrl_hidden, part,
+                       one ? g_w_inp : nullptr, one ? g_b_inp : nullptr, one ? g_w_out : nullptr);
     if ((rc = launch_check("ctrl_grad_kernel"))) return rc;
+    if (one) return FCR_OK;
     hipLaunchKernelGGL(grad_reduce_kernel, dim3(d->ctrl_hidden * 5), dim3(256), 0, s, (const float *)part,
                        L.ctrl_blocks, d->ctrl_hidden, g_w_inp, g_b_inp, g_w_out);
     return launch_check("grad_reduce_kernel");
@@ -1171,9 +1207,12 @@ int fcr_fnn_backward(int32_t B, int32_t in_dim, int32_t hidden, const float *X, 
     hipStream_t s = (hipStream_t)stream;
     const int blocks = (int)((B + fnn::kFnnItems - 1) / fnn::kFnnItems);
     if (blocks) {
+        const bool one = blocks == 1;   // one block writes the gradients itself (grad_out5)
         hipLaunchKernelGGL(fnn::fnn_bwd_kernel, dim3(blocks), dim3(fnn::kFnnBlock), 0, s, B, hidden, X, w_inp, b_inp,
-                           w_out, g_u, g_x, (float *)ws);
+                           w_out, g_u, g_x, (float *)ws, one ? g_w_inp : nullptr, one ? g_b_inp : nullptr,
+                           one ? g_w_out : nullptr);
         if ((rc = launch_check("fnn_bwd_kernel"))) return rc;
+        if (one) return FCR_OK;
     }
     hipLaunchKernelGGL(grad_reduce_kernel, dim3(hidden * 5), dim3(256), 0, s, (const float *)ws, blocks, hidden,
                        g_w_inp, g_b_inp, g_w_out);

@@ -304,4 +304,20 @@ __device__ __forceinline__ float fnn_pre(const float *__restrict__ fnp, int q, f
     return xor_sum_q(part);
 }
 
+// Last store of a controller parameter-gradient kernel (ctrl_grad_kernel, fnn_bwd_kernel): the block's
+// partial [block][k][p] for grad_reduce_kernel, or — launched as one block, with the outputs given — the
+// gradient itself, as 0 + s: what grad_reduce_kernel's fixed-order sum makes of a single partial, bit for
+// bit, one launch fewer (small batches are launch-bound)
+__device__ __forceinline__ void grad_out5(float *part, int hidden, int k, int p, float s, float *gwi, float *gbi,
+                                          float *gwo) {
+    if (gwi) {
+        const float v = 0.0f + s;
+        if (p < 3) gwi[k * kCtrlIn + p] = v;
+        else if (p == 3) gbi[k] = v;
+        else gwo[k] = v;
+    } else {
+        part[((size_t)blockIdx.x * hidden + k) * 5 + p] = s;
+    }
+}
+
 }  // namespace fcr

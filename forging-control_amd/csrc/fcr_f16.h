@@ -444,13 +444,12 @@ __device__ __forceinline__ float fwd16_weight(const PackArgs &a, int l, int unit
 // lane>>4 (see the header). Scaled for exp2 as the pointwise expects. Split-major: every hi fragment of
 // the layer [r][kb], then every lo one [r][kb] (the f16 mode reads the first part); with a packed tail
 // (tail_packed) the hi part's last block of each tile is the packed tail fragment and it has no lo.
-__global__ void pack_fwd16_kernel(PackArgs a, int l, _Float16 *dst) {
+__device__ __forceinline__ void pack_fwd16_item(const PackArgs &a, int l, _Float16 *dst, int idx) {
     const int HS = a.HS;
     const int KB = l == 0 ? (HS + 2 + 7) / 8 : (2 * HS + 7) / 8;
     const bool tail = l > 0 && tail_packed(HS);
     const int KL = tail ? KB - 1 : KB;   // lo blocks per tile
     const int n = HS * KB * kWave * 8;
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= n) return;
     const int j = idx & 7, lane = (idx >> 3) & 63, rk = idx >> 9;
     const int kb = rk % KB, r = rk / KB;
@@ -472,6 +471,9 @@ __global__ void pack_fwd16_kernel(PackArgs a, int l, _Float16 *dst) {
     const size_t nq = (size_t)HS * KB;
     dst[((size_t)rk * kWave + lane) * 8 + j] = hi;
     dst[((nq + (size_t)r * KL + kb) * kWave + lane) * 8 + j] = lo;
+}
+__global__ void pack_fwd16_kernel(PackArgs a, int l, _Float16 *dst) {
+    pack_fwd16_item(a, l, dst, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 }  // namespace fcr

@@ -54,7 +54,8 @@ __global__ __launch_bounds__(kFnnBlock) void fnn_fwd_kernel(int B, int hidden, c
 __global__ __launch_bounds__(kFnnBlock) void fnn_bwd_kernel(int B, int hidden, const float *__restrict__ X,
                                                             const float *W, const float *bi, const float *wo,
                                                             const float *__restrict__ g, float *__restrict__ gX,
-                                                            float *__restrict__ part) {
+                                                            float *__restrict__ part, float *gwi = nullptr,
+                                                            float *gbi = nullptr, float *gwo = nullptr) {
     __shared__ float sp[kFnnMaxHidden][5];
     __shared__ float sx[3][kFnnItems], sd[kFnnItems];
     __shared__ float red[kFnnBlock / kWave][kFnnMaxHidden][5];
@@ -113,7 +114,7 @@ __global__ __launch_bounds__(kFnnBlock) void fnn_bwd_kernel(int B, int hidden, c
             float s = 0.0f;
 #pragma unroll
             for (int ww = 0; ww < kFnnBlock / kWave; ++ww) s += red[ww][lane][p];
-            part[((size_t)blockIdx.x * hidden + lane) * 5 + p] = s;
+            grad_out5(part, hidden, lane, p, s, gwi, gbi, gwo);
         }
     }
 }

@@ -64,13 +64,12 @@ inline int img_pack_threads(int HS, int l) { return 16 * HS * 4 * img_units(img_
 // σ = 2HS .. 2HS+3, the copies (hi σ0, hi σ1, lo σ0, lo σ1) of its two real slots, so the recompute's
 // row read of that block IS the packed tail fragment; the transposed product never reads those
 // columns as anything but unused output rows, and the lo image keeps zeros there.
-__global__ void pack_img_kernel(PackArgs a, int l, _Float16 *dst) {
+__device__ __forceinline__ void pack_img_item(const PackArgs &a, int l, _Float16 *dst, int idx) {
     const int H = a.H, HS = a.HS;
     const int nsl = l == 0 ? HS + 2 : 2 * HS;
     const int kbn = (nsl + 7) / 8;
     const int U = img_units(kbn), TU = img_tile_units(U);
     const int cols = 4 * U, rows = 16 * HS;
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= rows * cols) return;
     const int col = idx % cols, R = idx / cols;
     const int slot = R >> 4, m = R & 15;
@@ -116,6 +115,9 @@ __global__ void pack_img_kernel(PackArgs a, int l, _Float16 *dst) {
     const size_t off = ((size_t)slot * TU + img_row_start(m, U) + u) * 4 + (col & 3);   // in halves
     dst[off] = hi;
     dst[(size_t)HS * TU * 4 + off] = lo;
+}
+__global__ void pack_img_kernel(PackArgs a, int l, _Float16 *dst) {
+    pack_img_item(a, l, dst, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));

@@ -25,10 +25,61 @@ struct PackArgs {
 // unguarded one. Values whose scaled weights leave the f16 range (|v W| ~ 1e9 and beyond) are not covered.
 constexpr int kRangeBlocks = 128;
 constexpr int kRangeThreads = 256;
+// wsc[c] = 2^-s_c (c < 5; wsc[5..7] = 1) from the partial maxima and the readout's bound (see above)
+// One wave: the maxima over the partials across the lanes (max is order-free), the readout sums in their
+// serial order k = 0..H-1 on lane c with the loads batched ahead of the adds (a dependent load per term
+// made this 17 us at small batches, on the critical path of every step).
+__device__ __forceinline__ void range_final_wave(const float *__restrict__ part, int nblk,
+                                                 const float *__restrict__ fcw, const float *__restrict__ fcb,
+                                                 int H, float *wsc, int lane) {
+    float mc[kIn];
+#pragma unroll
+    for (int c = 0; c < kIn; ++c) {
+        float m = 0.0f;
+        for (int i = lane; i < nblk; i += 64) m = fmaxf(m, part[i * 8 + c]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        mc[c] = m;
+    }
+    if (lane >= 8) return;
+    float sc = 1.0f;
+    if (lane < kIn) {
+        float m = mc[0];
+#pragma unroll
+        for (int c = 1; c < kIn; ++c)
+            if (lane == c) m = mc[c];
+        if (lane < kOut) {
+            float s = fabsf(fcb[lane]);
+            const float *w = fcw + lane * H;
+            int k = 0;
+            for (; k + 8 <= H; k += 8) {
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = w[k + j];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) s += fabsf(v[j]);
+            }
+            for (; k < H; ++k) s += fabsf(w[k]);
+            m += s;
+        } else {
+            m = fmaxf(m, 1.0f);
+        }
+        if (isfinite(m) && m >= 16384.0f) sc = __builtin_amdgcn_ldexpf(1.0f, 14 - __builtin_amdgcn_frexp_expf(m));
+    }
+    wsc[lane] = sc;
+}
+__global__ __launch_bounds__(64) void range_final_kernel(const float *__restrict__ part, int nblk,
+                                                         const float *__restrict__ fcw,
+                                                         const float *__restrict__ fcb, int H, float *wsc) {
+    range_final_wave(part, nblk, fcw, fcb, H, wsc, threadIdx.x);
+}
+
 __global__ __launch_bounds__(kRangeThreads) void range_partial_kernel(const float *__restrict__ states,
                                                                       const float *__restrict__ u0,
                                                                       const float *__restrict__ noise, int B, int N,
-                                                                      float *part) {
+                                                                      float *part, const float *fcw = nullptr,
+                                                                      const float *fcb = nullptr, int H = 0,
+                                                                      float *wsc = nullptr) {
     __shared__ float red[kIn][kRangeThreads];
     float m0 = 0.0f, m1 = 0.0f, m2 = 0.0f, m3 = 0.0f, m4 = 0.0f;
     const size_t stride = (size_t)gridDim.x * blockDim.x, tid0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -62,31 +113,13 @@ __global__ __launch_bounds__(kRangeThreads) void range_partial_kernel(const floa
         __syncthreads();
     }
     if (threadIdx.x < kIn) part[blockIdx.x * 8 + threadIdx.x] = red[threadIdx.x][0];
-}
-
-// wsc[c] = 2^-s_c (c < 5; wsc[5..7] = 1) from the partial maxima and the readout's bound (see above)
-__global__ void range_final_kernel(const float *__restrict__ part, int nblk, const float *__restrict__ fcw,
-                                   const float *__restrict__ fcb, int H, float *wsc) {
-    const int c = threadIdx.x;
-    if (c >= 8) return;
-    float sc = 1.0f;
-    if (c < kIn) {
-        float m = 0.0f;
-        for (int i = 0; i < nblk; ++i) m = fmaxf(m, part[i * 8 + c]);
-        if (c < kOut) {
-            float s = fabsf(fcb[c]);
-            for (int k = 0; k < H; ++k) s += fabsf(fcw[c * H + k]);
-            m += s;
-        } else {
-            m = fmaxf(m, 1.0f);
-        }
-        if (isfinite(m) && m >= 16384.0f) sc = __builtin_amdgcn_ldexpf(1.0f, 14 - __builtin_amdgcn_frexp_expf(m));
+    if (wsc) {   // launched as one block: the final step too (range_final_kernel's, one launch fewer)
+        __syncthreads();
+        if (threadIdx.x < 64) range_final_wave(part, 1, fcw, fcb, H, wsc, threadIdx.x);
     }
-    wsc[c] = sc;
 }
 
-__global__ void pack_misc_kernel(PackArgs a) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void pack_misc_item(const PackArgs &a, int idx) {
     const int H = a.H, HS = a.HS;
     const int nfc = kOut * HS * 4;
     if (idx < nfc) {
@@ -108,6 +141,7 @@ __global__ void pack_misc_kernel(PackArgs a) {
         a.fnp[idx] = v;
     }
 }
+__global__ void pack_misc_kernel(PackArgs a) { pack_misc_item(a, blockIdx.x * blockDim.x + threadIdx.x); }
 
 // loss = sum(loss_part[0..nw)) / B, fixed order (one block)
 __global__ void loss_reduce_kernel(const float *part, int nw, int B, float *loss) {
@@ -131,7 +165,8 @@ constexpr int kCtrlBlock = 256;
 constexpr int kCtrlItems = 1024;   // items per block
 __global__ __launch_bounds__(kCtrlBlock) void ctrl_grad_kernel(const float *X, const float *xhat, const float *dv,
                                                                const float *fnp, int B, int N, int hidden,
-                                                               float *part) {
+                                                               float *part, float *gwi = nullptr,
+                                                               float *gbi = nullptr, float *gwo = nullptr) {
     __shared__ float sx0[kCtrlItems], sx3[kCtrlItems], sref[kCtrlItems], sdv[kCtrlItems];
     __shared__ float red[kCtrlBlock / kWave][64][5];
     const long long items = (long long)B * N;
@@ -172,7 +207,7 @@ __global__ __launch_bounds__(kCtrlBlock) void ctrl_grad_kernel(const float *X, c
             float s = 0.0f;
 #pragma unroll
             for (int ww = 0; ww < kCtrlBlock / kWave; ++ww) s += red[ww][lane][p];
-            part[((size_t)blockIdx.x * hidden + k) * 5 + p] = s;
+            grad_out5(part, hidden, k, p, s, gwi, gbi, gwo);
         }
     }
 }
