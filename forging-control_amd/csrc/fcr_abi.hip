@@ -458,21 +458,22 @@ int launch_cell(int B, int H, hipStream_t s, const float *G, const float *c_prev
 template <bool PRE>
 int launch_cell_bwd(int B, int H, hipStream_t s, const float *act, const float *c, const float *c_prev,
                     const float *dH, const float *din, float *dC, float *dG, _Float16 *dgsp, const float *consts,
-                    int dh_scaled, int ldh, int ldx) {
+                    int dh_scaled, int ldh, int ldx, const float *wih0 = nullptr, float *rowg = nullptr) {
     const int V = cell_vec(H);
     const dim3 grid((unsigned)(((size_t)B * (H / V) + 255) / 256)), blk(256);
+    if (rowg && (V != 4 || 64 % (H / V)))
+        return fail(FCR_EINVAL, "wide_cell_bwd_kernel: in-kernel row gradient needs 64 %% (H / 4) == 0 (H = %d)", H);
     if (V == 4)
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H);
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, wih0, rowg);
     else if (V == 2)
         hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 2>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H);
     else
         hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 1>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H);
     return launch_check("wide_cell_bwd_kernel");
 }
+// the in-kernel layer-0 row gradient applies when a trajectory's cell threads (H / 4) tile a wave
+inline bool rowg_in_cell(int H) { return cell_vec(H) == 4 && 64 % (H / 4) == 0; }
 
-// Layers >= 1 of the split path: the cell's GEMM and update as one hand-written kernel (fcr_wgemm.h).
-// Off by default: its one-barrier 256 x 128 mainloop runs a cell in ~485 us where rocBLAS's GEMM + the cell
-// kernel take ~300 us (round 2, B = 65 536, H = 256; DESIGN.md §4 "Config 5"). Parity-tested when on.
 // The per-call weight packs (pack_fwd16_item, pack_img_item, pack_misc_item) as jobs of one launch:
 // block ranges in job order, 256 threads each, the same items the separate kernels ran
 enum { kPackFwd16 = 0, kPackImg = 1, kPackMisc = 2 };
@@ -495,6 +496,9 @@ __global__ __launch_bounds__(256) void pack_all_kernel(PackAllArgs p) {
     else pack_misc_item(p.a, idx);
 }
 
+// The split path's forward cells (every layer, H % 64 == 0): the cell's GEMM and update as one hand-written
+// kernel (fcr_wgemm.h): 262 us per cell against ~300 us for rocBLAS's GEMM + wide_cell_kernel (B = 65 536,
+// H = 256; DESIGN.md "Config 5"). FCR_WIDE_FUSED=0 builds the rocBLAS path for comparison.
 #ifndef FCR_WIDE_FUSED
 #define FCR_WIDE_FUSED 1
 #endif
@@ -696,16 +700,20 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
                 // >= 1 columns H..2H-1 of D[l-1] row t+1; the layer above's input gradient from D[l] row t
                 const float *dh_src = t == kL - 1 ? a.dH : l == 0 ? sp.E0 : D[l - 1] + (size_t)(t + 1) * 2 * cell + H;
                 const int ldh = t == kL - 1 ? H : l == 0 ? LE : 2 * H;
+                const bool rg = l == 0 && rowg_in_cell(H);   // layer 0's row gradient from the cell kernel
                 if ((rc = launch_cell_bwd<true>(B, H, s, a.Act + c_off * 4, a.Cs + c_off, t > 0 ? a.Cs + c_off - cell : nullptr,
                                                 dh_src, l < kLayers - 1 ? D[l] + (size_t)t * 2 * cell : nullptr, a.dC,
                                                 nullptr, sp.dGsp, sp.consts,
                                                 l < kLayers - 1 || t < kL - 1,   // (2, 9): the head's dH
-                                                ldh, 2 * H)))
+                                                ldh, 2 * H, rg ? wih[0] : nullptr,
+                                                rg ? a.rowg + (size_t)(j + t) * B * kIn : nullptr)))
                     return rc;
                 if (l > 0) {   // [input gradient | dh_{t-1}] (t = 0: the former only) into D[l-1] row t
                     if ((rc = gemm16_bwd(h, B, t > 0 ? 2 * H : H, H, sp.bih[l], 2 * H, sp.dGsp, D[l - 1] + (size_t)t * 2 * cell,
                                          2 * H)))
                         return rc;
+                } else if (rg) {   // layer 0, row gradient done: dh_{t-1} only (t = 0: nothing)
+                    if (t > 0 && (rc = gemm16_bwd(h, B, H, H, sp.bx0, H8, sp.dGsp, sp.E0, LE))) return rc;
                 } else {
                     // layer 0: [dh_{t-1} | window-row gradient] in one product (t = 0: the latter only), then the
                     // row gradient into rowg row j + t

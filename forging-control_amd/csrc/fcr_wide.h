@@ -277,7 +277,7 @@ __global__ void wide_cell_bwd_kernel(const float *__restrict__ act, const float 
                                      const float *__restrict__ c_prev, const float *__restrict__ dH,
                                      const float *__restrict__ din, float *dC, float *dG, _Float16 *dgsp,
                                      const float *__restrict__ consts, int dh_scaled, int ldh, int ldx, int B,
-                                     int H) {
+                                     int H, const float *__restrict__ wih0 = nullptr, float *rowg = nullptr) {
     using W = WideVec<V>;
     // with consts (split-f16 rollout) din, and dH unless it is the head's, come from gemm16_bwd in the
     // scaled units of the dgates: back by 1/scale = consts[0], one fp32 product each
@@ -328,6 +328,38 @@ __global__ void wide_cell_bwd_kernel(const float *__restrict__ act, const float 
         }
     }
     W::st(dC + idx, dco);
+    if (rowg) {   // layer 0: the window-row gradient sum_r dG[b][r] W_ih0[r][c] (c < kIn), fp32 from these
+        // dgates, reduced over the trajectory's H / V threads (one aligned segment of a wave: the host checks
+        // 64 % (H / V) == 0) — in place of kIn + 3 more columns in the backward product
+        static_assert(V * kIn % 4 == 0 || V == 1 || V == 2, "row block in 16-B pieces");
+        float pc[kIn] = {};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            // V consecutive rows of kIn floats: V * kIn / 4 16-B loads (80 B at V = 4, 16-B aligned as u % 4 == 0)
+            float wr[V * kIn];
+            if constexpr (V == 4) {
+                const f32x4 *w4 = reinterpret_cast<const f32x4 *>(wih0 + ((size_t)k * H + u) * kIn);
+#pragma unroll
+                for (int q = 0; q < V * kIn / 4; ++q) {
+                    const f32x4 v = w4[q];
+                    wr[4 * q] = v[0]; wr[4 * q + 1] = v[1]; wr[4 * q + 2] = v[2]; wr[4 * q + 3] = v[3];
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < V * kIn; ++q) wr[q] = wih0[((size_t)k * H + u) * kIn + q];
+            }
+#pragma unroll
+            for (int e = 0; e < V; ++e)
+#pragma unroll
+                for (int c = 0; c < kIn; ++c) pc[c] = fmaf(dg[k][e], wr[e * kIn + c], pc[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < kIn; ++c)
+            for (int o = 1; o < HV; o <<= 1) pc[c] += __shfl_xor(pc[c], o);
+        if (u == 0)
+#pragma unroll
+            for (int c = 0; c < kIn; ++c) rowg[b * kIn + c] += pc[c];
+    }
 }
 
 // Split-f16 operands of the config-5 gate GEMMs (fp32-accurate on the matrix cores, as fcr_f16.h does
