@@ -21,7 +21,8 @@ ERRORS = {-1: "FCR_EINVAL", -2: "FCR_EWORKSPACE", -3: "FCR_EHIP", -4: "FCR_EUNSU
 # Every symbol include/fcr.h declares (tests check the .so exports exactly these).
 EXPORTS = ("fcr_workspace_size", "fcr_forward", "fcr_backward", "fcr_lstm_workspace_size", "fcr_lstm_forward",
            "fcr_lstm_backward", "fcr_plant_rk4", "fcr_closed_loop_run", "fcr_window_gather", "fcr_fnn_workspace_size",
-           "fcr_fnn_forward", "fcr_fnn_backward", "fcr_set_small_batch_limit", "fcr_last_error", "fcr_abi_version")
+           "fcr_fnn_forward", "fcr_fnn_backward", "fcr_set_small_batch_limit", "fcr_set_wide_keep_budget", "fcr_last_error",
+           "fcr_abi_version")
 
 
 class FcrDims(ctypes.Structure):
@@ -109,6 +110,8 @@ def load() -> ctypes.CDLL:
         lib.fcr_fnn_backward.restype = i32
         lib.fcr_set_small_batch_limit.argtypes = [i32]
         lib.fcr_set_small_batch_limit.restype = i32
+        lib.fcr_set_wide_keep_budget.argtypes = [ctypes.c_int64]
+        lib.fcr_set_wide_keep_budget.restype = ctypes.c_int64
         lib.fcr_last_error.argtypes = []
         lib.fcr_last_error.restype = ctypes.c_char_p
         lib.fcr_abi_version.argtypes = []
@@ -128,6 +131,13 @@ def check(rc: int, what: str) -> None:
 def set_small_batch_limit(max_batch: int) -> int:
     """fcr_set_small_batch_limit: B <= max_batch runs the small-batch kernels (0 = never); returns the old limit."""
     return int(load().fcr_set_small_batch_limit(int(max_batch)))
+
+
+def set_wide_keep_budget(nbytes: int) -> int:
+    """fcr_set_wide_keep_budget (H > 52): bytes of kept windows a backward-enabled workspace may add, so their
+    backward skips the recompute (< 0 = default: the workspace within 60 % of the device; 0 = none);
+    returns the old budget. Per calling thread."""
+    return int(load().fcr_set_wide_keep_budget(int(nbytes)))
 
 
 def small_batch_limit() -> int:

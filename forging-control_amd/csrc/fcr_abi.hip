@@ -246,10 +246,14 @@ struct WideLayout {
     // operand rows XB [3][10][B][6H] (layer 0 rows 3H + kX16 long), the dgate rows [B][12H])
     size_t fa[3], bih[3], XB, dGsp, consts;   // bih: layers >= 1 backward A [12H][2H]
     size_t bx0, E0;   // layer 0's backward A [12H][H + 8] and its product rows [B][H + 8]
+    // kept windows (the last `keep` of N): the forward's gate pre-activations and c per cell
+    // [keep][3][10][B][4H] / [keep][3][10][B][H], so the backward skips their recompute (wide_keep_fit)
+    size_t KA, KC;
+    int keep;
     int ctrl_blocks;
 };
 
-WideLayout make_wide(const fcr_dims *d, int with_backward) {
+WideLayout make_wide(const fcr_dims *d, int with_backward, int keep = 0) {
     WideLayout L{};
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -305,10 +309,32 @@ WideLayout make_wide(const fcr_dims *d, int with_backward) {
         L.dv = take(F * B * N);
         L.ctrl_blocks = (int)(((long long)B * N + kCtrlItems - 1) / kCtrlItems);
         L.fnn_part = take(F * (size_t)L.ctrl_blocks * d->ctrl_hidden * 5);
+        if (keep > 0) {
+            L.keep = keep;
+            L.KA = take(F * (size_t)keep * kLayers * kL * B * 4 * H);
+            L.KC = take(F * (size_t)keep * kLayers * kL * B * H);
+        }
     }
     L.total = off;
     return L;
 }
+
+// The number of kept windows a workspace of ws_bytes holds (the most that fit): the forward and the
+// backward each derive it from the ws_bytes they are given, so they agree with no state between them.
+int wide_keep_fit(const fcr_dims *d, size_t ws_bytes) {
+    for (int k = d->N; k > 0; --k)
+        if (make_wide(d, 1, k).total <= ws_bytes) return k;
+    return 0;
+}
+// a kept window's slabs (window j of the last L.keep)
+float *kept_act(const WideLayout &L, char *base, const fcr_dims *d, int j) {
+    return (float *)(base + L.KA) + (size_t)(j - (d->N - L.keep)) * kLayers * kL * d->B * 4 * d->H;
+}
+float *kept_c(const WideLayout &L, char *base, const fcr_dims *d, int j) {
+    return (float *)(base + L.KC) + (size_t)(j - (d->N - L.keep)) * kLayers * kL * d->B * d->H;
+}
+// fcr_set_wide_keep_budget: bytes of kept windows fcr_workspace_size may add; < 0 = up to 60 % of the device
+thread_local long long g_wide_keep_budget = -1;
 
 rocblas_handle blas_on(hipStream_t s) {
     thread_local rocblas_handle h = nullptr;
@@ -590,8 +616,8 @@ int wide_cells(rocblas_handle h, const WideArgs &a, const float *const *w_ih, co
 
 int wide_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const float *u0, const float *states,
                  const float *noise, float *loss, float *cost, float *command, float *error, float *prediction,
-                 float *xhat, int with_backward, char *base, hipStream_t s) {
-    const WideLayout L = make_wide(d, with_backward);
+                 float *xhat, int with_backward, char *base, size_t ws_bytes, hipStream_t s) {
+    const WideLayout L = make_wide(d, with_backward, with_backward ? wide_keep_fit(d, ws_bytes) : 0);
     const size_t H = d->H, F = sizeof(float);
     int rc;
     // private copies of every parameter the backward needs (fcr_backward takes no weights)
@@ -643,7 +669,14 @@ int wide_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const 
     for (int j = 0; j < d->N; ++j) {
         hipLaunchKernelGGL(wide_window_kernel<true>, dim3(nb), dim3(256), 0, s, a, j);
         if ((rc = launch_check("wide_window_kernel"))) return rc;
-        if ((rc = wide_cells(h, a, wih, whh, false, &sp, s))) return rc;
+        if (j >= d->N - L.keep) {   // kept window: pre-activations and c into its own slabs for the backward
+            WideArgs ak = a;
+            ak.Act = kept_act(L, base, d, j);
+            ak.Cs = kept_c(L, base, d, j);
+            if ((rc = wide_cells(h, ak, wih, whh, true, &sp, s))) return rc;
+        } else if ((rc = wide_cells(h, a, wih, whh, false, &sp, s))) {
+            return rc;
+        }
         hipLaunchKernelGGL(wide_readout_kernel, dim3((unsigned)(((size_t)d->B * kRoLanes + 255) / 256)), dim3(256), 0, s, a, j,
                            (const float *)(a.Hs + ((size_t)2 * kL + kL - 1) * d->B * H));
         if ((rc = launch_check("wide_readout_kernel"))) return rc;
@@ -656,8 +689,8 @@ int wide_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const 
 
 int wide_backward(const fcr_dims *d, const float *X, const float *states, const float *prediction,
                   const float *dloss, float *g_u0, float *g_w_inp, float *g_b_inp, float *g_w_out, char *base,
-                  hipStream_t s) {
-    const WideLayout L = make_wide(d, 1);
+                  size_t ws_bytes, hipStream_t s) {
+    const WideLayout L = make_wide(d, 1, wide_keep_fit(d, ws_bytes));
     const int B = d->B, H = d->H, H8 = H + 8;
     const int LE = (H8 + 31) / 32 * 32;   // E0 rows padded to whole 128-B lines
     const size_t cell = (size_t)B * H;
@@ -687,9 +720,16 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
     for (int j = d->N - 1; j >= 0; --j) {
         hipLaunchKernelGGL(wide_head_kernel, dim3((unsigned)(((size_t)B * kRoLanes + 255) / 256)), dim3(256), 0, s, a, j);
         if ((rc = launch_check("wide_head_kernel"))) return rc;
-        hipLaunchKernelGGL(wide_window_kernel<false>, dim3(nb), dim3(256), 0, s, a, j);
-        if ((rc = launch_check("wide_window_kernel"))) return rc;
-        if ((rc = wide_cells(h, a, wih, whh, true, &sp, s))) return rc;   // checkpoint: recompute the window
+        if (j >= d->N - L.keep) {   // kept by the forward: no recompute
+            a.Act = kept_act(L, base, d, j);
+            a.Cs = kept_c(L, base, d, j);
+        } else {
+            a.Act = (float *)(base + L.Act);
+            a.Cs = (float *)(base + L.Cs);
+            hipLaunchKernelGGL(wide_window_kernel<false>, dim3(nb), dim3(256), 0, s, a, j);
+            if ((rc = launch_check("wide_window_kernel"))) return rc;
+            if ((rc = wide_cells(h, a, wih, whh, true, &sp, s))) return rc;   // checkpoint: recompute the window
+        }
         for (int l = kLayers - 1; l >= 0; --l) {
             if (l < kLayers - 1 && hipMemsetAsync(a.dH, 0, sizeof(float) * cell, s) != hipSuccess)
                 return fail(FCR_EHIP, "hipMemsetAsync failed");
@@ -893,6 +933,12 @@ int fcr_set_small_batch_limit(int32_t max_batch) {
     return prev;
 }
 
+int64_t fcr_set_wide_keep_budget(int64_t bytes) {
+    const long long prev = g_wide_keep_budget;
+    g_wide_keep_budget = bytes < 0 ? -1 : bytes;
+    return prev;
+}
+
 #if FCR_STAMP
 // diagnostic builds: byte offset (in ws) of the per-wave cycle sums [nw_pad][8] of the backward
 size_t fcr_debug_stamp_offset(const fcr_dims *d) { return make_layout(d, 1).stamp; }
@@ -904,7 +950,23 @@ int fcr_workspace_size(const fcr_dims *dims, int with_backward, size_t *bytes) {
     int rc = check_dims(dims);
     if (rc) return rc;
     if (!bytes) return fail(FCR_EINVAL, "bytes is NULL");
-    *bytes = is_wide(dims) ? make_wide(dims, with_backward).total : make_layout(dims, with_backward).total;
+    if (!is_wide(dims)) {
+        *bytes = make_layout(dims, with_backward).total;
+        return FCR_OK;
+    }
+    int keep = 0;
+    if (with_backward) {   // kept windows within the budget (fcr_set_wide_keep_budget)
+        const size_t base = make_wide(dims, 1, 0).total;
+        long long budget = g_wide_keep_budget;
+        if (budget < 0) {   // default: the whole workspace within 60 % of the device's memory (its TOTAL, not
+            // what is free now — torch's cache holds the last call's workspace, and the count must not drift)
+            size_t free_b = 0, total_b = 0;
+            const long long cap = hipMemGetInfo(&free_b, &total_b) == hipSuccess ? (long long)(total_b / 10 * 6) : 0;
+            budget = cap > (long long)base ? cap - (long long)base : 0;
+        }
+        while (keep < dims->N && make_wide(dims, 1, keep + 1).total - base <= (size_t)budget) ++keep;
+    }
+    *bytes = make_wide(dims, with_backward, keep).total;
     return FCR_OK;
 }
 
@@ -926,7 +988,7 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
         const size_t need = make_wide(d, with_backward).total;
         if (ws_bytes < need) return fail(FCR_EWORKSPACE, "fcr_forward: ws has %zu bytes, needs %zu", ws_bytes, need);
         return wide_forward(d, w, X, u0, states, noise, loss, cost, command, error, prediction, xhat, with_backward,
-                            (char *)ws, (hipStream_t)stream);
+                            (char *)ws, ws_bytes, (hipStream_t)stream);
     }
     const Layout L = make_layout(d, with_backward);
     if (ws_bytes < L.total)
@@ -1022,7 +1084,7 @@ int fcr_backward(const fcr_dims *d, const float *X, const float *states, const f
     if (is_wide(d)) {
         const size_t need = make_wide(d, 1).total;
         if (ws_bytes < need) return fail(FCR_EWORKSPACE, "fcr_backward: ws has %zu bytes, needs %zu", ws_bytes, need);
-        return wide_backward(d, X, states, prediction, dloss, g_u0, g_w_inp, g_b_inp, g_w_out, (char *)ws,
+        return wide_backward(d, X, states, prediction, dloss, g_u0, g_w_inp, g_b_inp, g_w_out, (char *)ws, ws_bytes,
                              (hipStream_t)stream);
     }
     const Layout L = make_layout(d, 1);

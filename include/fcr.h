@@ -232,6 +232,19 @@ int fcr_lstm_backward(const fcr_dims *dims, const fcr_weights *w, const float *d
  */
 int fcr_set_small_batch_limit(int32_t max_batch);
 
+/*
+ * H > 52 (the batch-wide GEMM path): how many bytes of "kept windows" fcr_workspace_size(with_backward = 1)
+ * may add. The backward recomputes each window's cells from a per-window checkpoint (the rollout's memory
+ * floor); a kept window instead holds the forward's gate pre-activations and c for all its 30 cells
+ * (30 B 5H floats: 10 GB at B = 65 536, H = 256 — torch's autograd keeps at least that for every window),
+ * so its backward skips the recompute (config 5: a third of the step). The last windows are kept, as many
+ * as the budget allows; fcr_forward / fcr_backward derive the count from the ws_bytes they are given.
+ * bytes < 0 (default): as many as keep the whole workspace within 60 % of the device's total memory
+ * (a stable count from call to call); 0: keep none.
+ * Per calling thread. Returns the previous budget.
+ */
+int64_t fcr_set_wide_keep_budget(int64_t bytes);
+
 /* Thread-local description of the last error (never NULL). */
 const char *fcr_last_error(void);
 

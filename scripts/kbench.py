@@ -43,6 +43,8 @@ def main(return_state=False):
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--sustain", type=int, default=0, help="then time this many back-to-back launches per lib")
     ap.add_argument("--precision", type=int, default=0, help="0 = fp32-accurate, 1 = f16 (config 3)")
+    ap.add_argument("--keep-budget", type=int, default=None,
+                    help="fcr_set_wide_keep_budget bytes (H > 52: kept windows skip the backward recompute)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     B, N, H = a.batch, a.horizon, a.hidden
@@ -61,10 +63,15 @@ def main(return_state=False):
     libs = [bind(p) for p in a.libs]
     need = []
     for lib in libs:
+        if a.keep_budget is not None and hasattr(lib, "fcr_set_wide_keep_budget"):
+            lib.fcr_set_wide_keep_budget.argtypes = [ctypes.c_int64]
+            lib.fcr_set_wide_keep_budget.restype = ctypes.c_int64
+            lib.fcr_set_wide_keep_budget(a.keep_budget)
         nb = ctypes.c_size_t()
         lib.fcr_workspace_size(ctypes.byref(dims), 1, ctypes.byref(nb))
         need.append(nb.value)
     nbytes = ctypes.c_size_t(max(need))
+    print(f"# workspace {nbytes.value / 2**30:.1f} GiB", flush=True)
     ws = torch.empty(nbytes.value, dtype=torch.uint8, device=dev)
     f32 = dict(dtype=torch.float32, device=dev)
     outs = {k: torch.empty(s, **f32) for k, s in

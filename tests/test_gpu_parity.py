@@ -266,6 +266,34 @@ def test_wide_path_hidden_sizes(H, B, N):
         assert relerr(o[k], g[k]) <= TOL, (H, k, relerr(o[k], g[k]))
 
 
+def test_wide_path_kept_windows_equal_recompute():
+    """H > 52: windows whose cell state the forward keeps (fcr_set_wide_keep_budget) skip the backward's
+    recompute; the kept pre-activations and c are the recompute's, so every output and gradient is the same
+    bit for bit with none, one or all windows kept, and all match the fp64 oracle."""
+    from tests.golden.make_golden import synth_params
+    H, B, N = 64, 200, 4
+    params = synth_params(H, 364)
+    X, S, _ = _synth(B, N, 464)
+    u0 = _u0(params, X)
+    outs = []
+    try:
+        for budget in (0, 1, 1 << 40):   # none; smaller than one window (none); all windows
+            fca._native.set_wide_keep_budget(budget)
+            outs.append(run(params, X, u0, S, N, 20.0))
+        per_window = 4 * 3 * 10 * B * 5 * H   # bytes of one kept window
+        fca._native.set_wide_keep_budget(per_window + 4096)   # exactly one window (the last)
+        outs.append(run(params, X, u0, S, N, 20.0))
+    finally:
+        fca._native.set_wide_keep_budget(-1)
+    for o in outs[1:]:
+        for k in FEATS + ("xhat",) + tuple(k for k, _ in GRADS):
+            assert np.array_equal(o[k], outs[0][k]), k
+    _, f, tape = R.rollout_forward(params, X, u0, S, N, 20.0)
+    g = R.rollout_backward(params, tape)
+    for k, _ in GRADS:
+        assert relerr(outs[2][k], g[k]) <= TOL, (k, relerr(outs[2][k], g[k]))
+
+
 @pytest.mark.parametrize("case", ["ref_b15_n10", "h64_b24_n3"])
 def test_nonfinite_incoming_gradient_propagates(case):
     """A non-finite upstream gradient (an overflowed loss scale) must come out non-finite, as torch's does —
