@@ -49,7 +49,16 @@ class RolloutFn(torch.autograd.Function):
         H = w_hh0.shape[1]
         dims = make_dims(B, N, H, 3, W_inp.shape[0], alpha, precision=precision)
         need_grad = any(ctx.needs_input_grad[i] for i in (1, 4, 5, 6))
-        ws = torch.empty(_native.workspace_bytes(dims, need_grad), dtype=torch.uint8, device=dev)
+        try:
+            ws = torch.empty(_native.workspace_bytes(dims, need_grad), dtype=torch.uint8, device=dev)
+        except torch.cuda.OutOfMemoryError:
+            # H > 52: the kept windows (fcr_set_wide_keep_budget) did not fit beside the caller's tensors; the
+            # floor workspace recomputes every window instead (the kernels derive the count from ws_bytes)
+            prev = _native.set_wide_keep_budget(0)
+            try:
+                ws = torch.empty(_native.workspace_bytes(dims, need_grad), dtype=torch.uint8, device=dev)
+            finally:
+                _native.set_wide_keep_budget(prev)
         f32 = dict(dtype=torch.float32, device=dev)
         loss = torch.empty((), **f32)
         cost = torch.empty(B, **f32)
