@@ -208,6 +208,14 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     };
     // forward MFMAs of slot pair kbb into fa[.][0..1]
     auto fwd_pair = [&](int kbb, f32x4 (&fp)[2]) {
+#if FCR_ABLATE == 5   // diagnostic: the pre-activations loaded (one 16-B record per slot and lane, cycling
+        // through the wave's h slab) instead of recomputed — what a stored-pre-activation backward would cost
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            if (2 * kbb + u < HS)
+                fp[u] = buf_ld4(nx.rh, lane * 16, (uint32_t)sp.t[6] + (uint32_t)((2 * kbb + u) * 1024));
+        return;
+#endif
 #pragma unroll
         for (int u = 0; u < 2; ++u)
             if (2 * kbb + u < HS) fwd_tile(2 * kbb + u, fp[u]);
@@ -323,6 +331,10 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
             dh[s] = acc[(HS + s) >> 2][(HS + s) & 3] * down;
         }
     }
+#if FCR_ABLATE == 5
+    sp.t[6] += HS * 1024;
+    if (sp.t[6] + HS * 1024 > sp.t[7]) sp.t[6] = 0;
+#endif
     if (FCR_STAMP) {
         const unsigned long long t3 = stamp_now();
         sp.t[0] += t1 - t0;
@@ -422,6 +434,9 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         return n;
     };
     Stamps sp = {{0, 0, 0, 0, (unsigned long long)((threadIdx.x >> 8) & 1), 0, 0, 0}};
+#if FCR_ABLATE == 5
+    sp.t[7] = seq_sz * 16 / 1024 * 1024;   // the h slab's whole KiB: the diagnostic's loads wrap inside it
+#endif
 #if FCR_PRIO == 2   // diagnostic: static priority for the second-dispatched half (MI355X_MICROARCH.md item 4)
     if ((threadIdx.x >> 8) & 1) __builtin_amdgcn_s_setprio(1);
 #endif
