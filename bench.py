@@ -265,6 +265,9 @@ def main():
     ap.add_argument("--small-limit", type=int, default=None,
                     help="fcr_set_small_batch_limit: B at or below it runs the small-batch kernels (0 = never; "
                          "default: the library's, 8192)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal of the N > 1 path on a 1-GPU box: every rank on cuda:0, gloo process group "
+                         "(launcher, barriers, grad all-reduce, max-over-ranks timing); not a scaling number")
     args = ap.parse_args()
 
     # --gpus N without a launcher: start N ranks (torchrun) as a child BEFORE anything touches the GPU
@@ -275,10 +278,13 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if args.graphed and world > 1:
         sys.exit("bench.py: --graphed times the 1-GPU captured step")
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", 0 if args.share_gpu else local)
     torch.cuda.set_device(dev)            # before the process group: RCCL binds each rank to its own GPU
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.share_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
         world = dist.get_world_size()
     B, N, H = args.batch, args.horizon, args.hidden
     if args.small_limit is not None:
@@ -398,7 +404,9 @@ def main():
             "config": {"workload": f"unsupervised-MPC rollout train step, B={B}/GPU, N={N}, H={H}, 3-layer LSTM, "
                                    f"ctrl 3-50-1, {prec_label}" + (", HIP-graph replay" if captured is not None else ""),
                        "batch_per_gpu": B, "global_batch": B * world,
-                       "horizon": N, "hidden": H, "parallelism": f"dp{world}", "world_size": world},
+                       "horizon": N, "hidden": H, "parallelism": f"dp{world}", "world_size": world,
+                       **({"rehearsal": "--share-gpu: every rank on cuda:0 over gloo (path check, not a scaling "
+                                        "number)"} if args.share_gpu else {})},
             "roofline": roof,
             "kernels_ms": {"fwd": f_ms, "bwd": b_ms,
                            "source": ("HIP events on the launching stream, 5 eager steps after the graphed timed region"

@@ -481,6 +481,11 @@ int launch_cell(int B, int H, hipStream_t s, const float *G, const float *c_prev
     return launch_check("wide_cell_kernel");
 }
 
+// trajectories per thread of layer 0's backward cell kernel (FCR_ROWG_T: 1 = one per thread, the old mapping)
+#ifndef FCR_ROWG_T
+#define FCR_ROWG_T 8
+#endif
+constexpr int kRowgT = FCR_ROWG_T;
 template <bool PRE>
 int launch_cell_bwd(int B, int H, hipStream_t s, const float *act, const float *c, const float *c_prev,
                     const float *dH, const float *din, float *dC, float *dG, _Float16 *dgsp, const float *consts,
@@ -489,8 +494,11 @@ int launch_cell_bwd(int B, int H, hipStream_t s, const float *act, const float *
     const dim3 grid((unsigned)(((size_t)B * (H / V) + 255) / 256)), blk(256);
     if (rowg && (V != 4 || 64 % (H / V)))
         return fail(FCR_EINVAL, "wide_cell_bwd_kernel: in-kernel row gradient needs 64 %% (H / 4) == 0 (H = %d)", H);
-    if (V == 4)
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, wih0, rowg);
+    if (rowg) {   // layer 0: kRowgT trajectories per thread share one load of its W_ih0 rows
+        const dim3 g0((unsigned)(((size_t)(B + kRowgT - 1) / kRowgT * (H / V) + 255) / 256));
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4, kRowgT>), g0, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, wih0, rowg);
+    } else if (V == 4)
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H);
     else if (V == 2)
         hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 2>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H);
     else

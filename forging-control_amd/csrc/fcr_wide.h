@@ -272,7 +272,7 @@ __global__ void wide_head_kernel(WideArgs a, int j) {
 // act: the gate activations (i, f, g, o) kept by the recompute, or with PRE their pre-activations (the
 // split-f16 rollout keeps the GEMM output per cell instead of writing a second 4H-wide array), from which
 // the activations are rebuilt with the forward's arithmetic. dG (fp32) may be null when only dgsp is used.
-template <bool PRE, int V>
+template <bool PRE, int V, int T = 1>
 __global__ void wide_cell_bwd_kernel(const float *__restrict__ act, const float *__restrict__ c,
                                      const float *__restrict__ c_prev, const float *__restrict__ dH,
                                      const float *__restrict__ din, float *dC, float *dG, _Float16 *dgsp,
@@ -283,82 +283,92 @@ __global__ void wide_cell_bwd_kernel(const float *__restrict__ act, const float 
     // scaled units of the dgates: back by 1/scale = consts[0], one fp32 product each
     const float c0 = consts ? consts[0] : 1.0f, mh = dh_scaled ? c0 : 1.0f;
     const int HV = H / V;
+    // a thread owns V units of T consecutive trajectories (T > 1 only for layer 0's row gradient: its W_ih0
+    // rows, 4 V kIn floats, are loaded once for the T trajectories instead of once per trajectory)
     const size_t iv = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (iv >= (size_t)B * HV) return;
-    const size_t b = iv / HV, u = (iv % HV) * V, idx = b * H + u;
-    const float *a4 = act + b * 4 * H + u;
-    const typename W::F ai = W::ld(a4), af = W::ld(a4 + H), ag = W::ld(a4 + 2 * H), ao = W::ld(a4 + 3 * H);
-    const typename W::F cv = W::ld(c + idx), dhv = W::ld(dH + b * ldh + u), dcv = W::ld(dC + idx);
-    typename W::F cp = {}, dn = {}, dg[4], dco;
-    if (c_prev) cp = W::ld(c_prev + idx);
-    if (din) dn = W::ld(din + b * ldx + u);
-#pragma unroll
-    for (int k = 0; k < V; ++k) {
-        const float i = PRE ? sigm(ai[k]) : ai[k], f = PRE ? sigm(af[k]) : af[k], g = PRE ? tanhf(ag[k]) : ag[k],
-                    o = PRE ? sigm(ao[k]) : ao[k];
-        const float tc = tanhf(cv[k]);
-        const float dh = dhv[k] * mh + dn[k] * c0;
-        const float dct = dcv[k] + dh * o * (1.0f - tc * tc);
-        dg[0][k] = dct * g * i * (1.0f - i);
-        dg[1][k] = dct * cp[k] * f * (1.0f - f);
-        dg[2][k] = dct * i * (1.0f - g * g);
-        dg[3][k] = dh * tc * o * (1.0f - o);
-        dco[k] = dct * f;
-    }
-    if (dG) {
-        float *d4 = dG + b * 4 * H + u;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) W::st(d4 + k * H, dg[k]);
-    }
-    if (dgsp) {   // split-f16 operand row [hi | lo | hi] of W^T dG, scaled into the f16 range (wide_bscale_kernel)
-        const float sc = consts[3];
-        _Float16 *o16 = dgsp + b * 12 * H + u;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            typename W::h hi, lo;
-#pragma unroll
-            for (int e = 0; e < V; ++e) {
-                const float v = dg[k][e] * sc;
-                hi[e] = (_Float16)v;
-                lo[e] = (_Float16)(v - (float)hi[e]);
-            }
-            W::st16(o16 + k * H, hi);
-            W::st16(o16 + (4 + k) * H, lo);
-            W::st16(o16 + (8 + k) * H, hi);
-        }
-    }
-    W::st(dC + idx, dco);
-    if (rowg) {   // layer 0: the window-row gradient sum_r dG[b][r] W_ih0[r][c] (c < kIn), fp32 from these
-        // dgates, reduced over the trajectory's H / V threads (one aligned segment of a wave: the host checks
-        // 64 % (H / V) == 0) — in place of kIn + 3 more columns in the backward product
+    if (iv >= ((size_t)B + T - 1) / T * HV) return;
+    const size_t bg = iv / HV, u = (iv % HV) * V;
+    float wr[4][V * kIn];
+    if (rowg) {
         static_assert(V * kIn % 4 == 0 || V == 1 || V == 2, "row block in 16-B pieces");
-        float pc[kIn] = {};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             // V consecutive rows of kIn floats: V * kIn / 4 16-B loads (80 B at V = 4, 16-B aligned as u % 4 == 0)
-            float wr[V * kIn];
             if constexpr (V == 4) {
                 const f32x4 *w4 = reinterpret_cast<const f32x4 *>(wih0 + ((size_t)k * H + u) * kIn);
 #pragma unroll
                 for (int q = 0; q < V * kIn / 4; ++q) {
                     const f32x4 v = w4[q];
-                    wr[4 * q] = v[0]; wr[4 * q + 1] = v[1]; wr[4 * q + 2] = v[2]; wr[4 * q + 3] = v[3];
+                    wr[k][4 * q] = v[0]; wr[k][4 * q + 1] = v[1]; wr[k][4 * q + 2] = v[2]; wr[k][4 * q + 3] = v[3];
                 }
             } else {
 #pragma unroll
-                for (int q = 0; q < V * kIn; ++q) wr[q] = wih0[((size_t)k * H + u) * kIn + q];
+                for (int q = 0; q < V * kIn; ++q) wr[k][q] = wih0[((size_t)k * H + u) * kIn + q];
             }
-#pragma unroll
-            for (int e = 0; e < V; ++e)
-#pragma unroll
-                for (int c = 0; c < kIn; ++c) pc[c] = fmaf(dg[k][e], wr[e * kIn + c], pc[c]);
         }
+    }
+    for (int t = 0; t < T; ++t) {
+        const size_t b = bg * T + t, idx = b * H + u;
+        if (b >= (size_t)B) break;   // uniform over the trajectory's H / V threads
+        const float *a4 = act + b * 4 * H + u;
+        const typename W::F ai = W::ld(a4), af = W::ld(a4 + H), ag = W::ld(a4 + 2 * H), ao = W::ld(a4 + 3 * H);
+        const typename W::F cv = W::ld(c + idx), dhv = W::ld(dH + b * ldh + u), dcv = W::ld(dC + idx);
+        typename W::F cp = {}, dn = {}, dg[4], dco;
+        if (c_prev) cp = W::ld(c_prev + idx);
+        if (din) dn = W::ld(din + b * ldx + u);
 #pragma unroll
-        for (int c = 0; c < kIn; ++c)
-            for (int o = 1; o < HV; o <<= 1) pc[c] += __shfl_xor(pc[c], o);
-        if (u == 0)
+        for (int k = 0; k < V; ++k) {
+            const float i = PRE ? sigm(ai[k]) : ai[k], f = PRE ? sigm(af[k]) : af[k], g = PRE ? tanhf(ag[k]) : ag[k],
+                        o = PRE ? sigm(ao[k]) : ao[k];
+            const float tc = tanhf(cv[k]);
+            const float dh = dhv[k] * mh + dn[k] * c0;
+            const float dct = dcv[k] + dh * o * (1.0f - tc * tc);
+            dg[0][k] = dct * g * i * (1.0f - i);
+            dg[1][k] = dct * cp[k] * f * (1.0f - f);
+            dg[2][k] = dct * i * (1.0f - g * g);
+            dg[3][k] = dh * tc * o * (1.0f - o);
+            dco[k] = dct * f;
+        }
+        if (dG) {
+            float *d4 = dG + b * 4 * H + u;
 #pragma unroll
-            for (int c = 0; c < kIn; ++c) rowg[b * kIn + c] += pc[c];
+            for (int k = 0; k < 4; ++k) W::st(d4 + k * H, dg[k]);
+        }
+        if (dgsp) {   // split-f16 operand row [hi | lo | hi] of W^T dG, scaled into the f16 range (wide_bscale_kernel)
+            const float sc = consts[3];
+            _Float16 *o16 = dgsp + b * 12 * H + u;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                typename W::h hi, lo;
+#pragma unroll
+                for (int e = 0; e < V; ++e) {
+                    const float v = dg[k][e] * sc;
+                    hi[e] = (_Float16)v;
+                    lo[e] = (_Float16)(v - (float)hi[e]);
+                }
+                W::st16(o16 + k * H, hi);
+                W::st16(o16 + (4 + k) * H, lo);
+                W::st16(o16 + (8 + k) * H, hi);
+            }
+        }
+        W::st(dC + idx, dco);
+        if (rowg) {   // layer 0: the window-row gradient sum_r dG[b][r] W_ih0[r][c] (c < kIn), fp32 from these
+            // dgates, reduced over the trajectory's H / V threads (one aligned segment of a wave: the host checks
+            // 64 % (H / V) == 0) — in place of kIn + 3 more columns in the backward product
+            float pc[kIn] = {};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int e = 0; e < V; ++e)
+#pragma unroll
+                    for (int cc = 0; cc < kIn; ++cc) pc[cc] = fmaf(dg[k][e], wr[k][e * kIn + cc], pc[cc]);
+#pragma unroll
+            for (int cc = 0; cc < kIn; ++cc)
+                for (int o = 1; o < HV; o <<= 1) pc[cc] += __shfl_xor(pc[cc], o);
+            if (u == 0)
+#pragma unroll
+                for (int cc = 0; cc < kIn; ++cc) rowg[b * kIn + cc] += pc[cc];
+        }
     }
 }
 
