@@ -21,7 +21,10 @@
 // Diagnostic builds bound the loop: cache-hot operand loads gain 6 %, no loads and LDS stores at all 33 %:
 // the staging (LDS write traffic and the wait before it), not HBM, is what the loop loses to. The stages
 // are filled by LDS-DMA (global_load_lds, FCR_WG_DMA): 2 % faster than the register round trip; a 3-stage
-// ring with the next step's fragment reads overlapping the MFMAs measured 5 % slower.)
+// ring with the next step's fragment reads overlapping the MFMAs measured 5 % slower. A 3-stage ring with
+// two steps of DMA prefetch and a bare s_barrier (FCR_WG_STAGES=3, default since round 2f): forward 191.9
+// -> 188.0 ms at config 5, bit-identical — the loop is not waiting on HBM latency so much as on its
+// per-step barrier and LDS traffic.)
 #pragma once
 #include "fcr_common.h"
 #include "fcr_f16.h"
@@ -50,7 +53,13 @@ static_assert(kWgWaves == 4 || kWgWaves == 8, "wave layout");
 constexpr int kWgStageA = kWgM * kWgK * 2;   // bytes
 constexpr int kWgStageB = kWgN * kWgK * 2;
 constexpr int kWgEpi = kWgN * ((kWgU + 4) * 4 + 2 * (kWgU + 8) * 2);   // the epilogue's c / hi / lo tiles
-constexpr int kWgStages = 2;
+#ifndef FCR_WG_STAGES
+#define FCR_WG_STAGES 3
+#endif
+// LDS stages of the DMA mainloop: 2 = one step of prefetch; 3 = two steps (the ring fits in the 72 KB the
+// epilogue's tiles take anyway), the stage wait is vmcnt(pieces of one step), not vmcnt(0)
+constexpr int kWgStages = FCR_WG_STAGES;
+static_assert(kWgStages == 2 || kWgStages == 3, "stages");
 constexpr int kWgLds = kWgStages * (kWgStageA + kWgStageB) > kWgEpi ? kWgStages * (kWgStageA + kWgStageB) : kWgEpi;
 static_assert(kWgK == 32 || kWgK == 64, "K step");
 
@@ -131,6 +140,40 @@ __global__ __launch_bounds__(kWgThreads, 8 / kWgWaves) void wide_gemm_cell_kerne
 #pragma unroll
         for (int n = 0; n < kWgNT; ++n) acc[m][n] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     const int fr = lane & 15, fq = lane >> 4;
+#if FCR_WG_STAGES == 3
+    // two steps of prefetch: stage ks is waited for with step ks + 1's pieces still in flight (vmcnt counts
+    // this wave's DMA in issue order), and the barrier is a bare s_barrier: __syncthreads()'s release fence
+    // would drain every outstanding load (vmcnt(0)). The empty asm statements keep the compiler's LDS
+    // accesses on their side of it.
+    dma(0, 0);
+    if (nk > 1) dma(1, 1);
+    int buf = 0;
+    for (int ks = 0; ks < nk; ++ks) {
+        if (ks + 1 < nk) {
+            static_assert(NPC == 6, "vmcnt immediate");
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        const char *base = lds + buf * (kWgStageA + kWgStageB);
+        f16x8 af[8], bf[kWgNT];
+#pragma unroll
+        for (int n = 0; n < kWgNT; ++n)
+            bf[n] = *reinterpret_cast<const f16x8 *>(base + kWgStageA + wg_off(16 * (kWgNT * wc + n) + fr, fq));
+#pragma unroll
+        for (int m = 0; m < 8; ++m) af[m] = *reinterpret_cast<const f16x8 *>(base + wg_off(128 * wr + 16 * m + fr, fq));
+        const int nb = buf == 0 ? 2 : buf - 1;       // (ks + 2) % 3: the stage every wave finished reading at ks - 1
+        if (ks + 2 < nk) dma(ks + 2, nb);
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+#pragma unroll
+            for (int n = 0; n < kWgNT; ++n) acc[m][n] = mfma16(af[m], bf[n], acc[m][n]);
+        buf = buf == 2 ? 0 : buf + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#else
     dma(0, 0);
     for (int ks = 0; ks < nk; ++ks) {
         const int buf = ks & 1;
@@ -152,6 +195,7 @@ __global__ __launch_bounds__(kWgThreads, 8 / kWgWaves) void wide_gemm_cell_kerne
             for (int n = 0; n < kWgNT; ++n) acc[m][n] = mfma16(af[m], bf[n], acc[m][n]);
     }
     __syncthreads();
+#endif
 #else
     // global -> register chunk assignment: A 256 rows x kWgC chunks, XB 128 rows x kWgC chunks
     constexpr int NA = kWgM * kWgC / kWgThreads, NB = kWgN * kWgC / kWgThreads, RS = kWgThreads / kWgC;
