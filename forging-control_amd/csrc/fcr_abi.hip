@@ -483,7 +483,7 @@ int launch_cell(int B, int H, hipStream_t s, const float *G, const float *c_prev
 
 // trajectories per thread of layer 0's backward cell kernel (FCR_ROWG_T: 1 = one per thread, the old mapping)
 #ifndef FCR_ROWG_T
-#define FCR_ROWG_T 8
+#define FCR_ROWG_T 4
 #endif
 constexpr int kRowgT = FCR_ROWG_T;
 template <bool PRE>

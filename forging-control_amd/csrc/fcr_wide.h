@@ -273,7 +273,7 @@ __global__ void wide_head_kernel(WideArgs a, int j) {
 // split-f16 rollout keeps the GEMM output per cell instead of writing a second 4H-wide array), from which
 // the activations are rebuilt with the forward's arithmetic. dG (fp32) may be null when only dgsp is used.
 template <bool PRE, int V, int T = 1>
-__global__ void wide_cell_bwd_kernel(const float *__restrict__ act, const float *__restrict__ c,
+__global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restrict__ act, const float *__restrict__ c,
                                      const float *__restrict__ c_prev, const float *__restrict__ dH,
                                      const float *__restrict__ din, float *dC, float *dG, _Float16 *dgsp,
                                      const float *__restrict__ consts, int dh_scaled, int ldh, int ldx, int B,
