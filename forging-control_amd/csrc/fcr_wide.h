@@ -272,6 +272,14 @@ __global__ void wide_head_kernel(WideArgs a, int j) {
 // act: the gate activations (i, f, g, o) kept by the recompute, or with PRE their pre-activations (the
 // split-f16 rollout keeps the GEMM output per cell instead of writing a second 4H-wide array), from which
 // the activations are rebuilt with the forward's arithmetic. dG (fp32) may be null when only dgsp is used.
+#ifndef FCR_ROWG_DPP
+#define FCR_ROWG_DPP 0
+#endif
+// a lane's value moved by a DPP pattern within its 16-lane row (every lane has a source: no bound control)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
 template <bool PRE, int V, int T = 1>
 __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restrict__ act, const float *__restrict__ c,
                                      const float *__restrict__ c_prev, const float *__restrict__ dH,
@@ -362,9 +370,22 @@ __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restr
                 for (int e = 0; e < V; ++e)
 #pragma unroll
                     for (int cc = 0; cc < kIn; ++cc) pc[cc] = fmaf(dg[k][e], wr[k][e * kIn + cc], pc[cc]);
+#if FCR_ROWG_DPP
+            // 16-lane partial sums on DPP (VALU, no LDS path): quad xor 1, xor 2, then the half-row and row
+            // mirrors pair the quads and the 8-lane halves; 16 and 32 on the bpermute path (HV >= 16 here)
+#pragma unroll
+            for (int cc = 0; cc < kIn; ++cc) {
+                pc[cc] += dpp_f32<0xB1>(pc[cc]);
+                pc[cc] += dpp_f32<0x4E>(pc[cc]);
+                pc[cc] += dpp_f32<0x141>(pc[cc]);
+                pc[cc] += dpp_f32<0x140>(pc[cc]);
+                for (int o = 16; o < HV; o <<= 1) pc[cc] += __shfl_xor(pc[cc], o);
+            }
+#else
 #pragma unroll
             for (int cc = 0; cc < kIn; ++cc)
                 for (int o = 1; o < HV; o <<= 1) pc[cc] += __shfl_xor(pc[cc], o);
+#endif
             if (u == 0)
 #pragma unroll
                 for (int cc = 0; cc < kIn; ++cc) rowg[b * kIn + cc] += pc[cc];
