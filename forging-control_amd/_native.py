@@ -21,8 +21,8 @@ ERRORS = {-1: "FCR_EINVAL", -2: "FCR_EWORKSPACE", -3: "FCR_EHIP", -4: "FCR_EUNSU
 # Every symbol include/fcr.h declares (tests check the .so exports exactly these).
 EXPORTS = ("fcr_workspace_size", "fcr_forward", "fcr_backward", "fcr_lstm_workspace_size", "fcr_lstm_forward",
            "fcr_lstm_backward", "fcr_plant_rk4", "fcr_closed_loop_run", "fcr_window_gather", "fcr_fnn_workspace_size",
-           "fcr_fnn_forward", "fcr_fnn_backward", "fcr_set_small_batch_limit", "fcr_set_wide_keep_budget", "fcr_last_error",
-           "fcr_abi_version")
+           "fcr_fnn_forward", "fcr_fnn_backward", "fcr_set_small_batch_limit", "fcr_set_wide_keep_budget", "fcr_last_kernels",
+           "fcr_last_error", "fcr_abi_version")
 
 
 class FcrDims(ctypes.Structure):
@@ -112,6 +112,8 @@ def load() -> ctypes.CDLL:
         lib.fcr_set_small_batch_limit.restype = i32
         lib.fcr_set_wide_keep_budget.argtypes = [ctypes.c_int64]
         lib.fcr_set_wide_keep_budget.restype = ctypes.c_int64
+        lib.fcr_last_kernels.argtypes = []
+        lib.fcr_last_kernels.restype = i32
         lib.fcr_last_error.argtypes = []
         lib.fcr_last_error.restype = ctypes.c_char_p
         lib.fcr_abi_version.argtypes = []
@@ -135,9 +137,19 @@ def set_small_batch_limit(max_batch: int) -> int:
 
 def set_wide_keep_budget(nbytes: int) -> int:
     """fcr_set_wide_keep_budget (H > 52): bytes of kept windows a backward-enabled workspace may add, so their
-    backward skips the recompute (< 0 = default: the workspace within 60 % of the device; 0 = none);
-    returns the old budget. Per calling thread."""
+    backward skips the recompute (< 0 = default: half the device memory free at its first sizing, at most 40 %
+    of the device; 0 = none); returns the old budget. Process-wide."""
     return int(load().fcr_set_wide_keep_budget(int(nbytes)))
+
+
+KERNEL_FAMILIES = {0: None, 1: "small", 2: "fused", 3: "wide"}
+
+
+def last_kernels() -> tuple:
+    """fcr_last_kernels: (forward family, backward family) the process last launched — "small", "fused",
+    "wide" or None."""
+    v = int(load().fcr_last_kernels())
+    return KERNEL_FAMILIES[v & 0xF], KERNEL_FAMILIES[(v >> 4) & 0xF]
 
 
 def small_batch_limit() -> int:

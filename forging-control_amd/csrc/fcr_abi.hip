@@ -11,6 +11,9 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include <atomic>
+#include <mutex>
+
 #include "fcr.h"
 #include "fcr_bwd.h"
 #include "fcr_common.h"
@@ -202,10 +205,20 @@ int launch_bwd(const BwdArgs &ba, const Layout &L, bool lp, hipStream_t s) {
 // Small-batch kernels (fcr_small.h): one workgroup of ceil(HS/4) waves per 16-trajectory group.
 // Used for the fp32-accurate mode at HS = 8, 13 when B <= g_small_max_batch (fcr_set_small_batch_limit):
 // below one wave per SIMD the fused kernels run at one wave's sequential latency.
-// thread-local like the last-error text: the ABI keeps no process-wide mutable state
-thread_local int g_small_max_batch = 8192;
+// Process-wide (not thread-local): torch runs a CUDA tensor's backward on its autograd worker thread, so a
+// per-thread limit set by the caller would reach the forward only. A change between a forward and its
+// backward is harmless: both families keep one workspace layout, and a mixed pair is valid (tested).
+std::atomic<int> g_small_max_batch{8192};
+// fcr_last_kernels: the family the last fcr_forward (bits 0-3) and fcr_backward (bits 4-7) launched, process-wide
+std::atomic<int> g_last_kernels{0};
+void note_kernels(int shift, int family) {
+    int cur = g_last_kernels.load(std::memory_order_relaxed);
+    while (!g_last_kernels.compare_exchange_weak(cur, (cur & ~(0xf << shift)) | (family << shift))) {
+    }
+}
 bool use_small(const fcr_dims *d, const Layout &L) {
-    return d->precision == FCR_PRECISION_FP32 && (L.HS == 8 || L.HS == 13) && d->B <= g_small_max_batch;
+    return d->precision == FCR_PRECISION_FP32 && (L.HS == 8 || L.HS == 13) &&
+           d->B <= g_small_max_batch.load(std::memory_order_relaxed);
 }
 
 template <int HS, bool STORE>
@@ -333,8 +346,35 @@ float *kept_act(const WideLayout &L, char *base, const fcr_dims *d, int j) {
 float *kept_c(const WideLayout &L, char *base, const fcr_dims *d, int j) {
     return (float *)(base + L.KC) + (size_t)(j - (d->N - L.keep)) * kLayers * kL * d->B * d->H;
 }
-// fcr_set_wide_keep_budget: bytes of kept windows fcr_workspace_size may add; < 0 = up to 60 % of the device
-thread_local long long g_wide_keep_budget = -1;
+// fcr_set_wide_keep_budget: bytes of kept windows fcr_workspace_size may add; < 0 = the default policy
+// (wide_default_cap). Process-wide, like the small-batch limit.
+std::atomic<long long> g_wide_keep_budget{-1};
+
+// Default cap of a backward-enabled wide workspace: half of the memory that was FREE on the device the first
+// time one was sized there (cached per device, so the count does not drift as torch's cache holds the last
+// call's workspace), and never more than kWideDefaultFrac of the device's total. Ranks sharing a device each
+// see what the others left; what exceeds the cap recomputes instead of keeping (the floor workspace stays).
+constexpr double kWideDefaultFrac = 0.40;
+long long wide_default_cap() {
+    static std::mutex mu;
+    static long long cap_of[64];
+    static bool have[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!have[dev]) {
+        size_t free_b = 0, total_b = 0;
+        long long cap = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+            cap = (long long)(free_b / 2);
+            const long long lim = (long long)((double)total_b * kWideDefaultFrac);
+            if (cap > lim) cap = lim;
+        }
+        cap_of[dev] = cap;
+        have[dev] = true;
+    }
+    return cap_of[dev];
+}
 
 rocblas_handle blas_on(hipStream_t s) {
     thread_local rocblas_handle h = nullptr;
@@ -936,15 +976,13 @@ const char *fcr_last_error(void) { return g_err; }
 int fcr_abi_version(void) { return FCR_ABI_VERSION; }
 
 int fcr_set_small_batch_limit(int32_t max_batch) {
-    const int prev = g_small_max_batch;
-    g_small_max_batch = max_batch < 0 ? 0 : max_batch;
-    return prev;
+    return g_small_max_batch.exchange(max_batch < 0 ? 0 : max_batch);
 }
 
+int fcr_last_kernels(void) { return g_last_kernels.load(); }
+
 int64_t fcr_set_wide_keep_budget(int64_t bytes) {
-    const long long prev = g_wide_keep_budget;
-    g_wide_keep_budget = bytes < 0 ? -1 : bytes;
-    return prev;
+    return g_wide_keep_budget.exchange(bytes < 0 ? -1 : bytes);
 }
 
 #if FCR_STAMP
@@ -965,11 +1003,9 @@ int fcr_workspace_size(const fcr_dims *dims, int with_backward, size_t *bytes) {
     int keep = 0;
     if (with_backward) {   // kept windows within the budget (fcr_set_wide_keep_budget)
         const size_t base = make_wide(dims, 1, 0).total;
-        long long budget = g_wide_keep_budget;
-        if (budget < 0) {   // default: the whole workspace within 60 % of the device's memory (its TOTAL, not
-            // what is free now — torch's cache holds the last call's workspace, and the count must not drift)
-            size_t free_b = 0, total_b = 0;
-            const long long cap = hipMemGetInfo(&free_b, &total_b) == hipSuccess ? (long long)(total_b / 10 * 6) : 0;
+        long long budget = g_wide_keep_budget.load();
+        if (budget < 0) {   // default: the whole workspace within wide_default_cap()
+            const long long cap = wide_default_cap();
             budget = cap > (long long)base ? cap - (long long)base : 0;
         }
         while (keep < dims->N && make_wide(dims, 1, keep + 1).total - base <= (size_t)budget) ++keep;
@@ -995,6 +1031,7 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
     if (is_wide(d)) {
         const size_t need = make_wide(d, with_backward).total;
         if (ws_bytes < need) return fail(FCR_EWORKSPACE, "fcr_forward: ws has %zu bytes, needs %zu", ws_bytes, need);
+        note_kernels(0, FCR_KERNELS_WIDE);
         return wide_forward(d, w, X, u0, states, noise, loss, cost, command, error, prediction, xhat, with_backward,
                             (char *)ws, ws_bytes, (hipStream_t)stream);
     }
@@ -1063,6 +1100,7 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
     fa.stamp = (unsigned long long *)(base + L.stamp) + (size_t)L.nw_pad * 8;
 #endif
     const bool small = use_small(d, L);
+    note_kernels(0, small ? FCR_KERNELS_SMALL : FCR_KERNELS_FUSED);
     if (small) {
         if (L.HS == 8) rc = with_backward ? launch_sfwd_t<8, true>(fa, L, s) : launch_sfwd_t<8, false>(fa, L, s);
         else rc = with_backward ? launch_sfwd_t<13, true>(fa, L, s) : launch_sfwd_t<13, false>(fa, L, s);
@@ -1092,6 +1130,7 @@ int fcr_backward(const fcr_dims *d, const float *X, const float *states, const f
     if (is_wide(d)) {
         const size_t need = make_wide(d, 1).total;
         if (ws_bytes < need) return fail(FCR_EWORKSPACE, "fcr_backward: ws has %zu bytes, needs %zu", ws_bytes, need);
+        note_kernels(4, FCR_KERNELS_WIDE);
         return wide_backward(d, X, states, prediction, dloss, g_u0, g_w_inp, g_b_inp, g_w_out, (char *)ws, ws_bytes,
                              (hipStream_t)stream);
     }
@@ -1121,6 +1160,7 @@ int fcr_backward(const fcr_dims *d, const float *X, const float *states, const f
     ba.stamp = (unsigned long long *)(base + L.stamp);
 #endif
     ba.p = packed_ptrs(L, base);
+    note_kernels(4, use_small(d, L) ? FCR_KERNELS_SMALL : FCR_KERNELS_FUSED);
     if (use_small(d, L)) {
         rc = L.HS == 8 ? launch_sbwd_t<8>(ba, L, s) : launch_sbwd_t<13>(ba, L, s);
     } else {

@@ -40,7 +40,13 @@ class GradAllReduce:
       uneven shards and short last batches still give the global-mean gradient with ONE all-reduce.
     * ``hook(module)``: equal shards are assumed (1/world), with a one-time warning.
 
-    Returns the global-mean loss when ``loss`` is given, else None.
+    Returns the global-mean loss when ``loss`` is given (every rank must then pass one), else None.
+
+    Every rank packs the same buffer whatever its shard held: each trainable parameter's gradient (zeros
+    where it has none) plus one has-gradient flag per parameter. A rank whose shard is EMPTY (more ranks
+    than trajectories in a short last batch) therefore still joins the all-reduce with b_local = 0 and
+    receives the others' gradients; a parameter no rank produced a gradient for (the idle ``fc_int``,
+    Functions.py:279) keeps ``grad = None``, so AdamW skips it as it does in the reference.
     """
 
     def __init__(self, group=None):
@@ -49,7 +55,7 @@ class GradAllReduce:
 
     def __call__(self, module: torch.nn.Module, b_local: int | None = None, b_global: int | None = None,
                  loss: torch.Tensor | None = None):
-        params = [p for p in module.parameters() if p.grad is not None]
+        params = [p for p in module.parameters() if p.requires_grad]
         if not params:
             return loss
         world = dist.get_world_size(self.group)
@@ -57,22 +63,34 @@ class GradAllReduce:
         if b_local is None and not self._warned:
             warnings.warn("GradAllReduce called without the shard size: assuming equal shards (1/world)")
             self._warned = True
-        pieces = [p.grad.reshape(-1) for p in params]
+        pieces = [p.grad.reshape(-1) if p.grad is not None else torch.zeros_like(p).reshape(-1) for p in params]
+        pieces.append(torch.tensor([float(p.grad is not None) for p in params], dtype=pieces[0].dtype,
+                                   device=pieces[0].device))
         if loss is not None:
             pieces.append(loss.detach().reshape(1).to(pieces[0].dtype))
         if count:
             pieces.append(pieces[0].new_ones(1))
         flat = torch.cat(pieces)
-        if count:
-            flat.mul_(float(b_local))
-        else:
-            flat.mul_((b_local / b_global) if b_local is not None else 1.0 / world)
+        nflag = len(params)
+        off_flags = flat.numel() - nflag - (loss is not None) - count
+        scale = float(b_local) if count else ((b_local / b_global) if b_local is not None else 1.0 / world)
+        flat[:off_flags].mul_(scale)
+        flat[off_flags + nflag:].mul_(scale)   # the loss and, in count mode, b_local itself
         dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+        # a rank that ran the step produces gradients for the same parameters as every other such rank, so it
+        # keeps its own pattern (no host sync); only a rank without any gradient reads the flags
+        if any(p.grad is not None for p in params):
+            flags = [float(p.grad is not None) for p in params]
+        else:
+            flags = flat[off_flags:off_flags + nflag].tolist()
         if count:
-            flat = flat[:-1] / flat[-1]
+            flat = flat / flat[-1].clamp_min(1.0)   # sum of b_r (0 only if every shard was empty)
         off = 0
-        for p in params:
-            n = p.grad.numel()
-            p.grad.copy_(flat[off:off + n].view_as(p.grad))
+        for p, has in zip(params, flags):
+            n = p.numel()
+            if has > 0:
+                if p.grad is None:
+                    p.grad = torch.empty_like(p)
+                p.grad.copy_(flat[off:off + n].view_as(p))
             off += n
-        return flat[off] if loss is not None else None
+        return flat[off_flags + nflag] if loss is not None else None

@@ -1,8 +1,10 @@
 """Host-side mirror of the reference's hot-path interface (Unsupervised Learning/Functions.py).
 
 Same class names, constructor/forward signatures, parameter names (so reference ``state_dict``s load
-unchanged) and return conventions as the reference; the rollout inside :class:`MPCLoss` runs on the
-gfx950 kernels through :mod:`.rollout` — there is no CPU path for it.
+unchanged) and return conventions as the reference. On a ROCm device the rollout inside :class:`MPCLoss`
+runs on the gfx950 kernels through :mod:`.rollout` (and raises if libfcr.so is missing: no fallback
+there); on the CPU — the reference's ``device = cpu`` branch (UL/Main.py:38) — it runs the reference's
+own op sequence on the caller's modules, as :class:`LSTMModel` / :class:`FNNModel` already do off-device.
 
 * :class:`FNNModel`     <- Functions.py:215-289
 * :class:`LSTMModel`    <- Functions.py:295-379
@@ -109,7 +111,8 @@ def _simulator_params(simulator):
 
 class MPCLoss(nn.Module):
     """Drop-in for the reference MPCLoss (Functions.py:1336-1472): the N-step closed-loop rollout of the
-    controller through the LSTM surrogate and its quadratic speed-tracking cost, fused on gfx950.
+    controller through the LSTM surrogate and its quadratic speed-tracking cost, fused on gfx950 (CPU
+    tensors: the reference's own op sequence, :meth:`_forward_host`).
 
     ``forward`` returns ``(loss, {'loss', 'command', 'error', 'prediction'})`` with the reference's
     shapes. ``enable_noise`` draws ``randn_like(x0) * 0.01`` per horizon step from the device's default
@@ -133,6 +136,8 @@ class MPCLoss(nn.Module):
         if dev.type != X.device.type or (dev.index is not None and dev.index != X.device.index):
             raise RuntimeError(f"MPCLoss: inputs are on {X.device}, device argument is {device}")
         B = X.shape[0]
+        if X.device.type == "cpu":
+            return self._forward_host(simulator, controller, X, output_controller, states, device, enable_noise, noise)
         if enable_noise and noise is None:
             noise = torch.stack([torch.randn(B, 4, device=X.device) * 0.01 for _ in range(self.N)], dim=1)
         elif not enable_noise:
@@ -142,6 +147,52 @@ class MPCLoss(nn.Module):
             self.N, self.alpha, noise, self.precision)
         self.last_trajectory = xhat
         return loss, {"loss": cost, "command": command, "error": error, "prediction": prediction}
+
+    def _forward_host(self, simulator, controller, X, u0, states, device, enable_noise, noise):
+        """The rollout where the reference runs it without a GPU (``device = cpu``, UL/Main.py:38): its op
+        sequence (Functions.py:1386-1472) on the caller's own modules — ``simulator(window, device)`` and
+        ``controller(x)`` are LSTMModel's / FNNModel's torch layers off-device — under autograd, so
+        ``loss.backward()`` reaches the controller parameters and ``output_controller`` as the reference's
+        does (the frozen LSTM's weight gradients included). Noise: ``randn_like(x̂) * 0.01`` drawn after every
+        surrogate call in the reference's order (:1400-1402, :1438-1440), or the given (B, N, 4) ``noise``."""
+        N, alpha, relu = self.N, self.alpha, self.activation
+        B = X.shape[0]
+
+        def perturb(xh, j):
+            if noise is not None and enable_noise:
+                return xh + noise[:, j]
+            if enable_noise:
+                return xh + torch.randn_like(xh) * 0.01
+            return xh
+
+        def constraint(xh):                                                       # Functions.py:1411, 1449
+            return relu(-xh[:, 1]) + relu(-xh[:, 2]) + relu(xh[:, 1] - 2.122366) + relu(xh[:, 2] - 1.036233)
+
+        ref = X[:, -1]                                                            # :1392
+        window = states.clone()                                                   # :1395-1396
+        window[:, -1, -1] = u0.reshape(B)
+        xh = perturb(simulator(window, device), 0)                                # :1399-1402
+        cmd = [alpha * torch.square(window[:, -2, -1] - window[:, -1, -1])]       # :1405
+        err = [torch.square(xh[:, 0] - ref)]                                      # :1408
+        tot = [err[0] + cmd[0] + constraint(xh)]                                  # :1414
+        u_next = u0.reshape(B, 1)
+        preds, traj = [u_next], [xh]
+        for j in range(N - 1):                                                    # :1421
+            u_prev = u_next
+            u_next = controller(torch.stack((xh[:, 0], xh[:, 3], ref), dim=1))    # :1424-1430
+            window = torch.cat((window[:, 1:10, :], torch.cat((xh, u_next), dim=1).unsqueeze(1)), dim=1)   # :1433-1434
+            xh = perturb(simulator(window, device), j + 1)                        # :1437-1440
+            err.append(torch.square(xh[:, 0] - ref))                              # :1443
+            cmd.append(alpha * torch.square(u_prev.reshape(B) - u_next.reshape(B)))   # :1446
+            tot.append(err[-1] + cmd[-1] + constraint(xh))                        # :1449-1452
+            preds.append(u_next)
+            traj.append(xh)
+        cost = torch.stack(tot).sum(dim=0) / N                                    # :1458-1460
+        command = torch.stack(cmd).sum(dim=0) / N
+        error = torch.stack(err).sum(dim=0) / N
+        self.last_trajectory = torch.stack(traj, dim=1).detach()
+        return cost.mean(), {"loss": cost, "command": command, "error": error,    # :1463-1472
+                             "prediction": torch.cat(preds, dim=1).flatten()}
 
 
 class NeuralNetwork:
@@ -180,6 +231,13 @@ class NeuralNetwork:
         for X, _, z in data_loader:
             X, z = X.to(device), z.to(device)
             optimizer.zero_grad()
+            if X.shape[0] == 0:
+                # an empty shard (more ranks than trajectories in a short last batch): no rollout, but the
+                # rank still joins the all-reduce with b_local = 0 and steps with everyone's gradient
+                if grad_sync is not None:
+                    grad_sync(model, 0)
+                    optimizer.step()
+                continue
             output = model(X)
             loss, f = loss_function(simulator, model, X, output, z, device, enable_noise)
             for k in feats:
@@ -190,7 +248,7 @@ class NeuralNetwork:
             optimizer.step()
             total += loss.item()
             n_batches += 1
-        feats = {k: torch.cat(v, dim=0) for k, v in feats.items()}
+        feats = {k: torch.cat(v, dim=0) if v else torch.empty(0, device=device) for k, v in feats.items()}
         return total / max(n_batches, 1), feats
 
     @staticmethod

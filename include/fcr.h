@@ -227,10 +227,20 @@ int fcr_lstm_backward(const fcr_dims *dims, const fcr_weights *w, const float *d
  * Kernel choice for small batches (fp32-accurate mode, H 17..52): B <= max_batch runs the small-batch
  * kernels, which split each 16-trajectory group's cell over the four waves of a workgroup (the reference
  * trains at B = 15, UL/Main.py:84,297); larger B runs the fused one-wave-per-group kernels. Default 8192;
- * 0 = never. Per calling thread (like fcr_last_error); both kernel families keep the same workspace
+ * 0 = never. Both kernel families keep the same workspace
  * layout, so a change between a forward and its backward is harmless. Returns the previous limit.
+ * PROCESS-WIDE (an atomic, not per thread): torch runs the backward of device tensors on its autograd worker
+ * thread, so a per-thread setting made by the caller would reach only the forward.
  */
 int fcr_set_small_batch_limit(int32_t max_batch);
+
+/* Which kernel family the last fcr_forward (bits 0-3) and fcr_backward (bits 4-7) of the process launched:
+ * FCR_KERNELS_SMALL (the small-batch kernels), _FUSED (the fused one-wave-per-group kernels) or _WIDE (H > 52,
+ * the batch-wide GEMM path); 0 before the first call. A debug query (tests assert the intended family ran). */
+#define FCR_KERNELS_SMALL 1
+#define FCR_KERNELS_FUSED 2
+#define FCR_KERNELS_WIDE 3
+int fcr_last_kernels(void);
 
 /*
  * H > 52 (the batch-wide GEMM path): how many bytes of "kept windows" fcr_workspace_size(with_backward = 1)
@@ -239,9 +249,11 @@ int fcr_set_small_batch_limit(int32_t max_batch);
  * (30 B 5H floats: 10 GB at B = 65 536, H = 256 — torch's autograd keeps at least that for every window),
  * so its backward skips the recompute (config 5: a third of the step). The last windows are kept, as many
  * as the budget allows; fcr_forward / fcr_backward derive the count from the ws_bytes they are given.
- * bytes < 0 (default): as many as keep the whole workspace within 60 % of the device's total memory
- * (a stable count from call to call); 0: keep none.
- * Per calling thread. Returns the previous budget.
+ * bytes < 0 (default): as many as keep the whole workspace within half of the memory that was free on the
+ * device when a workspace was first sized there (cached per device: a stable count from call to call), and
+ * within 40 % of the device's total memory; 0: keep none. The workspace stays allocated from the forward until
+ * its backward has run (torch: until RolloutFn.backward releases it).
+ * Process-wide. Returns the previous budget.
  */
 int64_t fcr_set_wide_keep_budget(int64_t bytes);
 

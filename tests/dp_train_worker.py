@@ -3,10 +3,11 @@
 ``python tests/dp_train_worker.py --ranks N --out DIR`` re-launches itself as N ranks with
 ``forging_control_amd.launch.spawn_ranks`` — the launcher ``bench.py --gpus N`` uses — and each rank runs
 the real ``NeuralNetwork.train_model(..., grad_sync=GradAllReduce())`` over its contiguous shard of every
-global batch (the reference's B = 15, so shards are uneven: 8 / 7, and the last batch of 7 splits 4 / 3).
-The loss is a CPU stand-in with MPCLoss's call signature: the stock-torch restatement of the rollout
-(oracle/rollout_torch.py) on the reference's trained surrogate — the GPU kernels are not needed to test
-the data-parallel plumbing. Every rank writes its final controller parameters and epoch losses to DIR.
+global batch (the reference's B = 15, so shards are uneven: 8 / 7, and the last batch of 7 splits 4 / 3; at
+8 ranks the last batch leaves rank 7 an EMPTY shard). The loss is the package's own ``MPCLoss`` on the CPU
+(its reference op sequence, functions.py) over the reference's trained surrogate — the GPU kernels are not
+needed to test the data-parallel plumbing. Every rank writes its final controller parameters and epoch
+losses to DIR.
 """
 import argparse
 import os
@@ -19,25 +20,20 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import forging_control_amd as fca  # noqa: E402
-from oracle import rollout_torch as T  # noqa: E402
 
 N_HORIZON, ALPHA = 3, 20.0
 BATCHES = [15, 15, 7]
 
 
-class StandInMPCLoss(torch.nn.Module):
-    """MPCLoss's call surface (Functions.py:1353) over the CPU restatement of its arithmetic."""
-
-    def forward(self, simulator, controller, input_controller, output_controller, states, device, enable_noise=False):
-        loss, f = T.mpc_loss(simulator, controller, input_controller, output_controller, states, N_HORIZON, ALPHA)
-        return loss, {k: f[k].detach() for k in ("loss", "command", "error", "prediction")}
-
-
 def surrogate():
     w = np.load(os.path.join(ROOT, "tests", "golden", "weights_ref.npz"))
-    params = {"Wih": [w[f"Wih{k}"] for k in range(3)], "Whh": [w[f"Whh{k}"] for k in range(3)], "fcW": w["fcW"],
-              "fcb": w["fcb"], "W_inp": w["W_inp"], "b_inp": w["b_inp"], "W_out": w["W_out"]}
-    sim, _ = T.build_modules(params, torch.float32)
+    sim = fca.LSTMModel(5, 50, 4, 3)
+    with torch.no_grad():
+        for k in range(3):
+            getattr(sim.lstm, f"weight_ih_l{k}").copy_(torch.as_tensor(w[f"Wih{k}"]))
+            getattr(sim.lstm, f"weight_hh_l{k}").copy_(torch.as_tensor(w[f"Whh{k}"]))
+        sim.fc.weight.copy_(torch.as_tensor(w["fcW"]))
+        sim.fc.bias.copy_(torch.as_tensor(w["fcb"]))
     return sim
 
 
@@ -59,7 +55,8 @@ def train(loader, grad_sync=None, epochs=2):
         fca.distributed.broadcast_params(ctrl)
     opt = torch.optim.AdamW(ctrl.parameters(), lr=1e-2)
     sim = surrogate()
-    losses = [fca.NeuralNetwork.train_model(loader, sim, ctrl, StandInMPCLoss(), opt, "cpu", grad_sync=grad_sync)[0]
+    losses = [fca.NeuralNetwork.train_model(loader, sim, ctrl, fca.MPCLoss(N_HORIZON, ALPHA), opt, "cpu",
+                                            grad_sync=grad_sync)[0]
               for _ in range(epochs)]
     return torch.cat([p.detach().reshape(-1) for p in ctrl.parameters()]).numpy(), np.array(losses)
 

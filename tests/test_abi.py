@@ -106,9 +106,10 @@ def test_fnn_model_on_cpu_is_the_torch_module():
     assert torch.equal(m(x), ref)
 
 
-def test_small_batch_limit_is_per_thread():
-    """fcr_set_small_batch_limit (the kernel-family choice) keeps no process-wide state: a setting made on
-    one thread is not seen by another (no global mutable state but the thread-local error)."""
+def test_small_batch_limit_is_process_wide():
+    """fcr_set_small_batch_limit (the kernel-family choice) is one process-wide setting: torch runs the
+    backward of device tensors on its autograd worker thread, so a setting made by the caller's thread must be
+    seen there too (a thread-local limit changed only the forward)."""
     import threading
     n = fca._native
     prev = n.set_small_batch_limit(77)
@@ -118,7 +119,11 @@ def test_small_batch_limit_is_per_thread():
         th = threading.Thread(target=lambda: seen.setdefault("other", n.small_batch_limit()))
         th.start()
         th.join()
-        assert seen["other"] == 8192
+        assert seen["other"] == 77
         assert n.set_small_batch_limit(-5) == 77 and n.small_batch_limit() == 0   # negative clamps to 0 = never
     finally:
         n.set_small_batch_limit(prev)
+
+
+def test_last_kernels_query_before_any_call():
+    assert fca._native.last_kernels() == (None, None)

@@ -1,6 +1,6 @@
 """Full-size parity at the benchmarked batch sizes (BASELINE.json configs 2, 3 and 5): the gfx950 rollout's
-loss, per-trajectory features, x̂, per-trajectory u0 gradients AND the controller-parameter gradients —
-sums over all B·N (trajectory, step) terms — against the stock-torch restatement (oracle/rollout_torch.py)
+loss, per-trajectory features and x̂ of EVERY trajectory, per-trajectory u0 gradients AND the
+controller-parameter gradients — sums over all B·N (trajectory, step) terms — against the stock-torch restatement (oracle/rollout_torch.py)
 evaluated in fp64 on the same GPU, chunked over trajectories (independent until the batch mean,
 Functions.py:1463; each chunk's loss weighted by b_chunk / B). Metric: per tensor max|hip - ref| / max|ref|
 (SURVEY.md §8(d)); parity unpinned (no reference output exists at these sizes)."""
@@ -16,13 +16,17 @@ from conftest import load_case
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
-PER_TRAJ = ("loss", "command", "error", "prediction", "xhat", "g_u0")
+FEATS = ("loss", "command", "error", "prediction", "xhat")
 PARAMS = ("g_W_inp", "g_b_inp", "g_W_out")
 # kink band: trajectories whose fp64 rollout passes within DELTA of a ReLU / Hardtanh / constraint kink
-# (oracle.rollout_torch.kink_margin) can have an fp32 mask flipped against fp64 — an O(1) change of one
-# term's slope that any fp32 implementation shows (torch's own fp32 path included); at B·N ~ 10^6 a few
-# trajectories always do. They are compared separately, and the parameter sums re-checked without them.
+# (oracle.rollout_torch.kink_margin), where an fp32 mask can flip against fp64's: one term's SLOPE changes by O(1),
+# so only d loss / d u0 of that trajectory can move — every forward output is continuous across the kink and is
+# compared over ALL trajectories, and the parameter gradients are the full-batch sums, flips included.
 DELTA = 1e-5
+# a flipped mask swaps one of a trajectory's ~N (50 + 4) piecewise slopes; the kink-band g_u0 error must stay far
+# below O(1) of the batch's largest gradient (the worst seen: 1.9e-4) and be the exception, not the rule
+KINK_GU0_MAX = 1e-3
+KINK_GU0_FRAC = 1e-3   # at most this share of the batch may exceed the 1e-5 bar (flips), of B
 
 
 def _hip(params, Xd, Sd, N, precision):
@@ -46,44 +50,44 @@ def _hip(params, Xd, Sd, N, precision):
 
 def _err(a, r, rows=None):
     a, r = a.double(), r.reshape(a.shape)
+    den = r.abs().max()
     if rows is not None:
         a, r = a[rows], r[rows]
-    return float((a - r).abs().max() / r.abs().max())
+    return float((a - r).abs().max() / den) if a.numel() else 0.0
 
 
 def hip_and_oracle(params, B, N, seed, precision="fp32", chunk=16384):
-    """Returns (err, info): err holds per-trajectory errors over the trajectories outside the kink band,
-    parameter-gradient errors of the full batch ('<g>_full') and of the batch without the kink-band
-    trajectories (re-run on the GPU and the oracle: '<g>'), and the loss."""
+    """Returns (err, info). err: per-trajectory outputs over ALL trajectories, g_u0 outside the kink band, the
+    full-batch parameter gradients and the loss (each max|hip - ref| / max|ref| over the batch); info: the kink
+    band's size, its largest g_u0 error and how many of its trajectories exceed 1e-5."""
     X, S, _ = synth_inputs(B, N, seed)
     d = lambda a: torch.as_tensor(np.asarray(a, np.float32), device=DEV)
     Xd, Sd = d(X), d(S)
     got, u0 = _hip(params, Xd, Sd, N, precision)
     ref = T.loss_and_grads_chunked(params, Xd, u0, Sd, N, 20.0, device=DEV, chunk=chunk)
     reg = T.kink_margin(params, Xd.double(), ref["xhat"].reshape(B, N, 4)) > DELTA
-    err = {k: _err(got[k], ref[k], reg) for k in PER_TRAJ}
-    err.update({f"{k}_full": _err(got[k], ref[k]) for k in PARAMS})
+    err = {k: _err(got[k], ref[k]) for k in FEATS + PARAMS}
+    err["g_u0"] = _err(got["g_u0"], ref["g_u0"], reg)
     err["loss_scalar"] = _err(got["loss_scalar"], ref["loss_scalar"])
-    kink = (~reg).nonzero().reshape(-1)
-    info = {"kink_trajectories": int(kink.numel()),
-            "g_u0_err_in_kink_band": _err(got["g_u0"], ref["g_u0"], ~reg) if kink.numel() else 0.0}
-    del got, ref
-    idx = reg.nonzero().reshape(-1)
-    sub, u_sub = _hip(params, Xd[idx].contiguous(), Sd[idx].contiguous(), N, precision)
-    ref = T.loss_and_grads_chunked(params, Xd[idx], u_sub, Sd[idx], N, 20.0, device=DEV, chunk=chunk)
-    err.update({k: _err(sub[k], ref[k]) for k in PARAMS})
+    band = ~reg
+    e_band = (got["g_u0"].double() - ref["g_u0"]).abs()[band] / ref["g_u0"].abs().max()
+    info = {"kink_trajectories": int(band.sum()),
+            "g_u0_err_in_kink_band": float(e_band.max()) if e_band.numel() else 0.0,
+            "kink_above_1e-5": int((e_band > 1e-5).sum())}
     print({k: f"{v:.2e}" for k, v in err.items()}, info)
     return err, info
 
 
-def _check(err, info, B, tol_traj, tol_gu0, tol_grad, tol_loss):
-    assert info["kink_trajectories"] <= 0.05 * B, info
+def _check(err, info, B, tol_traj, tol_gu0, tol_grad, tol_loss, kink=True):
     assert err["loss_scalar"] <= tol_loss, err
-    assert max(err[k] for k in PER_TRAJ if k != "g_u0") <= tol_traj, err
-    assert err["g_u0"] <= tol_gu0, err
-    assert max(err[k] for k in PARAMS) <= tol_grad, err
-    # the kink-band flips move the full-batch parameter sums by a few terms out of B·N
-    assert max(err[f"{k}_full"] for k in PARAMS) <= 10 * tol_grad, err
+    assert max(err[k] for k in FEATS) <= tol_traj, err          # every trajectory, no exclusion
+    assert err["g_u0"] <= tol_gu0, err                           # outside the kink band
+    assert max(err[k] for k in PARAMS) <= tol_grad, err          # full-batch sums, flips included
+    if kink:   # the kink band's g_u0: bounded, and flips the exception
+        assert info["g_u0_err_in_kink_band"] <= KINK_GU0_MAX, info
+        assert info["kink_above_1e-5"] <= KINK_GU0_FRAC * B, info
+    else:      # reduced precision: the band is held to the mode's own g_u0 tolerance
+        assert info["g_u0_err_in_kink_band"] <= tol_gu0, info
 
 
 @pytest.fixture(scope="module")
@@ -106,7 +110,7 @@ def test_config3_full_batch_f16fwd(ref_params):
     (tests/test_gpu_precision.py)."""
     from test_gpu_precision import TOL_FEATS, TOL_GRADS_F16FWD_FULL, TOL_GU0_F16FWD, TOL_LOSS
     _check(*hip_and_oracle(ref_params, 262144, 10, 23, precision="f16fwd"), 262144, TOL_FEATS, TOL_GU0_F16FWD,
-           TOL_GRADS_F16FWD_FULL, TOL_LOSS)
+           TOL_GRADS_F16FWD_FULL, TOL_LOSS, kink=False)   # the f16 forward's own error exceeds the kink bar
 
 
 def test_config5_full_batch():

@@ -49,7 +49,9 @@ def test_small_and_fused_kernels_meet_oracle(name):
     for lim in (0, BIG):
         with small_limit(lim):
             o = run(params, c["X"], c["u0"], c["states"], c["N"], c["alpha"], c["noise"])
-        _check_oracle(o, c, name, "small" if lim else "fused")
+        fam = "small" if lim else "fused"
+        assert native.last_kernels() == (fam, fam), (name, lim, native.last_kernels())   # both passes ran it
+        _check_oracle(o, c, name, fam)
         outs[lim] = o
     for k in FEATS + ("xhat",):
         assert relerr(outs[BIG][k], outs[0][k]) <= 2e-6, (name, k, relerr(outs[BIG][k], outs[0][k]))
@@ -66,7 +68,7 @@ def _run_mixed(params, X, u0, S, N, lim_fwd, lim_bwd):
     with small_limit(lim_bwd):
         loss.backward()
     torch.cuda.synchronize()
-    out = {"g_u0": u0_t.grad.reshape(-1).cpu().numpy()}
+    out = {"g_u0": u0_t.grad.reshape(-1).cpu().numpy(), "families": native.last_kernels()}
     for k, name in GRADS[1:]:
         mod, attr = name.split(".")
         out[k] = getattr(getattr(ctrl, mod), attr).grad.cpu().numpy()
@@ -77,6 +79,8 @@ def _run_mixed(params, X, u0, S, N, lim_fwd, lim_bwd):
 def test_forward_of_one_family_backward_of_the_other(lim_fwd, lim_bwd):
     c, params = load_case("ref_b37_n25")
     o = _run_mixed(params, c["X"], c["u0"], c["states"], c["N"], lim_fwd, lim_bwd)
+    fam = lambda lim: "small" if lim else "fused"
+    assert o["families"] == (fam(lim_fwd), fam(lim_bwd)), o["families"]   # the backward ran on autograd's thread
     for k, _ in GRADS:
         assert relerr(o[k], c[f"{k}_64"]) <= TOL, (k, relerr(o[k], c[f"{k}_64"]))
 
@@ -116,4 +120,7 @@ def test_small_kernels_deterministic_and_dloss_linear():
 def test_default_limit_routes_the_reference_batch_to_the_small_kernels():
     prev = native.set_small_batch_limit(123)
     assert native.set_small_batch_limit(prev) == 123
-    assert prev == 8192   # per thread (tests/test_abi.py)
+    assert prev == 8192   # process-wide default (tests/test_abi.py)
+    c, params = load_case("ref_b15_n10")
+    run(params, c["X"], c["u0"], c["states"], c["N"], c["alpha"])
+    assert native.last_kernels() == ("small", "small")

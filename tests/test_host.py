@@ -34,13 +34,77 @@ def test_fnn_forward_matches_oracle():
     assert np.allclose(ctrl(x).detach().numpy()[:, 0], u_np, atol=1e-14)
 
 
-def test_mpcloss_refuses_cpu_tensors():
-    """No CPU fallback: the product path runs on the ROCm device or raises."""
+def _cpu_modules(params):
+    H = params["Whh"][0].shape[1]
+    sim = fca.LSTMModel(5, H, 4, 3)
+    ctrl = fca.FNNModel(3, params["W_inp"].shape[0], 1, 1)
+    t = lambda a: torch.as_tensor(np.asarray(a, np.float32))
+    with torch.no_grad():
+        for k in range(3):
+            getattr(sim.lstm, f"weight_ih_l{k}").copy_(t(params["Wih"][k]))
+            getattr(sim.lstm, f"weight_hh_l{k}").copy_(t(params["Whh"][k]))
+        sim.fc.weight.copy_(t(params["fcW"]))
+        sim.fc.bias.copy_(t(params["fcb"]))
+        ctrl.fc_inp.weight.copy_(t(params["W_inp"]))
+        ctrl.fc_inp.bias.copy_(t(params["b_inp"]))
+        ctrl.fc_out.weight.copy_(t(params["W_out"]))
+    return sim, ctrl
+
+
+def test_mpcloss_cpu_device_matches_fixture(golden):
+    """MPCLoss with device = cpu (the reference's no-GPU branch, UL/Main.py:38): the package's host path
+    (functions.MPCLoss._forward_host — the reference's op sequence on the caller's modules, not the oracle)
+    against the committed fp64 fixture at the 1e-5 bar: loss, loss features, x̂, d loss/d u0 and the
+    controller-parameter gradients after loss.backward()."""
+    from conftest import relerr
+    name, c, params = golden
+    sim, ctrl = _cpu_modules(params)
+    f32 = lambda a: torch.as_tensor(np.asarray(a, np.float32))
+    X, S = f32(c["X"]), f32(c["states"])
+    u0 = f32(c["u0"]).reshape(-1, 1).requires_grad_(True)
+    fn = fca.MPCLoss(prediction_horizon=c["N"], alpha=c["alpha"])
+    noise = None if c["noise"] is None else f32(c["noise"])
+    loss, f = fn(sim, ctrl, X, u0, S, "cpu", enable_noise=noise is not None, noise=noise)
+    loss.backward()
+    got = {k: v.detach().numpy() for k, v in f.items()}
+    got["xhat"] = fn.last_trajectory.numpy()
+    got["g_u0"] = u0.grad.reshape(-1).numpy()
+    g = lambda p: (p.grad if p.grad is not None else torch.zeros_like(p)).numpy()   # N = 1: no in-loss controller call
+    got["g_W_inp"], got["g_b_inp"], got["g_W_out"] = g(ctrl.fc_inp.weight), g(ctrl.fc_inp.bias), g(ctrl.fc_out.weight)
+    assert abs(loss.item() - float(c["loss64"])) <= 1e-5 * abs(float(c["loss64"]))
+    for k in ("loss", "command", "error", "prediction", "xhat", "g_u0", "g_W_inp", "g_b_inp", "g_W_out"):
+        assert relerr(got[k], c[f"{k}_64"]) <= 1e-5, (name, k, relerr(got[k], c[f"{k}_64"]))
+    # the reference's autograd also reaches the frozen LSTM's weights (never stepped, UL/Main.py:195)
+    assert all(p.grad is not None for p in sim.lstm.parameters())
+
+
+def test_mpcloss_cpu_noise_draws_in_reference_order():
+    """enable_noise on the CPU draws randn_like(x̂) * 0.01 after every surrogate call (Functions.py:1401, 1439):
+    with the generator reseeded, the same draws as a pre-drawn (B, N, 4) noise tensor taken in that order."""
+    from conftest import load_case
+    c, params = load_case("ref_b15_n10")
+    sim, ctrl = _cpu_modules(params)
+    X, S = torch.as_tensor(c["X"]), torch.as_tensor(c["states"])
+    u0 = torch.as_tensor(c["u0"]).reshape(-1, 1)
+    fn = fca.MPCLoss(prediction_horizon=c["N"], alpha=20.0)
+    torch.manual_seed(5)
+    l1, f1 = fn(sim, ctrl, X, u0, S, "cpu", enable_noise=True)
+    torch.manual_seed(5)
+    noise = torch.stack([torch.randn(X.shape[0], 4) * 0.01 for _ in range(c["N"])], dim=1)
+    l2, f2 = fn(sim, ctrl, X, u0, S, "cpu", enable_noise=True, noise=noise)
+    assert torch.equal(l1, l2) and torch.equal(f1["prediction"], f2["prediction"])
+    l3, _ = fn(sim, ctrl, X, u0, S, "cpu")
+    assert not torch.equal(l1, l3)
+
+
+def test_rollout_entry_refuses_cpu_tensors():
+    """The functional kernel entry (rollout.rollout) runs on the ROCm device or raises: no hidden fallback."""
     sim = fca.LSTMModel(5, 50, 4, 3)
     ctrl = fca.FNNModel(3, 50, 1, 1)
     X = torch.zeros(4, 3)
     with pytest.raises(RuntimeError, match="ROCm device only"):
-        fca.MPCLoss(10, 20.0)(sim, ctrl, X, ctrl(X), torch.zeros(4, 10, 5), "cpu")
+        fca.rollout.rollout(X, ctrl(X), torch.zeros(4, 10, 5), fca.functions._controller_params(ctrl),
+                            fca.functions._simulator_params(sim), 10, 20.0)
 
 
 def test_mpcloss_rejects_unsupported_models():
@@ -149,21 +213,23 @@ def test_inference_refuses_cpu_tensors():
         fca.simulate_step(sim, torch.zeros(2, 10, 5))
 
 
-def test_train_model_data_parallel_through_launcher_gloo(tmp_path):
-    """The launcher bench.py --gpus N uses (forging_control_amd.launch) starts 2 gloo ranks that each run the
-    real NeuralNetwork.train_model(grad_sync=GradAllReduce()) on UNEVEN shards of the reference's B = 15
-    batches (8/7, last batch 4/3): after two epochs both ranks hold bit-identical parameters equal to one
-    process training on the whole batches (train_model passes each rank's batch size to the hook)."""
+@pytest.mark.parametrize("ranks", [2, 8])
+def test_train_model_data_parallel_through_launcher_gloo(tmp_path, ranks):
+    """The launcher bench.py --gpus N uses (forging_control_amd.launch) starts N gloo ranks that each run the
+    real NeuralNetwork.train_model(grad_sync=GradAllReduce()) with the package's MPCLoss (CPU path) on UNEVEN
+    shards of the reference's B = 15 batches (2 ranks: 8/7, last batch 4/3; 8 ranks: 2/2/.../1, and the last
+    batch of 7 leaves rank 7 an EMPTY shard, which must still join the all-reduce): after two epochs every rank
+    holds bit-identical parameters equal to one process training on the whole batches."""
     import subprocess
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__))))
     import dp_train_worker as W
     script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dp_train_worker.py")
-    rc = subprocess.run([sys.executable, script, "--ranks", "2", "--out", str(tmp_path)], timeout=400).returncode
+    rc = subprocess.run([sys.executable, script, "--ranks", str(ranks), "--out", str(tmp_path)], timeout=400).returncode
     assert rc == 0
-    res = [np.load(tmp_path / f"rank{r}.npz") for r in (0, 1)]
-    assert all(int(r["world"]) == 2 for r in res)
-    assert np.array_equal(res[0]["params"], res[1]["params"])
+    res = [np.load(tmp_path / f"rank{r}.npz") for r in range(ranks)]
+    assert all(int(r["world"]) == ranks for r in res)
+    assert all(np.array_equal(res[0]["params"], r["params"]) for r in res[1:])
     ref_params, _ = W.train(W.global_batches())
     assert np.allclose(res[0]["params"], ref_params, rtol=0, atol=2e-6), np.abs(res[0]["params"] - ref_params).max()
     assert not np.allclose(ref_params, W.train(W.global_batches(), epochs=0)[0])   # training moved them
