@@ -24,6 +24,7 @@ struct CellIn {
     f32x4 h[Geo<HS>::HQ];   // split record of h_{t-1} (fcr_f16.h)
     f32x4 c[Geo<HS>::HQ];   // c_{t-1}
     f32x4 d[Geo<HS>::HQ];   // din = dx of the layer above at t (layers 0, 1)
+    f32x4 o[Geo<HS>::HQ];   // split record of the cell's own h_t (its tanh(c_t) = h_t / o_t: lstm_point_grad_h)
 };
 
 // Where the next cell's inputs live: buffer descriptors over this wave's own slab regions (SGPRs)
@@ -33,7 +34,7 @@ struct CellIn {
 // only those are fetched. A fetched-but-unused register would be reused at once, i.e. waited for.
 struct NextIn {
     __amdgpu_buffer_rsrc_t rh, rc, rx, rd;   // hseq, cseq, xw, dseq
-    uint32_t x, h, c, d;
+    uint32_t x, h, c, d, o;
 };
 
 template <int HS, int k = 0>
@@ -76,6 +77,9 @@ constexpr float kInvNegLog2e = 1.0f / kNegLog2e;
 // slots, which bounds every dgate) before the f16 split, and the products scaled back: both exact.
 // Schedule: region kb issues the transposed products of dgate block kb (slots 2kb, 2kb+1) beside the
 // recomputed forward tiles 2kb+2, 2kb+3 and their gradients, which form block kb+1.
+// OWN: the cell's own h_t record is in ci.o (every cell but the first of a window's layer-2 phase, whose h_9
+// only fed the readout): tanh(c_t) comes from it (lstm_point_grad_h) instead of being re-evaluated.
+// NX_OWN: the next cell's is fetched.
 #ifndef FCR_BWD_LAUNDER
 #define FCR_BWD_LAUNDER 1
 #endif
@@ -96,7 +100,8 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 #endif
 }
 
-template <int HS, bool L0, bool DIN, bool FIRST, bool NX_L0, bool NX_HC, bool NX_DIN, bool LP>
+template <int HS, bool L0, bool DIN, bool FIRST, bool NX_L0, bool NX_HC, bool NX_DIN, bool LP, bool OWN = true,
+          bool NX_OWN = true>
 __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, const float (&ext)[HS],
                                          float (&dh)[HS], float (&dc)[HS], float (&dxo)[HS], float &dxq,
                                          float &dx4, CellIn<HS> &ci, const NextIn &nx, Stamps &sp) {
@@ -118,8 +123,10 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
 
     float up, down, sg0, sgg;   // the trajectory's power-of-two scale, set once the incoming dh is in
 
-    // packed tail block (fcr_f16.h, fcr_img.h): its hi-image row read is the packed fragment
+    // packed tail block (fcr_f16.h, fcr_img.h): its hi-image row read is the packed fragment, and the
+    // transposed product's last output tile reads W_lo of its two real rows from the hi image's padding rows
     constexpr bool TAIL = !L0 && G::TAIL1;
+    constexpr bool TAILT = TAIL && !LP && (2 * HS) % 4 == 2;
     // ---- the recomputation's B operands (this cell's x_t and h_{t-1}) ----
     f16x8 bh[KB], bl[KB] = {};
     {
@@ -186,7 +193,8 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     auto slot_grad = [&](int r, f32x4 a, float *va, float *vb) {
         f32x4 P;
         f32x2 Q;
-        lstm_point_grad<FIRST>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], P, Q);
+        if (OWN) lstm_point_grad_h<FIRST>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], rec_h<HS>(ci.o, r), P, Q);
+        else lstm_point_grad<FIRST>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], P, Q);
         // torch LSTM semantics: dc = dc_carried + dh dh/dc; the carried dc of the cell below is dc f
         const float dcv = fmaf(dh[r], P[0], dc[r]);
         dc[r] = dcv * Q[1];
@@ -279,12 +287,15 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
 #pragma unroll
         for (int tau = 0; tau < NB; ++tau) {
             const uint32_t ct = 8u * (2 * (tau >> 1) + (tau & 1)) + 2 * kbb * TILE;
+            // the last tile of a packed-tail layer: its hi-image rows hold W_hi AND W_lo of the two real
+            // inputs (fcr_img.h), so the lo image is not read and its W_lo·dgate_hi product is not issued
+            const bool hi_only = TAILT && tau == NB - 1;
             f16x8 ah, al;
-            const f16x4 h0 = lds_tr_f16(tb + ct), l0 = LP ? f16x4{0, 0, 0, 0} : lds_tr_f16(tbl + ct);
+            const f16x4 h0 = lds_tr_f16(tb + ct), l0 = (LP || hi_only) ? f16x4{0, 0, 0, 0} : lds_tr_f16(tbl + ct);
             f16x4 h1 = {0, 0, 0, 0}, l1 = {0, 0, 0, 0};
             if (two) {
                 h1 = lds_tr_f16(tb + ct + TILE);
-                if (!LP) l1 = lds_tr_f16(tbl + ct + TILE);
+                if (!LP && !hi_only) l1 = lds_tr_f16(tbl + ct + TILE);
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -309,13 +320,18 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
 #pragma unroll
                 for (int k = 0; k < 4; ++k) a2[k] = a2[4 + k] = h0[k];
                 acc[tau] = mfma16(a2, __builtin_bit_cast(f16x8, u32x4{h[0], h[1], l[0], l[1]}), acc[tau]);
-                acc[tau] = mfma16(al, gh[cu], acc[tau]);
+                if (!hi_only) acc[tau] = mfma16(al, gh[cu], acc[tau]);
+            } else if (hi_only) {
+                acc[tau] = mfma16(ah, gl[cu], acc[tau]);
+                acc[tau] = mfma16(ah, gh[cu], acc[tau]);
             } else {
                 acc[tau] = mma_p<LP>(ah, al, gh[cu], gl[cu], acc[tau]);
             }
 #endif
         }
         if (kbb + 1 < KBB) dgate_block(kbb + 1, fa[(kbb + 1) % 3], gh[nu], gl[nu]);
+        // every slot's own h consumed: the next cell's record comes in (an L2 hit: this cell read it as h_{t-1})
+        if (NX_OWN && kbb + 2 == KBB) ld_quads<HS>(ci.o, nx.rh, nx.o, lane);
     }
     sched_fence();
     const unsigned long long t2 = stamp_now();
@@ -325,6 +341,10 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
         dxq = acc[HS >> 2][HS & 3] * down;
         dx4 = acc[(HS + 1) >> 2][(HS + 1) & 3] * down;
     } else {
+        if (TAILT) {   // the last tile's padding rows 2HS, 2HS+1 carry the W_lo terms of rows 2HS-2, 2HS-1
+            acc[NB - 1][0] += acc[NB - 1][2];
+            acc[NB - 1][1] += acc[NB - 1][3];
+        }
 #pragma unroll
         for (int s = 0; s < HS; ++s) {
             dxo[s] = acc[s >> 2][s & 3] * down;
@@ -430,6 +450,7 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         n.x = nl == 0 ? (uint32_t)((nj * kL + nt) * kWave * 8) : hoff(nj, nl > 0 ? nl - 1 : 0, nt);
         n.h = hoff(nj, nl, nt > 0 ? nt - 1 : 0);
         n.c = n.h;
+        n.o = hoff(nj, nl, nt);   // the next cell's own h_t (not stored for layer 2's t = 9: not fetched then)
         n.d = (uint32_t)((nl < 2 ? doff(nj, nl + 1, nt) : 0) * 16);
         return n;
     };
@@ -511,15 +532,17 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
         // t = 9 .. 2: the next cell is t-1 of the same layer; t = 1: the next is the FIRST cell (no
         // h, c); t = 0: the next is t = 9 of the layer below (or of layer 2 of the previous window)
-        for (int t = kL - 1; t >= 2; --t) {
+        // t = 9: h_9 of layer 2 only fed the readout (no split record), so this cell re-evaluates tanh(c_9)
+        bwd_cell<HS, false, false, false, false, true, false, LP, false>(L1.fb, L1.tb, lane, dh_out, dh, dc, dxo, unused0,
+                                                                    unused1, ci, next_of(j, 2, kL - 1), sp);
+        store_quads<HS>(dseq_w + doff(j, 2, kL - 1), dxo, lane);
 #pragma unroll
-            for (int r = 0; r < HS; ++r) dab[r] = (t == kL - 1) ? dh_out[r] : 0.0f;
+        for (int r = 0; r < HS; ++r) dab[r] = 0.0f;
+        for (int t = kL - 2; t >= 2; --t) {
             bwd_cell<HS, false, false, false, false, true, false, LP>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
                                                                 unused1, ci, next_of(j, 2, t), sp);
             store_quads<HS>(dseq_w + doff(j, 2, t), dxo, lane);
         }
-#pragma unroll
-        for (int r = 0; r < HS; ++r) dab[r] = 0.0f;
         bwd_cell<HS, false, false, false, false, false, false, LP>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
                                                              unused1, ci, next_of(j, 2, 1), sp);
         store_quads<HS>(dseq_w + doff(j, 2, 1), dxo, lane);
@@ -564,8 +587,8 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
             bwd_cell<HS, true, true, false, true, false, true, LP>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
                                                              next_of(j, 0, 1), sp);
             buf_st2(rr, lane * 8, (uint32_t)((j * kL + 1) * kWave * 8), f32x2{dxq * scq, dx4 * sc4});   // row j+1
-            bwd_cell<HS, true, true, true, false, true, false, LP>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq, dx4, ci,
-                                                             next_of(j, 0, 0), sp);
+            bwd_cell<HS, true, true, true, false, true, false, LP, true, false>(L0.fb, L0.tb, lane, dab, dh, dc, dxo, dxq,
+                                                                           dx4, ci, next_of(j, 0, 0), sp);
             buf_st2(rr, lane * 8, (uint32_t)((j * kL) * kWave * 8), f32x2{dxq * scq, dx4 * sc4});   // row j
         }
     }

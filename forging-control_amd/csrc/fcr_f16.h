@@ -25,9 +25,12 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 // Packed tail block (layers >= 1 when 2·HS = 8·(KB1-1) + 2, i.e. HS = 13): the last k-block holds
 // only combined slots 2HS-2, 2HS-1 (6 of its 8 k are zero padding), so its three split products go
-// into ONE MFMA over k = [A_hi B_hi | A_hi B_lo | A_lo B_hi | 0 0]: the A fragment carries
-// (hi σ0, hi σ1, hi σ0, hi σ1, lo σ0, lo σ1, 0, 0) and the B operand (hi, hi, lo, lo, hi, hi, 0, 0)
-// of the two slots. 10 instead of 12 MFMAs per tile and 13 % less fragment LDS at H = 50.
+// into ONE MFMA over k = [A_hi B_hi | A_lo B_hi | A_hi B_lo | 0 0]: the A fragment carries
+// (hi σ0, hi σ1, lo σ0, lo σ1, hi σ0, hi σ1, 0, 0) and the B operand (hi, hi, hi, hi, lo, lo, 0, 0)
+// of the two slots. 10 instead of 12 MFMAs per tile and 13 % less fragment LDS at H = 50. The lo copies
+// sit at k positions 2, 3 — combined slots 2HS, 2HS+1 of the backward's weight image (fcr_img.h) — so the
+// transposed product's last output tile, whose rows 2HS, 2HS+1 are padding, reads W_lo there from the hi
+// image and gets the W_lo·dgate_hi term for free (fcr_bwd.h).
 __host__ __device__ constexpr bool tail_packed(int HS) { return 2 * HS - 8 * ((2 * HS + 7) / 8 - 1) == 2; }
 
 template <int HS>
@@ -52,12 +55,12 @@ struct Geo16 {
 };
 
 // B operand of the packed tail block from the block's split halves (elements 0, 1 are the two real
-// slots): (hi, hi, lo, lo, hi, hi, 0, 0); the f16 mode keeps only the hi·hi part.
+// slots): (hi, hi, hi, hi, lo, lo, 0, 0); the f16 mode keeps only the hi·hi part.
 template <bool LP>
 __device__ __forceinline__ f16x8 tail_operand(f16x8 bh, f16x8 bl) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     const u32x4 h = __builtin_bit_cast(u32x4, bh), l = __builtin_bit_cast(u32x4, bl);
-    return __builtin_bit_cast(f16x8, LP ? u32x4{h[0], 0u, 0u, 0u} : u32x4{h[0], l[0], h[0], 0u});
+    return __builtin_bit_cast(f16x8, LP ? u32x4{h[0], 0u, 0u, 0u} : u32x4{h[0], h[0], l[0], 0u});
 }
 
 __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
@@ -343,9 +346,32 @@ __device__ __forceinline__ void rec_operand(int kb, float x0, float x1, const fl
 }
 
 // Cell update of one unit slot from its pre-activations a = (i, f, g, o), pre-scaled for exp2 (the
-// packed weights carry -log2e for i, f, o and 2 log2e for g): exp2 + add + rcp per activation.
+// packed weights carry -log2e for i, f, o and 2 log2e for g). The forward needs only c = f c_prev + i g
+// and h = o tanh(c), so each of the two products shares ONE reciprocal (e_x = exp2 of a pre-activation):
+//   i g      = (e_g - 1) / ((1 + e_i)(1 + e_g))          [fma(e_i, D_g, D_g), rcp, fma(e_g, r, -r)]
+//   o tanh c = (e_c - 1) / ((1 + e_o)(1 + e_c))          [e_c = exp2(2 log2e c)]
+// 8 transcendentals per slot instead of 10 (f keeps its own). Overflow: e_g is taken at min(a_g, 64), so
+// e_g stays finite and an infinite denominator (e_i or e_o = inf: i or o = 0) gives the product 0, as the
+// separate sigmoids do; |c| <= 10 (|c_t| <= |c_{t-1}| + 1 from zero), so e_c is finite. The backward's
+// recompute (lstm_point_grad*) evaluates i, f, g, o separately, as its local derivatives need them.
 // lstm_point_grad forms, from the same arithmetic, the six local derivatives the backward needs:
 // P = (dh/dc, dh/do, dc/di, dc/df) and Q = (dc/dg, f), each one fma from products the cell has.
+template <bool FIRST>
+__device__ __forceinline__ float lstm_gi_c(f32x4 a, float c_prev) {
+    const float f = sigm_pre(a[1]);
+    const float ei = __builtin_amdgcn_exp2f(a[0]);
+    const float eg = __builtin_amdgcn_exp2f(fminf(a[2], 64.0f));
+    const float dg = 1.0f + eg;
+    const float r = __builtin_amdgcn_rcpf(fmaf(ei, dg, dg));
+    const float gi = fmaf(eg, r, -r);
+    return FIRST ? gi : fmaf(f, c_prev, gi);           // c_{-1} = 0 (Functions.py:349-350)
+}
+__device__ __forceinline__ float lstm_h(float c, float eo) {
+    const float ec = __builtin_amdgcn_exp2f(c * 2.8853900817779268f);
+    const float dc = 1.0f + ec;
+    const float r = __builtin_amdgcn_rcpf(fmaf(eo, dc, dc));
+    return fmaf(ec, r, -r);
+}
 template <bool FIRST>
 __device__ __forceinline__ void lstm_point(f32x4 a, float c_prev, float &c, float &h) {
 #if FCR_ABLATE == 2   // diagnostic: the cell pointwise goes
@@ -353,38 +379,27 @@ __device__ __forceinline__ void lstm_point(f32x4 a, float c_prev, float &c, floa
     h = a[1];
     return;
 #endif
-    const float i = sigm_pre(a[0]);
-    const float f = sigm_pre(a[1]);
-    const float g = tanh_pre(a[2]);
-    const float o = sigm_pre(a[3]);
-    const float gi = g * i;
-    const float cf = FIRST ? 0.0f : f * c_prev;        // c_{-1} = 0 (Functions.py:349-350)
-    c = cf + gi;
-    h = o * tanh_f(c);
+    c = lstm_gi_c<FIRST>(a, c_prev);
+    h = lstm_h(c, __builtin_amdgcn_exp2f(a[3]));
 }
 // lstm_point in two stages (the same arithmetic in the same order), so the forward cell can spread a
-// tile pair's pointwise over the next pair's MFMA regions: A = gates and c, B = h from (c, o)
+// tile pair's pointwise over the next pair's MFMA regions: A = gates and c (and e_o), B = h from (c, e_o)
 template <bool FIRST>
-__device__ __forceinline__ void lstm_point_a(f32x4 a, float c_prev, float &c, float &o) {
+__device__ __forceinline__ void lstm_point_a(f32x4 a, float c_prev, float &c, float &eo) {
 #if FCR_ABLATE == 2
     c = a[0] + c_prev;
-    o = a[1];
+    eo = a[1];
     return;
 #endif
-    const float i = sigm_pre(a[0]);
-    const float f = sigm_pre(a[1]);
-    const float g = tanh_pre(a[2]);
-    o = sigm_pre(a[3]);
-    const float gi = g * i;
-    const float cf = FIRST ? 0.0f : f * c_prev;
-    c = cf + gi;
+    c = lstm_gi_c<FIRST>(a, c_prev);
+    eo = __builtin_amdgcn_exp2f(a[3]);
 }
-__device__ __forceinline__ void lstm_point_b(float c, float o, float &h) {
+__device__ __forceinline__ void lstm_point_b(float c, float eo, float &h) {
 #if FCR_ABLATE == 2
-    h = o;
+    h = eo;
     return;
 #endif
-    h = o * tanh_f(c);
+    h = lstm_h(c, eo);
 }
 template <bool FIRST>
 __device__ __forceinline__ void lstm_point_grad(f32x4 a, float c_prev, f32x4 &P, f32x2 &Q) {
@@ -402,6 +417,43 @@ __device__ __forceinline__ void lstm_point_grad(f32x4 a, float c_prev, f32x4 &P,
     const float cn = cf + gi;
     const float tc = tanh_f(cn);
     const float h = o * tc;
+    P = f32x4{fmaf(-h, tc, o), fmaf(-h, o, h), fmaf(-gi, i, gi), fmaf(-cf, f, cf)};
+    Q = f32x2{fmaf(-gi, g, i), f};
+}
+
+// h of unit slot s from its split record (split_rec: hi at half s, lo at half HS + s of the record words):
+// hi + lo in ONE v_fma_mix_f32 (f16 sources picked by op_sel; exact in fp32) — the compiler's form of the
+// same sum is two conversions and an add. A VALU-to-VALU dependency: no MFMA operand hazard. s is a
+// compile-time constant once the cell is unrolled: one of the four op_sel forms survives.
+template <int HS>
+__device__ __forceinline__ float rec_h(const f32x4 *rec, int s) {
+    const int wh = s >> 1, wl = (HS + s) >> 1;
+    const float a = rec[wh >> 2][wh & 3], b = rec[wl >> 2][wl & 3];
+    float r;
+#define FCR_MIX_H(SA, SB) asm("v_fma_mix_f32 %0, %1, 1.0, %2 op_sel:[" #SA ",0," #SB "] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(b))
+    if ((s & 1) == 0 && ((HS + s) & 1) == 0) FCR_MIX_H(0, 0);
+    else if ((s & 1) == 0) FCR_MIX_H(0, 1);
+    else if (((HS + s) & 1) == 0) FCR_MIX_H(1, 0);
+    else FCR_MIX_H(1, 1);
+#undef FCR_MIX_H
+    return r;
+}
+
+// lstm_point_grad with tanh(c_t) recovered from the cell's own h_t (the forward's h_t = o tanh(c_t) with
+// o = 1/(1 + e_o), so tanh(c_t) = h_t (1 + e_o), one multiply by the denominator the sigmoid already formed)
+// instead of re-evaluated (exp2, rcp and three VALU): the same six local derivatives. h is the forward's h_t
+// as its split record holds it (fp32-accurate; f16-subnormal h only perturbs P by the record's absolute
+// 2^-25, below the gradients' fp32 level).
+template <bool FIRST>
+__device__ __forceinline__ void lstm_point_grad_h(f32x4 a, float c_prev, float h, f32x4 &P, f32x2 &Q) {
+    const float i = sigm_pre(a[0]);
+    const float f = sigm_pre(a[1]);
+    const float g = tanh_pre(a[2]);
+    const float d_o = 1.0f + __builtin_amdgcn_exp2f(a[3]);
+    const float o = __builtin_amdgcn_rcpf(d_o);
+    const float gi = g * i;
+    const float cf = FIRST ? 0.0f : f * c_prev;
+    const float tc = h * d_o;
     P = f32x4{fmaf(-h, tc, o), fmaf(-h, o, h), fmaf(-gi, i, gi), fmaf(-cf, f, cf)};
     Q = f32x2{fmaf(-gi, g, i), f};
 }
@@ -455,12 +507,12 @@ __device__ __forceinline__ void pack_fwd16_item(const PackArgs &a, int l, _Float
     const int kb = rk % KB, r = rk / KB;
     const int rho = lane & 15, kq = lane >> 4;
     const int unit = 4 * r + (rho >> 2), gate = rho & 3;
-    if (tail && kb == KB - 1) {   // packed tail: (hi s0, hi s1, hi s0, hi s1, lo s0, lo s1, 0, 0)
+    if (tail && kb == KB - 1) {   // packed tail: (hi s0, hi s1, lo s0, lo s1, hi s0, hi s1, 0, 0)
         _Float16 out = (_Float16)0.0f;
         if (j < 6) {
             const float v = fwd16_weight(a, l, unit, gate, 8 * kb + (j & 1), kq);
             const _Float16 hi = (_Float16)v;
-            out = j < 4 ? hi : (_Float16)(v - (float)hi);
+            out = (j == 2 || j == 3) ? (_Float16)(v - (float)hi) : hi;
         }
         dst[((size_t)rk * kWave + lane) * 8 + j] = out;
         return;

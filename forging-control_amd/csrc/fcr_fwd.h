@@ -95,7 +95,7 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
     if (R0 + 1 < R1) rd(R0 + 1, KLO, ah[1], al[1]);
     f32x4 prev[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
     constexpr int R = KHI - KLO;   // regions per tile pair
-    float po[2] = {0.0f, 0.0f};    // output gates of the previous pair between the pointwise stages
+    float po[2] = {0.0f, 0.0f};    // exp2 of the previous pair's output-gate pre-activations between the stages
 #pragma unroll
     for (int p = P0; p < P1; ++p) {
         const int r0 = 2 * p, r1 = 2 * p + 1;

@@ -61,9 +61,10 @@ inline int img_pack_threads(int HS, int l) { return 16 * HS * 4 * img_units(img_
 // One thread per (image row, column): value W[gate*H + unit][input of (σ, grp)], pre-scaled for exp2
 // like the forward fragments (the backward divides its dgates by the same per-gate factor). With a
 // packed tail (tail_packed, fcr_f16.h) the hi image's last k-block carries, in its padding columns
-// σ = 2HS .. 2HS+3, the copies (hi σ0, hi σ1, lo σ0, lo σ1) of its two real slots, so the recompute's
-// row read of that block IS the packed tail fragment; the transposed product never reads those
-// columns as anything but unused output rows, and the lo image keeps zeros there.
+// σ = 2HS .. 2HS+3, the copies (lo σ0, lo σ1, hi σ0, hi σ1) of its two real slots σ0, σ1, so the
+// recompute's row read of that block IS the packed tail fragment; the transposed product's last output
+// tile reads rows σ0, σ1, 2HS, 2HS+1 of the hi image — W_hi and W_lo of the two real slots — so its
+// hi-image products carry the W_lo·dgate term too (fcr_bwd.h); the lo image keeps zeros there.
 __device__ __forceinline__ void pack_img_item(const PackArgs &a, int l, _Float16 *dst, int idx) {
     const int H = a.H, HS = a.HS;
     const int nsl = l == 0 ? HS + 2 : 2 * HS;
@@ -103,7 +104,7 @@ __device__ __forceinline__ void pack_img_item(const PackArgs &a, int l, _Float16
     if (l > 0 && tail_packed(HS) && jt >= 2 && jt < 6) {
         const float v = weight(8 * (kbn - 1) + (jt & 1));
         const _Float16 vh = (_Float16)v;
-        hi = jt < 4 ? vh : (_Float16)(v - (float)vh);
+        hi = jt < 4 ? (_Float16)(v - (float)vh) : vh;
         lo = (_Float16)0.0f;
     } else {
         const float v = weight(sg);
