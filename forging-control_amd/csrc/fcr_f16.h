@@ -360,7 +360,8 @@ template <bool FIRST>
 __device__ __forceinline__ float lstm_gi_c(f32x4 a, float c_prev) {
     const float f = sigm_pre(a[1]);
     const float ei = __builtin_amdgcn_exp2f(a[0]);
-    const float eg = __builtin_amdgcn_exp2f(fminf(a[2], 64.0f));
+    // min(a_g, 64) as ONE v_med3_f32 (fminf adds a canonicalising v_max of the MFMA result in front of it)
+    const float eg = __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(a[2], -1e30f, 64.0f));
     const float dg = 1.0f + eg;
     const float r = __builtin_amdgcn_rcpf(fmaf(ei, dg, dg));
     const float gi = fmaf(eg, r, -r);
