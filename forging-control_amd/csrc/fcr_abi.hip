@@ -25,6 +25,7 @@
 #include "fcr_small.h"
 #include "fcr_surrogate.h"
 #include "fcr_wide.h"
+#include "fcr_wbwd.h"
 #include "fcr_wgemm.h"
 
 namespace fcr {
@@ -80,6 +81,17 @@ constexpr int kMaxSlots = 13;
 constexpr int kMaxWideH = 2048;   // H > 4*kMaxSlots: the GEMM-per-cell path (fcr_wide.h)
 bool is_wide(const fcr_dims *d) { return d->H > 4 * kMaxSlots; }
 int slot_tier(int H) { return H <= 16 ? 4 : (H <= 32 ? 8 : 13); }
+
+// H > 52: the backward's gradient products on the hand-written split-f16 kernel (fcr_wbwd.h) when its k-blocks
+// tile 4H and layer 0's window-row gradient is formed in the cell kernel (rowg_in_cell); rocBLAS otherwise.
+// FCR_WIDE_HWBWD=0 builds the rocBLAS path for comparison.
+#ifndef FCR_WIDE_HWBWD
+#define FCR_WIDE_HWBWD 1
+#endif
+bool wide_hwbwd_ok(int H) {
+    const bool rowg_cell = H % 4 == 0 && 64 % (H / 4) == 0;   // rowg_in_cell (below)
+    return FCR_WIDE_HWBWD && H % 8 == 0 && rowg_cell;
+}
 
 int check_dims(const fcr_dims *d) {
     if (!d) return fail(FCR_EINVAL, "dims is NULL");
@@ -258,6 +270,7 @@ struct WideLayout {
     // split-f16 gate GEMM operands (fcr_wide.h: forward A per layer, backward A per weight, the cells'
     // operand rows XB [3][10][B][6H] (layer 0 rows 3H + kX16 long), the dgate rows [B][12H])
     size_t fa[3], bih[3], XB, dGsp, consts;   // bih: layers >= 1 backward A [12H][2H]
+    size_t bt[3];     // hand-written gradient product (fcr_wbwd.h): W^T split [NO][4H] hi, then lo
     size_t bx0, E0;   // layer 0's backward A [12H][H + 8] and its product rows [B][H + 8]
     // kept windows (the last `keep` of N): the forward's gate pre-activations and c per cell
     // [keep][3][10][B][4H] / [keep][3][10][B][H], so the backward skips their recompute (wide_keep_fit)
@@ -298,9 +311,12 @@ WideLayout make_wide(const fcr_dims *d, int with_backward, int keep = 0) {
     L.Cs = take(F * kLayers * kL * B * H);
     L.G = take(F * B * 4 * H);
     const size_t F16 = sizeof(_Float16), WW = 4 * H * H;
+    const bool hw = wide_hwbwd_ok((int)H);
     for (int l = 0; l < kLayers; ++l) {
         L.fa[l] = take(l == 0 ? F16 * 4 * H * (3 * H + kX16) : F16 * WW * 6);
-        if (with_backward) {
+        if (with_backward && hw) {
+            L.bt[l] = take(F16 * 2 * (l == 0 ? H : 2 * H) * 4 * H);
+        } else if (with_backward) {
             if (l > 0) {
                 L.bih[l] = take(F16 * 6 * WW);   // [12H][2H]: W_ih | W_hh per split row (wide_split_bcat_kernel)
             } else {
@@ -430,7 +446,7 @@ int gemm16_bwd(rocblas_handle h, int B, int n, int H, const _Float16 *A, int lda
 
 // Device pointers of the split-f16 operands (rollout only; the surrogate's training step stays fp32)
 struct WideSplit {
-    const _Float16 *fa[kLayers], *bih[kLayers];
+    const _Float16 *fa[kLayers], *bih[kLayers], *bt[kLayers];
     _Float16 *XB, *dGsp;
     float *consts;
     const _Float16 *bx0;
@@ -442,6 +458,7 @@ WideSplit wide_split(const WideLayout &L, char *base) {
     for (int l = 0; l < kLayers; ++l) {
         w.fa[l] = (const _Float16 *)(base + L.fa[l]);
         w.bih[l] = L.bih[l] ? (const _Float16 *)(base + L.bih[l]) : nullptr;
+        w.bt[l] = L.bt[l] ? (const _Float16 *)(base + L.bt[l]) : nullptr;
     }
     w.XB = (_Float16 *)(base + L.XB);
     w.dGsp = L.dGsp ? (_Float16 *)(base + L.dGsp) : nullptr;
@@ -462,6 +479,15 @@ int wide_pack_split(const float *const *w_ih, const float *const *w_hh, int H, b
                            (int)(l == 0), wsc, (_Float16 *)sp.fa[l]);
         if ((rc = launch_check("wide_split_fa_kernel"))) return rc;
         if (!backward) continue;
+        if (sp.bt[l]) {   // hand-written gradient product: W^T split, [NO][4H] hi then lo
+            const int NO = l == 0 ? H : 2 * H;
+            const size_t nbt = (size_t)NO * 4 * H;
+            _Float16 *hi = (_Float16 *)sp.bt[l];
+            hipLaunchKernelGGL(wide_split_bt_kernel, dim3((unsigned)((nbt + 255) / 256)), dim3(256), 0, s,
+                               l == 0 ? (const float *)nullptr : w_ih[l], w_hh[l], H, NO, hi, hi + nbt);
+            if ((rc = launch_check("wide_split_bt_kernel"))) return rc;
+            continue;
+        }
         if (l == 0) {
             const size_t nb0 = (size_t)12 * H * (H + 8);
             hipLaunchKernelGGL(wide_split_bx0_kernel, dim3((unsigned)((nb0 + 255) / 256)), dim3(256), 0, s, w_ih[0], w_hh[0],
@@ -529,20 +555,20 @@ constexpr int kRowgT = FCR_ROWG_T;
 template <bool PRE>
 int launch_cell_bwd(int B, int H, hipStream_t s, const float *act, const float *c, const float *c_prev,
                     const float *dH, const float *din, float *dC, float *dG, _Float16 *dgsp, const float *consts,
-                    int dh_scaled, int ldh, int ldx, const float *wih0 = nullptr, float *rowg = nullptr) {
+                    int dh_scaled, int ldh, int ldx, const float *wih0 = nullptr, float *rowg = nullptr, int dg3 = 1) {
     const int V = cell_vec(H);
     const dim3 grid((unsigned)(((size_t)B * (H / V) + 255) / 256)), blk(256);
     if (rowg && (V != 4 || 64 % (H / V)))
         return fail(FCR_EINVAL, "wide_cell_bwd_kernel: in-kernel row gradient needs 64 %% (H / 4) == 0 (H = %d)", H);
     if (rowg) {   // layer 0: kRowgT trajectories per thread share one load of its W_ih0 rows
         const dim3 g0((unsigned)(((size_t)(B + kRowgT - 1) / kRowgT * (H / V) + 255) / 256));
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4, kRowgT>), g0, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, wih0, rowg);
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4, kRowgT>), g0, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, dg3, wih0, rowg);
     } else if (V == 4)
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H);
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, dg3);
     else if (V == 2)
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 2>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H);
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 2>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, dg3);
     else
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 1>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H);
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 1>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, dg3);
     return launch_check("wide_cell_bwd_kernel");
 }
 // the in-kernel layer-0 row gradient applies when a trajectory's cell threads (H / 4) tile a wave
@@ -591,6 +617,36 @@ int launch_wgemm_cell(const WgArgs &wa, hipStream_t s) {
     const int nx = (wa.B + kWgN - 1) / kWgN, ny = wa.H / kWgU;
     hipLaunchKernelGGL(wide_gemm_cell_kernel, dim3((unsigned)(nx * ny)), dim3(kWgThreads), kWgLds, s, wa);
     return launch_check("wide_gemm_cell_kernel");
+}
+
+// dX' (row-major [B][ldo], columns [0, NO)) = dGs W on the hand-written split-f16 kernel (fcr_wbwd.h), in the
+// dgates' scaled units like gemm16_bwd; bt = W^T split [NP][4H] hi then lo (NP packed rows; the product uses the
+// first NO <= NP of them), dGs = [hi 4H | lo 4H | (hi 4H)] rows
+int launch_wb(const _Float16 *bt, int NP, int NO, int H, int B, const _Float16 *dGs, float *dX, int ldo, hipStream_t s) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        const hipError_t e = hipFuncSetAttribute((const void *)wide_bwd_gemm_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kWbLds);
+        if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(wbwd): %s", hipGetErrorString(e));
+        attr_set = true;
+    }
+    WbArgs wa{};
+    wa.Ahi = bt;
+    wa.Alo = bt + (size_t)NP * 4 * H;
+    wa.B = dGs;
+    wa.out = dX;
+    wa.lda = 4 * H;
+    wa.ldb = 12 * H;
+    wa.lo_off = 4 * H;
+    wa.ldo = ldo;
+    wa.NB = B;
+    wa.NO = NO;
+    wa.K = 4 * H;
+    if (NO <= 0 || NO > NP || NO % 16 || wa.K % kWbK || B <= 0 || ldo % 4)
+        return fail(FCR_EINVAL, "wide_bwd_gemm_kernel: NO %d K %d B %d ldo %d off its tiling", NO, wa.K, B, ldo);
+    const int nx = (B + kWbN - 1) / kWbN, ny = (NO + kWbM - 1) / kWbM;
+    hipLaunchKernelGGL(wide_bwd_gemm_kernel, dim3((unsigned)(nx * ny)), dim3(kWbThreads), kWbLds, s, wa);
+    return launch_check("wide_bwd_gemm_kernel");
 }
 
 // One window's cells, forward: 3 layers x 10 steps of [GEMM x_t W_ih^T, GEMM h_{t-1} W_hh^T, cell].
@@ -794,12 +850,17 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
                                                 nullptr, sp.dGsp, sp.consts,
                                                 l < kLayers - 1 || t < kL - 1,   // (2, 9): the head's dH
                                                 ldh, 2 * H, rg ? wih[0] : nullptr,
-                                                rg ? a.rowg + (size_t)(j + t) * B * kIn : nullptr)))
+                                                rg ? a.rowg + (size_t)(j + t) * B * kIn : nullptr, sp.bt[0] ? 0 : 1)))
                     return rc;
-                if (l > 0) {   // [input gradient | dh_{t-1}] (t = 0: the former only) into D[l-1] row t
+                if (l > 0 && sp.bt[l]) {   // [input gradient | dh_{t-1}] (t = 0: the former only), hand-written product
+                    if ((rc = launch_wb(sp.bt[l], 2 * H, t > 0 ? 2 * H : H, H, B, sp.dGsp, D[l - 1] + (size_t)t * 2 * cell, 2 * H, s)))
+                        return rc;
+                } else if (l > 0) {   // [input gradient | dh_{t-1}] (t = 0: the former only) into D[l-1] row t
                     if ((rc = gemm16_bwd(h, B, t > 0 ? 2 * H : H, H, sp.bih[l], 2 * H, sp.dGsp, D[l - 1] + (size_t)t * 2 * cell,
                                          2 * H)))
                         return rc;
+                } else if (rg && sp.bt[0]) {   // layer 0, row gradient done: dh_{t-1} only (t = 0: nothing)
+                    if (t > 0 && (rc = launch_wb(sp.bt[0], H, H, H, B, sp.dGsp, sp.E0, LE, s))) return rc;
                 } else if (rg) {   // layer 0, row gradient done: dh_{t-1} only (t = 0: nothing)
                     if (t > 0 && (rc = gemm16_bwd(h, B, H, H, sp.bx0, H8, sp.dGsp, sp.E0, LE))) return rc;
                 } else {

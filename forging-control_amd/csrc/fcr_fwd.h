@@ -340,6 +340,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             if (STORE) store_quads<HS>(SEQ_C(l, 0), c, lane);
 #pragma unroll
             for (int r = 0; r < HS; ++r) xc[r] = xn[r];
+#pragma unroll 3
             for (int t = 1; t < kL; ++t) {
                 load_quads<HS>(xn, SEQ_H(l - 1, t + 1 < kL ? t + 1 : t), lane);
                 fwd16_cell<HS, false, false, LP>(lwc, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);

@@ -285,7 +285,7 @@ __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restr
                                      const float *__restrict__ c_prev, const float *__restrict__ dH,
                                      const float *__restrict__ din, float *dC, float *dG, _Float16 *dgsp,
                                      const float *__restrict__ consts, int dh_scaled, int ldh, int ldx, int B,
-                                     int H, const float *__restrict__ wih0 = nullptr, float *rowg = nullptr) {
+                                     int H, int dg3, const float *__restrict__ wih0 = nullptr, float *rowg = nullptr) {
     using W = WideVec<V>;
     // with consts (split-f16 rollout) din, and dH unless it is the head's, come from gemm16_bwd in the
     // scaled units of the dgates: back by 1/scale = consts[0], one fp32 product each
@@ -342,7 +342,8 @@ __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restr
 #pragma unroll
             for (int k = 0; k < 4; ++k) W::st(d4 + k * H, dg[k]);
         }
-        if (dgsp) {   // split-f16 operand row [hi | lo | hi] of W^T dG, scaled into the f16 range (wide_bscale_kernel)
+        if (dgsp) {   // split-f16 operand row [hi | lo | hi] of W^T dG, scaled into the f16 range (wide_bscale_kernel);
+            // the hand-written product (fcr_wbwd.h) reads hi and lo once each: no third copy (dg3 = 0)
             const float sc = consts[3];
             _Float16 *o16 = dgsp + b * 12 * H + u;
 #pragma unroll
@@ -356,7 +357,7 @@ __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restr
                 }
                 W::st16(o16 + k * H, hi);
                 W::st16(o16 + (4 + k) * H, lo);
-                W::st16(o16 + (8 + k) * H, hi);
+                if (dg3) W::st16(o16 + (8 + k) * H, hi);
             }
         }
         W::st(dC + idx, dco);
