@@ -49,14 +49,15 @@ def hbm_bytes_per_rollout_step(N=10):
     return (12 + 200 + 3 * 4 + 4 * N) / N
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, suffix=""):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of this workload
-    (profiles/round<k>_pmc.json, scripts/profile_round.sh; older profiles/r<k>_pmc.json otherwise), or None."""
+    (profiles/round<k><suffix>_pmc.json, scripts/profile_round.sh; older profiles/r<k>_pmc.json otherwise), or
+    None. suffix "_c5": config 5's summary, whose "bwd_pass" entry is the HBM bytes of one whole backward pass."""
     import glob
     import re
     pick = []
     for f in glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")):
-        m = re.fullmatch(r"(round|r)(\d+)([a-z]?)_pmc\.json", os.path.basename(f))   # the rollout's, not the plant's
+        m = re.fullmatch(r"(round|r)(\d+)([a-z]?)" + suffix + r"_pmc\.json", os.path.basename(f))   # the rollout's
         if m:
             pick.append((m.group(1) == "round", int(m.group(2)), m.group(3), f))
     if not pick:
@@ -380,20 +381,24 @@ def main():
         wide_label = {   # H > 52 (fcr_wide.h / fcr_wgemm.h); the fused cell kernel needs H % 64 == 0
             "fwd": "wide_gemm_cell_kernel (hand-written split-f16 GEMM + cell update)" if H % 64 == 0 else
                    "rocBLAS split-f16 gate GEMM + wide_cell_kernel",
-            "bwd": ("recompute wide_gemm_cell_kernel" if H % 64 == 0 else "recompute rocBLAS gate GEMM + wide_cell_kernel")
-                   + " + wide_cell_bwd_kernel + rocBLAS split-f16 [input grad | dh] and weight-gradient products"}
+            "bwd": ("backward pass: recompute wide_gemm_cell_kernel" if H % 64 == 0 else
+                    "backward pass: recompute rocBLAS gate GEMM + wide_cell_kernel")
+                   + " + wide_cell_bwd_kernel + hand-written split-f16 [input grad | dh] product wide_bwd_gemm_kernel"}
         kernel = (f"fcr_s{dom[0]}_kernel" if small else f"fcr_{dom[0]}_kernel") if narrow else wide_label[dom[0]]
         achieved = B * N * fl[dom[0]] / (dom[1] * 1e-3) / 1e12
         hbm_roof = HBM_PEAK_GBS * 1e9 / hbm_bytes_per_rollout_step(N)
         default_cfg = (B, N, H, args.precision) == (65536, 10, 50, "fp32")
-        traffic, traffic_src = pmc_traffic(f"fcr_{dom[0]}_kernel") if default_cfg else (None, None)
+        c5_cfg = (B, N, H, args.precision) == (65536, 25, 256, "fp32")
+        traffic, traffic_src = (pmc_traffic(f"fcr_{dom[0]}_kernel") if default_cfg else
+                                pmc_traffic("bwd_pass", "_c5") if c5_cfg and dom[0] == "bwd" else (None, None))
         # ceiling of the arithmetic as executed: an fp32-accurate product is three f16 MFMA products
         # (hi.hi + hi.lo + lo.hi, fcr_f16.h), so the fp32-equivalent ceiling is the f16 peak / 3;
         # in the reduced-precision pass one f16 product each
         f16_pass = args.precision == "f16" or (args.precision == "f16fwd" and dom[0] == "fwd")
         peak = F16_PEAK_TFLOPS if f16_pass else F16_PEAK_TFLOPS / 3
         roof = {"bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
-                "frac": achieved / peak, "traffic": traffic, "traffic_unit": "bytes/launch",
+                "frac": achieved / peak, "traffic": traffic,
+                "traffic_unit": "bytes/launch" if narrow else "bytes per backward pass (all its dispatches)",
                 "traffic_source": traffic_src,
                 "achieved_def": f"algorithmic {fl[dom[0]]} FLOP per rollout-step x B*N / mean HIP-event time of the "
                                 f"{dom[0]} pass over the timed steps",

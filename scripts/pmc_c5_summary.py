@@ -1,0 +1,55 @@
+"""Config-5 PMC summary (scripts/profile_round3.sh): HBM bytes per launch of the main H = 256 kernels, and the
+HBM bytes of one whole backward pass (every dispatch from wide_bscale_kernel to the ctrl_grad_kernel after it),
+FETCH_SIZE / WRITE_SIZE in separate passes with the gfx950 correction (2 x FETCH + WRITE, MI355X_MICROARCH.md).
+    python scripts/pmc_c5_summary.py TAG DIR  ->  profiles/TAG_c5_pmc.json"""
+import csv
+import glob
+import json
+import sys
+
+tag, root = sys.argv[1], sys.argv[2]
+KERNELS = ("wide_gemm_cell_kernel", "wide_bwd_gemm_kernel", "wide_cell_bwd_kernel")
+
+
+def dispatches(kind, counter):
+    f = glob.glob(f"{root}/{kind}/**/*counter_collection.csv", recursive=True)
+    by = {}
+    for r in (csv.DictReader(open(f[0])) if f else []):
+        if r["Counter_Name"] != counter:
+            continue
+        k = int(r["Dispatch_Id"])
+        name, v = by.get(k, (r["Kernel_Name"], 0.0))
+        by[k] = (name, v + float(r["Counter_Value"]))
+    return [by[k] for k in sorted(by)]
+
+
+out = {}
+passes = {}
+for kind, cnt in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+    ds = dispatches(kind, cnt)
+    for name in KERNELS:
+        vals = [v for n, v in ds if name in n]
+        if vals:
+            out.setdefault(name, {})[cnt + "_KB_per_launch"] = sum(vals) / len(vals)
+            out[name]["launches"] = len(vals)
+    # backward passes: wide_bscale_kernel .. the next ctrl_grad_kernel (inclusive); the last one profiled counts
+    tot, on, last = 0.0, False, None
+    for n, v in ds:
+        if "wide_bscale_kernel" in n:
+            on, tot = True, 0.0
+        if on:
+            tot += v
+        if on and "ctrl_grad_kernel" in n:
+            on, last = False, tot
+    passes[cnt] = last
+for name, d in out.items():
+    if "FETCH_SIZE_KB_per_launch" in d and "WRITE_SIZE_KB_per_launch" in d:
+        d["hbm_bytes_corrected"] = (2 * d["FETCH_SIZE_KB_per_launch"] + d["WRITE_SIZE_KB_per_launch"]) * 1024
+if passes.get("FETCH_SIZE") is not None and passes.get("WRITE_SIZE") is not None:
+    out["bwd_pass"] = {"FETCH_SIZE_KB": passes["FETCH_SIZE"], "WRITE_SIZE_KB": passes["WRITE_SIZE"],
+                       "hbm_bytes_corrected": (2 * passes["FETCH_SIZE"] + passes["WRITE_SIZE"]) * 1024}
+out["_note"] = ("rocprofv3 PMC passes of bench.py --hidden 256 --horizon 25 --batch 65536 (config 5), KB; "
+                "hbm_bytes_corrected = 2*FETCH + WRITE (gfx950). bwd_pass = every dispatch of the last profiled "
+                "backward pass, wide_bscale_kernel .. ctrl_grad_kernel.")
+json.dump(out, open(f"profiles/{tag}_c5_pmc.json", "w"), indent=1)
+print(json.dumps(out, indent=1))
