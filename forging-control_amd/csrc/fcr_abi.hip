@@ -23,6 +23,7 @@
 #include "fcr_pack.h"
 #include "fcr_host.h"
 #include "fcr_small.h"
+#include "fcr_sur.h"
 #include "fcr_surrogate.h"
 #include "fcr_wide.h"
 #include "fcr_wbwd.h"
@@ -1025,6 +1026,214 @@ WideArgs lstm_args(const fcr_dims *d, const LstmLayout &L, char *base) {
     return a;
 }
 
+// ------------------------------------------------------------------------------------------------
+// LSTM surrogate, H <= 52: the rollout's fused split-f16 cells over one window (fcr_sur.h). Workspace:
+// the packed fragments / images / readout as the rollout packs them, the window-batch slabs, and for the
+// backward the dgate slab, its scales and the weight-gradient partials.
+struct SurLayout {
+    int HS, nw, nw_pad, groups;
+    size_t fa[3], img[3], fcp, fcb, fnp, wsc, rng, hseq, cseq, xw, htop, dseq, dgs, dsc, part, total;
+};
+inline int sur_kbb(int HS) { return (HS + 1) / 2; }
+// weight-gradient k-blocks: groups of kSurKW backward waves x kL / kSurKC step groups (a missing last wave of a
+// group reads a padding wave of the slabs, whose dgates and scales the backward wrote as zero)
+inline int sur_nkb(int nw) { return (nw + kSurKW - 1) / kSurKW * (kL / kSurKC); }
+inline size_t sur_part_floats(int HS, bool l0) {
+    const int RA = (2 * HS + 3) / 4, NT = l0 ? RA + 1 : 2 * RA;
+    return (size_t)16 * HS * 16 * NT;
+}
+SurLayout make_sur(const fcr_dims *d, int with_backward) {
+    SurLayout L{};
+    L.HS = slot_tier(d->H);
+    L.nw = (d->B + kTile - 1) / kTile;
+    constexpr int kPad = kFwdWaves > kBwdWaves ? kFwdWaves : kBwdWaves;
+    L.nw_pad = (L.nw + kPad - 1) / kPad * kPad;
+    const int nkb = sur_nkb(L.nw);
+    L.groups = nkb < kSurWgMaxGroups ? nkb : kSurWgMaxGroups;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += align_up(bytes);
+        return o;
+    };
+    const int HS = L.HS;
+    const size_t cells = (size_t)L.nw_pad * kLayers * kL;
+    for (int l = 0; l < kLayers; ++l) L.fa[l] = take(f16_fwd_bytes(HS, l));
+    if (with_backward)
+        for (int l = 0; l < kLayers; ++l) L.img[l] = take(img_bytes(HS, l));
+    L.fcp = take(sizeof(float) * kOut * HS * 4);
+    L.fcb = take(sizeof(float) * kOut);
+    L.fnp = take(sizeof(float) * kMS * 4 * kFnpStride);   // written (zeros) by the shared pack job, unused
+    L.wsc = take(sizeof(float) * 8);
+    L.rng = take(sizeof(float) * 8 * kRangeBlocks);
+    L.hseq = take(sizeof(f32x4) * cells * HS * 16);
+    if (with_backward) {
+        L.cseq = take(sizeof(f32x4) * cells * HS * 16);
+        L.xw = take(sizeof(f32x2) * (size_t)L.nw_pad * kL * kWave);
+        L.htop = take(sizeof(float) * (size_t)d->B * d->H);
+        L.dseq = take(sizeof(f32x4) * (size_t)L.nw_pad * 2 * kL * HS * 16);
+        L.dgs = take(cells * sur_kbb(HS) * 2048);
+        L.dsc = take(sizeof(float) * cells * 16);
+        const size_t pf = sur_part_floats(HS, false) > sur_part_floats(HS, true) ? sur_part_floats(HS, false)
+                                                                                 : sur_part_floats(HS, true);
+        const size_t fcf = (size_t)((d->B + kFcRows - 1) / kFcRows) * (kOut * d->H + kOut);   // readout partials
+        const size_t wgf = (size_t)L.groups * pf;
+        L.part = take(sizeof(float) * (wgf > fcf ? wgf : fcf));
+    }
+    L.total = off;
+    return L;
+}
+SurArgs sur_args(const fcr_dims *d, const SurLayout &L, char *base) {
+    SurArgs a{};
+    a.B = d->B;
+    a.H = d->H;
+    a.hseq = (f32x4 *)(base + L.hseq);
+    if (L.cseq) {
+        a.cseq = (f32x4 *)(base + L.cseq);
+        a.xw = (f32x2 *)(base + L.xw);
+        a.htop = (float *)(base + L.htop);
+        a.dseq = (f32x4 *)(base + L.dseq);
+        a.dgs = base + L.dgs;
+        a.dsc = (float *)(base + L.dsc);
+    }
+    for (int l = 0; l < kLayers; ++l) {
+        a.p.fa[l] = (const float *)(base + L.fa[l]);
+        a.p.img[l] = (const float *)(base + L.img[l]);
+    }
+    a.p.fcp = (const float *)(base + L.fcp);
+    a.p.fcb = (const float *)(base + L.fcb);
+    a.p.fnp = (const float *)(base + L.fnp);
+    a.p.wsc = (const float *)(base + L.wsc);
+    return a;
+}
+
+template <int HS>
+int sur_forward_t(const SurArgs &a, const SurLayout &L, bool store, hipStream_t s) {
+    constexpr int lds = SurGeo<HS>::LDS_FWD;
+    static bool attr_set[2] = {false, false};
+    const void *fn = store ? (const void *)sur_fwd_kernel<HS, true> : (const void *)sur_fwd_kernel<HS, false>;
+    if (!attr_set[store]) {
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(sur_fwd): %s", hipGetErrorString(e));
+        attr_set[store] = true;
+    }
+    if (store) hipLaunchKernelGGL((sur_fwd_kernel<HS, true>), dim3(L.nw_pad / kFwdWaves), dim3(kFwdWaves * kWave), lds, s, a);
+    else hipLaunchKernelGGL((sur_fwd_kernel<HS, false>), dim3(L.nw_pad / kFwdWaves), dim3(kFwdWaves * kWave), lds, s, a);
+    return launch_check("sur_fwd_kernel");
+}
+
+template <int HS, bool L0>
+int sur_wgrad_t(const SurArgs &a, const SurLayout &L, int l, float *part, float *g_ih, float *g_hh, hipStream_t s) {
+    using W = SurWg<HS, L0>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        const hipError_t e = hipFuncSetAttribute((const void *)sur_wgrad_kernel<HS, L0>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, W::LDS);
+        if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(sur_wgrad): %s", hipGetErrorString(e));
+        attr_set = true;
+    }
+    const int nkb = sur_nkb(L.nw);
+    hipLaunchKernelGGL((sur_wgrad_kernel<HS, L0>), dim3(L.groups), dim3(kSurWgThreads), W::LDS, s, a, l, nkb, part);
+    int rc = launch_check("sur_wgrad_kernel");
+    if (rc) return rc;
+    if (L.groups > 1) {   // the partials summed into the first (coalesced, fixed order), then decoded from it
+        hipLaunchKernelGGL(sur_part_sum_kernel, dim3((W::PART / 4 + 255) / 256), dim3(256), 0, s, part, L.groups, W::PART);
+        if ((rc = launch_check("sur_part_sum_kernel"))) return rc;
+    }
+    const int nin = L0 ? kIn : a.H;
+    const int n = 4 * a.H * (nin + a.H);
+    hipLaunchKernelGGL((sur_wgrad_finish_kernel<HS, L0>), dim3((n + 255) / 256), dim3(256), 0, s, (const float *)part, 1,
+                       a.H, a.p.wsc, g_ih, g_hh);
+    return launch_check("sur_wgrad_finish_kernel");
+}
+
+template <int HS>
+int sur_backward_t(const SurArgs &a, const SurLayout &L, float *const *g_w_ih, float *const *g_w_hh, float *part,
+                   hipStream_t s) {
+    constexpr int lds = SurGeo<HS>::LDS_BWD;
+    static bool attr_set = false;
+    if (!attr_set) {
+        const hipError_t e = hipFuncSetAttribute((const void *)sur_bwd_kernel<HS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 lds);
+        if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(sur_bwd): %s", hipGetErrorString(e));
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((sur_bwd_kernel<HS>), dim3(L.nw_pad / kBwdWaves), dim3(kBwdWaves * kWave), lds, s, a);
+    int rc = launch_check("sur_bwd_kernel");
+    if (rc) return rc;
+    if ((rc = sur_wgrad_t<HS, false>(a, L, 2, part, g_w_ih[2], g_w_hh[2], s))) return rc;
+    if ((rc = sur_wgrad_t<HS, false>(a, L, 1, part, g_w_ih[1], g_w_hh[1], s))) return rc;
+    return sur_wgrad_t<HS, true>(a, L, 0, part, g_w_ih[0], g_w_hh[0], s);
+}
+
+int sur_forward(const fcr_dims *d, const fcr_weights *w, const float *x, float *y, int with_backward, char *base,
+                hipStream_t s) {
+    const SurLayout L = make_sur(d, with_backward);
+    int rc;
+    // range guard of the window columns from the batch itself (u0 = x: its first B values are window values, so the
+    // column-4 bound stays a bound)
+    if ((rc = launch_range(d, x, x, nullptr, w->fc_w, w->fc_b, (float *)(base + L.rng), (float *)(base + L.wsc), s)))
+        return rc;
+    PackArgs pa{};
+    pa.H = d->H;
+    pa.HS = L.HS;
+    pa.CH = 0;
+    for (int l = 0; l < kLayers; ++l) {
+        pa.wih[l] = w->w_ih[l];
+        pa.whh[l] = w->w_hh[l];
+    }
+    pa.fcw = w->fc_w;
+    pa.fcb = w->fc_b;
+    pa.fcp = (float *)(base + L.fcp);
+    pa.fcbo = (float *)(base + L.fcb);
+    pa.fnp = (float *)(base + L.fnp);
+    pa.wsc = (const float *)(base + L.wsc);
+    PackAllArgs pk{};
+    pk.a = pa;
+    for (int l = 0; l < kLayers; ++l) {
+        const int nf = L.HS * (l == 0 ? (L.HS + 2 + 7) / 8 : (2 * L.HS + 7) / 8) * kWave * 8;
+        pk.job[pk.njobs++] = PackJob{kPackFwd16, l, (nf + 255) / 256, (_Float16 *)(base + L.fa[l])};
+        if (with_backward)
+            pk.job[pk.njobs++] = PackJob{kPackImg, l, (img_pack_threads(L.HS, l) + 255) / 256, (_Float16 *)(base + L.img[l])};
+    }
+    pk.job[pk.njobs++] = PackJob{kPackMisc, 0, 2, nullptr};
+    int blocks = 0;
+    for (int j = 0; j < pk.njobs; ++j) blocks += pk.job[j].blocks;
+    hipLaunchKernelGGL(pack_all_kernel, dim3(blocks), dim3(256), 0, s, pk);
+    if ((rc = launch_check("pack_all_kernel"))) return rc;
+    SurArgs a = sur_args(d, L, base);
+    a.x = x;
+    a.y = y;
+    switch (L.HS) {
+        case 4: return sur_forward_t<4>(a, L, with_backward != 0, s);
+        case 8: return sur_forward_t<8>(a, L, with_backward != 0, s);
+        default: return sur_forward_t<13>(a, L, with_backward != 0, s);
+    }
+}
+
+int sur_backward(const fcr_dims *d, const float *dy, float *const *g_w_ih, float *const *g_w_hh, float *g_fc_w,
+                 float *g_fc_b, float *g_x, char *base, hipStream_t s) {
+    const SurLayout L = make_sur(d, 1);
+    SurArgs a = sur_args(d, L, base);
+    a.dy = dy;
+    a.g_x = g_x;
+    float *part = (float *)(base + L.part);
+    int rc;
+    switch (L.HS) {
+        case 4: rc = sur_backward_t<4>(a, L, g_w_ih, g_w_hh, part, s); break;
+        case 8: rc = sur_backward_t<8>(a, L, g_w_ih, g_w_hh, part, s); break;
+        default: rc = sur_backward_t<13>(a, L, g_w_ih, g_w_hh, part, s);
+    }
+    if (rc) return rc;
+    // readout: d fc.W = dy^T h_9, d fc.b = sum dy (per-tile partials in the weight-gradient scratch, fixed-order sum)
+    const int nfb = (d->B + kFcRows - 1) / kFcRows;
+    hipLaunchKernelGGL(sur_fc_partial_kernel, dim3(nfb), dim3(256), 0, s, dy, (const float *)a.htop, d->B, d->H, part);
+    if ((rc = launch_check("sur_fc_partial_kernel"))) return rc;
+    hipLaunchKernelGGL(sur_fc_final_kernel, dim3(kOut * d->H + kOut), dim3(256), 0, s, (const float *)part, nfb, d->H, g_fc_w,
+                       g_fc_b);
+    return launch_check("sur_fc_final_kernel");
+}
+
 }  // namespace
 }  // namespace fcr
 
@@ -1249,7 +1458,7 @@ int fcr_lstm_workspace_size(const fcr_dims *dims, int with_backward, size_t *byt
     int rc = check_lstm_dims(dims);
     if (rc) return rc;
     if (!bytes) return fail(FCR_EINVAL, "bytes is NULL");
-    *bytes = make_lstm(dims, with_backward).total;
+    *bytes = is_wide(dims) ? make_lstm(dims, with_backward).total : make_sur(dims, with_backward).total;
     return FCR_OK;
 }
 
@@ -1260,6 +1469,11 @@ int fcr_lstm_forward(const fcr_dims *d, const fcr_weights *w, const float *x, fl
     if (!x || !y || !ws) return fail(FCR_EINVAL, "fcr_lstm_forward: a required pointer is NULL");
     if (!lstm_weights_ok(w)) return fail(FCR_EINVAL, "fcr_lstm_forward: an LSTM/fc weight pointer is NULL");
     if (((uintptr_t)ws) & 255) return fail(FCR_EINVAL, "fcr_lstm_forward: ws must be 256-byte aligned");
+    if (!is_wide(d)) {   // H <= 52: the fused kernels (fcr_sur.h)
+        const size_t need = make_sur(d, with_backward).total;
+        if (ws_bytes < need) return fail(FCR_EWORKSPACE, "fcr_lstm_forward: ws has %zu bytes, needs %zu", ws_bytes, need);
+        return sur_forward(d, w, x, y, with_backward, (char *)ws, (hipStream_t)stream);
+    }
     const LstmLayout L = make_lstm(d, with_backward);
     if (ws_bytes < L.total) return fail(FCR_EWORKSPACE, "fcr_lstm_forward: ws has %zu bytes, needs %zu", ws_bytes, L.total);
     hipStream_t s = (hipStream_t)stream;
@@ -1289,6 +1503,11 @@ int fcr_lstm_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, 
         if (!g_w_ih[l] || !g_w_hh[l]) return fail(FCR_EINVAL, "fcr_lstm_backward: gradient of layer %d is NULL", l);
     if (!lstm_weights_ok(w)) return fail(FCR_EINVAL, "fcr_lstm_backward: an LSTM/fc weight pointer is NULL");
     if (((uintptr_t)ws) & 255) return fail(FCR_EINVAL, "fcr_lstm_backward: ws must be 256-byte aligned");
+    if (!is_wide(d)) {
+        const size_t need = make_sur(d, 1).total;
+        if (ws_bytes < need) return fail(FCR_EWORKSPACE, "fcr_lstm_backward: ws has %zu bytes, needs %zu", ws_bytes, need);
+        return sur_backward(d, dy, g_w_ih, g_w_hh, g_fc_w, g_fc_b, g_x, (char *)ws, (hipStream_t)stream);
+    }
     const LstmLayout L = make_lstm(d, 1);
     if (ws_bytes < L.total) return fail(FCR_EWORKSPACE, "fcr_lstm_backward: ws has %zu bytes, needs %zu", ws_bytes, L.total);
     hipStream_t s = (hipStream_t)stream;

@@ -37,6 +37,14 @@ struct NextIn {
     uint32_t x, h, c, d, o;
 };
 
+// Where a cell's scaled dgates go when the caller wants them (the surrogate's weight gradients, fcr_sur.h):
+// every dgate block as it is formed — [block kbb][hi | lo][64 lanes][8 halves] from byte `off` — and the
+// trajectory's unscaling factor (`down`, a power of two) at `soff` (lane group 0). Unused (DG = false) by the rollout.
+struct DgOut {
+    __amdgpu_buffer_rsrc_t r, rs;
+    uint32_t off, soff;
+};
+
 template <int HS, int k = 0>
 __device__ __forceinline__ void ld_quads(f32x4 (&dst)[Geo<HS>::HQ], __amdgpu_buffer_rsrc_t r, uint32_t off, int lane) {
     if constexpr (k < Geo<HS>::HQ) {
@@ -101,10 +109,11 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 }
 
 template <int HS, bool L0, bool DIN, bool FIRST, bool NX_L0, bool NX_HC, bool NX_DIN, bool LP, bool OWN = true,
-          bool NX_OWN = true>
+          bool NX_OWN = true, bool DG = false>
 __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, const float (&ext)[HS],
                                          float (&dh)[HS], float (&dc)[HS], float (&dxo)[HS], float &dxq,
-                                         float &dx4, CellIn<HS> &ci, const NextIn &nx, Stamps &sp) {
+                                         float &dx4, CellIn<HS> &ci, const NextIn &nx, Stamps &sp,
+                                         const DgOut *dgo = nullptr) {
     const unsigned long long t0 = stamp_now();
 #if FCR_PRIO == 1
     // the two waves of a SIMD take turns at the higher issue priority, cell by cell, so neither runs
@@ -122,6 +131,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     constexpr int KHI = FIRST ? (L0 ? G::XBLK + 1 : G::KX1) : KB;
 
     float up, down, sg0, sgg;   // the trajectory's power-of-two scale, set once the incoming dh is in
+    float dgd = 0.0f;           // DG: down, or 0 when the trajectory has no gradient here (its dgates are zero)
 
     // packed tail block (fcr_f16.h, fcr_img.h): its hi-image row read is the packed fragment, and the
     // transposed product's last output tile reads W_lo of its two real rows from the hi image's padding rows
@@ -269,9 +279,21 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
         down = __builtin_amdgcn_ldexpf(1.0f, e - 13);
         sg0 = up * kInvNegLog2e;   // dgate scale of the i, f, o rows
         sgg = sg0 * -0.5f;         // and of the g rows
+        if (DG) dgd = m > 0.0f ? down : 0.0f;
     }
     load_xhd<HS, NX_L0, NX_HC, NX_DIN>(ci, nx, lane);   // x, h, din of this cell are consumed
+    // DG: the block leaves as it is formed (two 16-B stores per lane), and the trajectory's `down`
+    auto dg_store = [&](int kbb, f16x8 h, f16x8 l) {
+        if constexpr (DG) {
+            buf_st4(dgo->r, lane * 16, dgo->off + kbb * 2048, __builtin_bit_cast(f32x4, h));
+            buf_st4(dgo->r, lane * 16, dgo->off + kbb * 2048 + 1024, __builtin_bit_cast(f32x4, l));
+        }
+    };
+    if constexpr (DG) {
+        if (lane < 16) buf_st1(dgo->rs, lane * 4, dgo->soff, dgd);
+    }
     dgate_block(0, fa[0], gh[0], gl[0]);
+    dg_store(0, gh[0], gl[0]);
     const unsigned long long t1 = stamp_now();
 #pragma unroll
     for (int kbb = 0; kbb < KBB; ++kbb) {
@@ -329,7 +351,10 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
             }
 #endif
         }
-        if (kbb + 1 < KBB) dgate_block(kbb + 1, fa[(kbb + 1) % 3], gh[nu], gl[nu]);
+        if (kbb + 1 < KBB) {
+            dgate_block(kbb + 1, fa[(kbb + 1) % 3], gh[nu], gl[nu]);
+            dg_store(kbb + 1, gh[nu], gl[nu]);
+        }
         // every slot's own h consumed: the next cell's record comes in (an L2 hit: this cell read it as h_{t-1})
         if (NX_OWN && kbb + 2 == KBB) ld_quads<HS>(ci.o, nx.rh, nx.o, lane);
     }

@@ -223,6 +223,14 @@ __device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, uint32_t voff,
                                           (int)voff, (int)soff, 0);
 }
 
+__device__ __forceinline__ void buf_st4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, f32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), r,
+                                           (int)voff, (int)soff, 0);
+}
+__device__ __forceinline__ void buf_st1(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, v), r, (int)voff, (int)soff, 0);
+}
+
 // Copy a fragment block (global, L2-resident) into LDS; the caller brackets it with barriers.
 __device__ __forceinline__ void lds_copy(float *lw, const float *__restrict__ src, int nfloats) {
     const float4 *s4 = reinterpret_cast<const float4 *>(src);

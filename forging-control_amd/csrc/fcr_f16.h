@@ -450,7 +450,9 @@ __device__ __forceinline__ void lstm_point_grad_h(f32x4 a, float c_prev, float h
     const float i = sigm_pre(a[0]);
     const float f = sigm_pre(a[1]);
     const float g = tanh_pre(a[2]);
-    const float d_o = 1.0f + __builtin_amdgcn_exp2f(a[3]);
+    // a_o at most 126 (one v_med3): a saturated output gate (the forward's e_o = inf, o = h = 0) keeps d_o finite,
+    // so tc = h d_o is 0 there, not 0 * inf (tests/test_surrogate.py, range-guarded columns)
+    const float d_o = 1.0f + __builtin_amdgcn_exp2f(__builtin_amdgcn_fmed3f(a[3], -1e30f, 126.0f));
     const float o = __builtin_amdgcn_rcpf(d_o);
     const float gi = g * i;
     const float cf = FIRST ? 0.0f : f * c_prev;

@@ -4,10 +4,12 @@ The reference trains the plant surrogate ``LSTMModel(5, 50, 4, 3)`` with ``nn.MS
 (Model_NN/Main.py:218-242) through ``NeuralNetwork.train_model`` (Model_NN/Functions.py:520-569), i.e.
 ``output = model(X, device); loss = loss_function(output, y.squeeze()); loss.backward();
 optimizer.step()`` per batch. Here ``LSTMModel.forward`` on a ROCm device runs :class:`LSTMFunction`:
-``fcr_lstm_forward`` (per-cell rocBLAS gate GEMMs + HIP cell kernels, every cell's state kept) and, on
-``backward``, ``fcr_lstm_backward`` (dgates per cell, then ONE weight-gradient GEMM per weight matrix
-over all 10·B (step, sample) rows). Every LSTM weight, the readout and — when it requires grad — the
-input window receive gradients, so the reference's loop and optimizer run unchanged.
+``fcr_lstm_forward`` and, on ``backward``, ``fcr_lstm_backward``. For H <= 52 (the reference's H = 50)
+they are the rollout's fused split-f16 cell kernels over one window (csrc/fcr_sur.h: one forward launch,
+one backward launch that also keeps every cell's dgates, and one hand-written weight-gradient product per
+layer over all 10·B (step, sample) rows); wider models run the per-cell path (csrc/fcr_wide.h). Every
+LSTM weight, the readout and — when it requires grad — the input window receive gradients, so the
+reference's loop and optimizer run unchanged.
 """
 from __future__ import annotations
 

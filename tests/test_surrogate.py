@@ -167,3 +167,100 @@ def test_gpu_forward_matches_rollout_kernel_one_step():
         y = m(xt, "cuda:0")
     y2 = fca.simulate_step(m, xt)
     assert relerr(y.cpu().numpy(), y2.cpu().numpy()) < 2 * TOL
+
+
+def _oracle_grads_dy(p, x, dy, dev):
+    """fp64 autograd of y = LSTMModel(x) against an arbitrary dL/dy (the oracle model on `dev`)."""
+    m = S.build(p).to(dev)
+    xt = torch.as_tensor(x, dtype=torch.float64, device=dev).clone().requires_grad_(True)
+    y = m(xt)
+    y.backward(torch.as_tensor(dy, dtype=torch.float64, device=dev))
+    g = {"Wih": [getattr(m.lstm, f"weight_ih_l{k}").grad.cpu().numpy() for k in range(3)],
+         "Whh": [getattr(m.lstm, f"weight_hh_l{k}").grad.cpu().numpy() for k in range(3)],
+         "fcW": m.fc.weight.grad.cpu().numpy(), "fcb": m.fc.bias.grad.cpu().numpy(), "x": xt.grad.cpu().numpy()}
+    return y.detach().cpu().numpy(), g
+
+
+def _hip_grads_dy(p, x, dy):
+    m = model_for(p)
+    xt = torch.tensor(x, dtype=torch.float32, device="cuda:0", requires_grad=True)
+    y = m(xt, "cuda:0")
+    y.backward(torch.tensor(dy, dtype=torch.float32, device="cuda:0"))
+    g = grads_of(m)
+    g["x"] = xt.grad.cpu().numpy()
+    return y.detach().cpu().numpy(), g
+
+
+def _check_all(y, g, y_ref, g_ref, tol=TOL):
+    assert relerr(y, y_ref) < tol
+    for key in ("Wih", "Whh"):
+        for k in range(3):
+            assert relerr(g[key][k], g_ref[key][k]) < tol, (key, k, relerr(g[key][k], g_ref[key][k]))
+    for key in ("fcW", "fcb", "x"):
+        assert relerr(g[key], g_ref[key]) < tol, (key, relerr(g[key], g_ref[key]))
+
+
+@pytest.mark.gpu
+def test_gpu_full_batch_step_matches_oracle():
+    """B = 65 536 (the benchmark's batch), H = 50: every weight gradient summed over 655 360 (window, step) rows, the
+    readout's over 65 536 windows, and dL/dx, against fp64 autograd (on the GPU, checker only)."""
+    p = ref_params()
+    x, target = batch(65536, seed=7)
+    B = x.shape[0]
+    dy = 2.0 * (0.0 + 1.0) / (B * 4) * np.random.default_rng(8).uniform(-1, 1, (B, 4))   # an MSE-sized dL/dy
+    y_ref, g_ref = _oracle_grads_dy(p, x, dy, "cuda:0")
+    y, g = _hip_grads_dy(p, x, dy)
+    _check_all(y, g, y_ref, g_ref)
+
+
+@pytest.mark.gpu
+def test_gpu_rows_without_or_with_tiny_gradient():
+    """Per-row dgate scales: windows with dL/dy = 0, ~1e-30 and ~1e4 in one batch (the weight-gradient kernel
+    rescales every row to its workgroup's largest; zero rows must not set that scale)."""
+    p = ref_params()
+    x, _ = batch(4099, seed=11)
+    rng = np.random.default_rng(12)
+    dy = rng.uniform(-1, 1, (4099, 4))
+    dy[::3] = 0.0
+    dy[1::7] *= 1e-30
+    dy[5::11] *= 1e4
+    y_ref, g_ref = _oracle_grads_dy(p, x, dy, "cuda:0")
+    y, g = _hip_grads_dy(p, x, dy)
+    _check_all(y, g, y_ref, g_ref)
+    # the tiny rows alone: their gradients are not flushed (every row's own power-of-two scale)
+    dt = np.zeros_like(dy)
+    dt[1::7] = dy[1::7]
+    _, gt_ref = _oracle_grads_dy(p, x, dt, "cuda:0")
+    _, gt = _hip_grads_dy(p, x, dt)
+    for key in ("Wih", "Whh"):
+        for k in range(3):
+            assert relerr(gt[key][k], gt_ref[key][k]) < TOL
+
+
+@pytest.mark.gpu
+def test_gpu_range_guarded_window_columns():
+    """Unscaled window columns (|x| up to 3e4 and 1e5, beyond f16's range: hi = f16(x) would be inf): the range guard
+    (fcr_pack.h) runs them on x 2^-s_c against W_ih0 2^s_c and scales their weight gradients back. Against O(1) weights
+    the layer-0 gates cancel terms of ~1e4, where any fp32 implementation is off fp64 by ~|W||x| 2^-24 (stock torch
+    fp32: 4e-4 on W_ih0's gradient here) — so, as the rollout's test of the guard (test_gpu_parity.py), every tensor is
+    held to max(1e-5, 4 x torch fp32's own distance to fp64)."""
+    p = ref_params()
+    x, target = batch(300, seed=13)
+    x[..., 0] *= 3e4
+    x[..., 4] *= 1e5
+    dy = np.random.default_rng(14).uniform(-1, 1, (300, 4)) * 1e-3
+    y_ref, g_ref = _oracle_grads_dy(p, x, dy, "cuda:0")
+    m32 = S.build(p, torch.float32)
+    xt = torch.as_tensor(x, dtype=torch.float32).clone().requires_grad_(True)
+    y32 = m32(xt)
+    y32.backward(torch.as_tensor(dy, dtype=torch.float32))
+    g32 = {"Wih": [getattr(m32.lstm, f"weight_ih_l{k}").grad.numpy() for k in range(3)],
+           "Whh": [getattr(m32.lstm, f"weight_hh_l{k}").grad.numpy() for k in range(3)],
+           "fcW": m32.fc.weight.grad.numpy(), "fcb": m32.fc.bias.grad.numpy(), "x": xt.grad.numpy()}
+    y, g = _hip_grads_dy(p, x, dy)
+    assert np.isfinite(y).all() and relerr(y, y_ref) <= max(TOL, 4 * relerr(y32.detach().numpy(), y_ref))
+    pairs = [(g[k][i], g32[k][i], g_ref[k][i]) for k in ("Wih", "Whh") for i in range(3)]
+    pairs += [(g[k], g32[k], g_ref[k]) for k in ("fcW", "fcb", "x")]
+    for got, t32, ref in pairs:
+        assert np.isfinite(got).all()
+        assert relerr(got, ref) <= max(TOL, 4 * relerr(t32, ref)), (relerr(got, ref), relerr(t32, ref))
