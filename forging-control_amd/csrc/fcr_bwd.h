@@ -88,6 +88,9 @@ constexpr float kInvNegLog2e = 1.0f / kNegLog2e;
 // OWN: the cell's own h_t record is in ci.o (every cell but the first of a window's layer-2 phase, whose h_9
 // only fed the readout): tanh(c_t) comes from it (lstm_point_grad_h) instead of being re-evaluated.
 // NX_OWN: the next cell's is fetched.
+#ifndef FCR_OWN_REG
+#define FCR_OWN_REG 1
+#endif
 #ifndef FCR_BWD_LAUNDER
 #define FCR_BWD_LAUNDER 1
 #endif
@@ -281,6 +284,14 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
         sgg = sg0 * -0.5f;         // and of the g rows
         if (DG) dgd = m > 0.0f ? down : 0.0f;
     }
+    // OWN_REG: the next cell (t - 1, same phase) owns h_{t-1}, whose record this cell has in ci.h: kept in registers
+    // for it instead of re-read from the slab (an L2 miss by then)
+    constexpr bool OWN_REG = FCR_OWN_REG && NX_OWN && !FIRST;
+    f32x4 hkeep[Geo<HS>::HQ];
+    if constexpr (OWN_REG) {
+#pragma unroll
+        for (int k = 0; k < Geo<HS>::HQ; ++k) hkeep[k] = ci.h[k];
+    }
     load_xhd<HS, NX_L0, NX_HC, NX_DIN>(ci, nx, lane);   // x, h, din of this cell are consumed
     // DG: the block leaves as it is formed (two 16-B stores per lane), and the trajectory's `down`
     auto dg_store = [&](int kbb, f16x8 h, f16x8 l) {
@@ -356,7 +367,14 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
             dg_store(kbb + 1, gh[nu], gl[nu]);
         }
         // every slot's own h consumed: the next cell's record comes in (an L2 hit: this cell read it as h_{t-1})
-        if (NX_OWN && kbb + 2 == KBB) ld_quads<HS>(ci.o, nx.rh, nx.o, lane);
+        if (NX_OWN && kbb + 2 == KBB) {
+            if constexpr (OWN_REG) {
+#pragma unroll
+                for (int k = 0; k < Geo<HS>::HQ; ++k) ci.o[k] = hkeep[k];
+            } else {
+                ld_quads<HS>(ci.o, nx.rh, nx.o, lane);
+            }
+        }
     }
     sched_fence();
     const unsigned long long t2 = stamp_now();
