@@ -329,6 +329,14 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
             if (two) {
                 h1 = lds_tr_f16(tb + ct + TILE);
                 if (!LP && !hi_only) l1 = lds_tr_f16(tbl + ct + TILE);
+            } else if (!LP) {
+                // half block: the upper k-halves are read again instead of copied (a VGPR copy into an MFMA
+                // operand costs two v_mov and an s_nop per tile): W_hi once more for the shared hi·hi | hi·lo
+                // MFMA below, and W_lo once more as the (finite) partner of the padding slot's zero dgates
+                uint32_t tbd = tb, tbld = tbl;
+                asm volatile("" : "+v"(tbd), "+v"(tbld));
+                h1 = lds_tr_f16(tbd + ct);
+                if (!hi_only) l1 = lds_tr_f16(tbld + ct);
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -349,10 +357,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
                 // hi·hi and hi·lo products share ONE MFMA over k = [W_hi d_hi | W_hi d_lo], then lo·hi
                 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
                 const u32x4 h = __builtin_bit_cast(u32x4, gh[cu]), l = __builtin_bit_cast(u32x4, gl[cu]);
-                f16x8 a2;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) a2[k] = a2[4 + k] = h0[k];
-                acc[tau] = mfma16(a2, __builtin_bit_cast(f16x8, u32x4{h[0], h[1], l[0], l[1]}), acc[tau]);
+                acc[tau] = mfma16(ah, __builtin_bit_cast(f16x8, u32x4{h[0], h[1], l[0], l[1]}), acc[tau]);   // ah = [W_hi | W_hi]
                 if (!hi_only) acc[tau] = mfma16(al, gh[cu], acc[tau]);
             } else if (hi_only) {
                 acc[tau] = mfma16(ah, gl[cu], acc[tau]);
