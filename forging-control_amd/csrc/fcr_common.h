@@ -297,6 +297,44 @@ __device__ __forceinline__ void load_quads(float (&v)[HS], const f32x4 *src, int
     for (int e = 0; e < TS; ++e) v[4 * FQ + e] = t[e];
 }
 
+// store_quads / load_quads through a wave-uniform buffer descriptor (the layout above): the lane part is
+// quad_voff, the cell's offset an SGPR soffset — no per-access 64-bit address arithmetic
+template <int HS, int k = 0>
+__device__ __forceinline__ void buf_store_quads(__amdgpu_buffer_rsrc_t r, uint32_t off, const float (&v)[HS], int lane) {
+#if FCR_ABLATE == 3
+    if constexpr (k == 0)
+        for (int e = 0; e < HS; ++e) asm volatile("" ::"v"(v[e]));
+    return;
+#endif
+    if constexpr (k < Geo<HS>::HQ) {
+        constexpr int n = quad_n<HS, k>();
+        const uint32_t vo = quad_voff<HS, k>(lane), so = off + quad_soff<HS, k>();
+        if constexpr (n == 4) {
+            buf_st4(r, vo, so, f32x4{v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]});
+        } else if constexpr (n == 3) {
+            typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+            __builtin_amdgcn_raw_buffer_store_b96(u32x3{__builtin_bit_cast(unsigned, v[4 * k]), __builtin_bit_cast(unsigned, v[4 * k + 1]),
+                                                        __builtin_bit_cast(unsigned, v[4 * k + 2])},
+                                                  r, (int)vo, (int)so, 0);
+        } else if constexpr (n == 2) {
+            buf_st2(r, vo, so, f32x2{v[4 * k], v[4 * k + 1]});
+        } else {
+            buf_st1(r, vo, so, v[4 * k]);
+        }
+        buf_store_quads<HS, k + 1>(r, off, v, lane);
+    }
+}
+template <int HS, int k = 0>
+__device__ __forceinline__ void buf_load_quads(float (&v)[HS], __amdgpu_buffer_rsrc_t r, uint32_t off, int lane) {
+    if constexpr (k < Geo<HS>::HQ) {
+        constexpr int n = quad_n<HS, k>();
+        const f32x4 q = buf_ldq<n>(r, quad_voff<HS, k>(lane), off + quad_soff<HS, k>());
+#pragma unroll
+        for (int e = 0; e < n; ++e) v[4 * k + e] = q[e];
+        buf_load_quads<HS, k + 1>(v, r, off, lane);
+    }
+}
+
 // Controller pre-activation (FNNModel.forward, Functions.py:261-289): lane group q evaluates hidden
 // units 4m+q; returns the pre-Hardtanh output (identical arithmetic in forward and backward).
 __device__ __forceinline__ float fnn_pre(const float *__restrict__ fnp, int q, float a, float b,

@@ -224,9 +224,10 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
     // next phase's input; with STORE also layer 2) and, with STORE, c; plus the window rows [wave][j][t][64]
     const size_t qcell = (size_t)Geo<HS>::QC;    // one cell of a sequence slab, in 16-B units
     const size_t wseq = (size_t)wave * N * kLayers * kL * qcell;
-    f32x4 *hs_wave = a.hseq + wseq;
-    f32x4 *cs_wave = a.cseq + wseq;
-    f32x2 *xw_wave = a.xw + (size_t)wave * N * kL * kWave;
+    // the wave's slab regions as buffer descriptors: every record access is (lane offset, SGPR cell offset)
+    const __amdgpu_buffer_rsrc_t rh = wave_rsrc(a.hseq + wseq, (size_t)N * kLayers * kL * qcell * 16);
+    const __amdgpu_buffer_rsrc_t rc = wave_rsrc(a.cseq + wseq, (size_t)N * kLayers * kL * qcell * 16);
+    const __amdgpu_buffer_rsrc_t rx = wave_rsrc(a.xw + (size_t)wave * N * kL * kWave, (size_t)N * kL * kWave * 8);
 
     unsigned long long st_fill = 0, st_l0 = 0, st_l12 = 0, st_head = 0, st_drain = 0, st_skew1 = 0, st_dma = 0;
     Pace turn;
@@ -263,10 +264,8 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
         }
         if (valid && q == 0) a.prediction[(size_t)b * N + j] = pred;   // Functions.py:1455,1466
 
-        f32x4 *hsj = hs_wave + (size_t)j * kLayers * kL * qcell;   // h of window j, [layer][t]
-        f32x4 *csj = cs_wave + (size_t)j * kLayers * kL * qcell;
-#define SEQ_H(l, t) (hsj + (size_t)((l) * kL + (t)) * qcell)
-#define SEQ_C(l, t) (csj + (size_t)((l) * kL + (t)) * qcell)
+        const uint32_t oj = (uint32_t)((size_t)j * kLayers * kL * qcell * 16);   // window j's cells, [layer][t]
+#define SEQ_O(l, t) (oj + (uint32_t)(((l) * kL + (t)) * qcell * 16))
         const unsigned long long st_w1 = fstamp();
         st_head += st_w1 - st_w0;
         // ---- layer 0 over the window (Functions.py:374) ----
@@ -280,10 +279,10 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             rot_left(w1);
             fwd16_cell<HS, true, true, LP>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
             split_rec<HS>(hout, hp);
-            store_quads<HS>(SEQ_H(0, 0), hp, lane);
+            buf_store_quads<HS>(rh, SEQ_O(0, 0), hp, lane);
             if (STORE) {
-                if (FCR_ABLATE != 3) xw_wave[(size_t)j * kL * kWave + lane] = f32x2{x0, x1};
-                store_quads<HS>(SEQ_C(0, 0), c, lane);
+                if (FCR_ABLATE != 3) buf_st2(rx, lane * 8, (uint32_t)(j * kL * kWave * 8), f32x2{x0, x1});
+                buf_store_quads<HS>(rc, SEQ_O(0, 0), c, lane);
             }
         }
         for (int t = 1; t < kL; ++t) {
@@ -292,10 +291,10 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             rot_left(w1);
             fwd16_cell<HS, true, false, LP>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
             split_rec<HS>(hout, hp);
-            store_quads<HS>(SEQ_H(0, t), hp, lane);
+            buf_store_quads<HS>(rh, SEQ_O(0, t), hp, lane);
             if (STORE) {
-                if (FCR_ABLATE != 3) xw_wave[((size_t)j * kL + t) * kWave + lane] = f32x2{x0, x1};
-                if (t + 1 < kL) store_quads<HS>(SEQ_C(0, t), c, lane);   // c_9 is never a c_{t-1}
+                if (FCR_ABLATE != 3) buf_st2(rx, lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{x0, x1});
+                if (t + 1 < kL) buf_store_quads<HS>(rc, SEQ_O(0, t), c, lane);   // c_9 is never a c_{t-1}
             }
         }
         // ---- layers 1, 2: input sequence streamed back from the slab, one cell ahead ----
@@ -332,29 +331,28 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             const float *lwc = LP ? lwl[l] : lw;
             const unsigned long long st_f1 = fstamp();
             st_fill += st_f1 - st_f0;
-            load_quads<HS>(xc, SEQ_H(l - 1, 0), lane);
-            load_quads<HS>(xn, SEQ_H(l - 1, 1), lane);
+            buf_load_quads<HS>(xc, rh, SEQ_O(l - 1, 0), lane);
+            buf_load_quads<HS>(xn, rh, SEQ_O(l - 1, 1), lane);
             fwd16_cell<HS, false, true, LP>(lwc, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
             split_rec<HS>(hout, hp);
-            if (keep_h) store_quads<HS>(SEQ_H(l, 0), hp, lane);
-            if (STORE) store_quads<HS>(SEQ_C(l, 0), c, lane);
+            if (keep_h) buf_store_quads<HS>(rh, SEQ_O(l, 0), hp, lane);
+            if (STORE) buf_store_quads<HS>(rc, SEQ_O(l, 0), c, lane);
 #pragma unroll
             for (int r = 0; r < HS; ++r) xc[r] = xn[r];
 #pragma unroll 3
             for (int t = 1; t < kL; ++t) {
-                load_quads<HS>(xn, SEQ_H(l - 1, t + 1 < kL ? t + 1 : t), lane);
+                buf_load_quads<HS>(xn, rh, SEQ_O(l - 1, t + 1 < kL ? t + 1 : t), lane);
                 fwd16_cell<HS, false, false, LP>(lwc, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
                 if (!(l == 2 && t + 1 == kL)) {   // h_9 of layer 2 only feeds the readout (fp32 hout)
                     split_rec<HS>(hout, hp);
-                    if (keep_h) store_quads<HS>(SEQ_H(l, t), hp, lane);
+                    if (keep_h) buf_store_quads<HS>(rh, SEQ_O(l, t), hp, lane);
                 }
-                if (STORE && t + 1 < kL) store_quads<HS>(SEQ_C(l, t), c, lane);
+                if (STORE && t + 1 < kL) buf_store_quads<HS>(rc, SEQ_O(l, t), c, lane);
 #pragma unroll
                 for (int r = 0; r < HS; ++r) xc[r] = xn[r];
             }
         }
-#undef SEQ_H
-#undef SEQ_C
+#undef SEQ_O
         // ---- readout fc(h_9 of layer 2) (Functions.py:377) ----
         float xo[kOut];
 #pragma unroll

@@ -77,11 +77,10 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void sur_fwd_kern
     }
     float c[HS], hout[HS], hp[HS], xc[HS], xn[HS];
     constexpr size_t qcell = (size_t)Geo<HS>::QC;
-    f32x4 *hs = a.hseq + (size_t)wave * SurGeo<HS>::SEQ;
-    f32x4 *cs = a.cseq + (size_t)wave * SurGeo<HS>::SEQ;
-    f32x2 *xw = a.xw + (size_t)wave * kL * kWave;
-#define SEQ_H(l, t) (hs + (size_t)((l) * kL + (t)) * qcell)
-#define SEQ_C(l, t) (cs + (size_t)((l) * kL + (t)) * qcell)
+    const __amdgpu_buffer_rsrc_t rh = wave_rsrc(a.hseq + (size_t)wave * SurGeo<HS>::SEQ, SurGeo<HS>::SEQ * 16);
+    const __amdgpu_buffer_rsrc_t rc = wave_rsrc(a.cseq + (size_t)wave * SurGeo<HS>::SEQ, SurGeo<HS>::SEQ * 16);
+    const __amdgpu_buffer_rsrc_t rx = wave_rsrc(a.xw + (size_t)wave * kL * kWave, (size_t)kL * kWave * 8);
+#define SEQ_O(l, t) ((uint32_t)(((l) * kL + (t)) * qcell * 16))
     Pace turn;
     turn.turn = (threadIdx.x >> 8) & 1;
     turn.me = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -96,10 +95,10 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void sur_fwd_kern
         rot_left(w1);
         fwd16_cell<HS, true, true, false>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
         split_rec<HS>(hout, hp);
-        store_quads<HS>(SEQ_H(0, 0), hp, lane);
+        buf_store_quads<HS>(rh, SEQ_O(0, 0), hp, lane);
         if (STORE) {
-            xw[lane] = f32x2{x0, x1};
-            store_quads<HS>(SEQ_C(0, 0), c, lane);
+            buf_st2(rx, lane * 8, 0u, f32x2{x0, x1});
+            buf_store_quads<HS>(rc, SEQ_O(0, 0), c, lane);
         }
     }
     for (int t = 1; t < kL; ++t) {
@@ -108,10 +107,10 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void sur_fwd_kern
         rot_left(w1);
         fwd16_cell<HS, true, false, false>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
         split_rec<HS>(hout, hp);
-        store_quads<HS>(SEQ_H(0, t), hp, lane);
+        buf_store_quads<HS>(rh, SEQ_O(0, t), hp, lane);
         if (STORE) {
-            xw[(size_t)t * kWave + lane] = f32x2{x0, x1};
-            if (t + 1 < kL) store_quads<HS>(SEQ_C(0, t), c, lane);
+            buf_st2(rx, lane * 8, (uint32_t)(t * kWave * 8), f32x2{x0, x1});
+            if (t + 1 < kL) buf_store_quads<HS>(rc, SEQ_O(0, t), c, lane);
         }
     }
     // ---- layers 1, 2 ----
@@ -119,29 +118,28 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void sur_fwd_kern
     for (int l = 1; l < kLayers; ++l) {
         lds_fill<G::FA1 * 4, kFwdWaves>(lw, a.p.fa[l]);
         stagger();
-        load_quads<HS>(xc, SEQ_H(l - 1, 0), lane);
-        load_quads<HS>(xn, SEQ_H(l - 1, 1), lane);
+        buf_load_quads<HS>(xc, rh, SEQ_O(l - 1, 0), lane);
+        buf_load_quads<HS>(xn, rh, SEQ_O(l - 1, 1), lane);
         fwd16_cell<HS, false, true, false>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
         split_rec<HS>(hout, hp);
-        if (l == 1 || STORE) store_quads<HS>(SEQ_H(l, 0), hp, lane);
-        if (STORE) store_quads<HS>(SEQ_C(l, 0), c, lane);
+        if (l == 1 || STORE) buf_store_quads<HS>(rh, SEQ_O(l, 0), hp, lane);
+        if (STORE) buf_store_quads<HS>(rc, SEQ_O(l, 0), c, lane);
 #pragma unroll
         for (int r = 0; r < HS; ++r) xc[r] = xn[r];
 #pragma unroll 3
         for (int t = 1; t < kL; ++t) {
-            load_quads<HS>(xn, SEQ_H(l - 1, t + 1 < kL ? t + 1 : t), lane);
+            buf_load_quads<HS>(xn, rh, SEQ_O(l - 1, t + 1 < kL ? t + 1 : t), lane);
             fwd16_cell<HS, false, false, false>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
             if (!(l == 2 && t + 1 == kL)) {   // h_9 of layer 2 only feeds the readout (fp32 hout)
                 split_rec<HS>(hout, hp);
-                if (l == 1 || STORE) store_quads<HS>(SEQ_H(l, t), hp, lane);
+                if (l == 1 || STORE) buf_store_quads<HS>(rh, SEQ_O(l, t), hp, lane);
             }
-            if (STORE && t + 1 < kL) store_quads<HS>(SEQ_C(l, t), c, lane);
+            if (STORE && t + 1 < kL) buf_store_quads<HS>(rc, SEQ_O(l, t), c, lane);
 #pragma unroll
             for (int r = 0; r < HS; ++r) xc[r] = xn[r];
         }
     }
-#undef SEQ_H
-#undef SEQ_C
+#undef SEQ_O
     // ---- readout fc(out[:, -1, :]) (Model_NN/Functions.py:330) ----
     float xo[kOut];
 #pragma unroll
