@@ -483,7 +483,6 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
     nb.rc = wave_rsrc(a.cseq + (size_t)wave * seq_sz, seq_sz * 16);
     nb.rx = wave_rsrc(a.xw + (size_t)wave * N * kL * kWave, (size_t)N * kL * kWave * 8);
     nb.rd = wave_rsrc(a.dseq + (size_t)wave * dseq_sz, dseq_sz * 16);
-    f32x4 *dseq_w = a.dseq + (size_t)wave * dseq_sz;
     auto hoff = [&](int j, int l, int t) { return (uint32_t)(((size_t)(j * kLayers + l) * kL + t) * qcell * 16); };
     auto doff = [&](int j, int lfrom, int t) { return ((size_t)(j * 2 + (2 - lfrom)) * kL + t) * qcell; };
     auto next_of = [&](int j, int l, int t) {   // the cell processed after (j, l, t)
@@ -583,20 +582,20 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         // t = 9: h_9 of layer 2 only fed the readout (no split record), so this cell re-evaluates tanh(c_9)
         bwd_cell<HS, false, false, false, false, true, false, LP, false>(L1.fb, L1.tb, lane, dh_out, dh, dc, dxo, unused0,
                                                                     unused1, ci, next_of(j, 2, kL - 1), sp);
-        store_quads<HS>(dseq_w + doff(j, 2, kL - 1), dxo, lane);
+        buf_store_quads<HS>(nb.rd, (uint32_t)((doff(j, 2, kL - 1)) * 16), dxo, lane);
 #pragma unroll
         for (int r = 0; r < HS; ++r) dab[r] = 0.0f;
         for (int t = kL - 2; t >= 2; --t) {
             bwd_cell<HS, false, false, false, false, true, false, LP>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
                                                                 unused1, ci, next_of(j, 2, t), sp);
-            store_quads<HS>(dseq_w + doff(j, 2, t), dxo, lane);
+            buf_store_quads<HS>(nb.rd, (uint32_t)((doff(j, 2, t)) * 16), dxo, lane);
         }
         bwd_cell<HS, false, false, false, false, false, false, LP>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
                                                              unused1, ci, next_of(j, 2, 1), sp);
-        store_quads<HS>(dseq_w + doff(j, 2, 1), dxo, lane);
+        buf_store_quads<HS>(nb.rd, (uint32_t)((doff(j, 2, 1)) * 16), dxo, lane);
         bwd_cell<HS, false, false, true, false, true, true, LP>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
                                                           unused1, ci, next_of(j, 2, 0), sp);
-        store_quads<HS>(dseq_w + doff(j, 2, 0), dxo, lane);
+        buf_store_quads<HS>(nb.rd, (uint32_t)((doff(j, 2, 0)) * 16), dxo, lane);
         // ---- layer 1 ----
         const unsigned long long tw3 = stamp_now();
         if (!LP) {
@@ -609,14 +608,14 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         for (int t = kL - 1; t >= 2; --t) {
             bwd_cell<HS, false, true, false, false, true, true, LP>(L1b.fb, L1b.tb, lane, dab, dh, dc, dxo, unused0,
                                                               unused1, ci, next_of(j, 1, t), sp);
-            store_quads<HS>(dseq_w + doff(j, 1, t), dxo, lane);
+            buf_store_quads<HS>(nb.rd, (uint32_t)((doff(j, 1, t)) * 16), dxo, lane);
         }
         bwd_cell<HS, false, true, false, false, false, true, LP>(L1b.fb, L1b.tb, lane, dab, dh, dc, dxo, unused0,
                                                            unused1, ci, next_of(j, 1, 1), sp);
-        store_quads<HS>(dseq_w + doff(j, 1, 1), dxo, lane);
+        buf_store_quads<HS>(nb.rd, (uint32_t)((doff(j, 1, 1)) * 16), dxo, lane);
         bwd_cell<HS, false, true, true, true, true, true, LP>(L1b.fb, L1b.tb, lane, dab, dh, dc, dxo, unused0,
                                                         unused1, ci, next_of(j, 1, 0), sp);
-        store_quads<HS>(dseq_w + doff(j, 1, 0), dxo, lane);
+        buf_store_quads<HS>(nb.rd, (uint32_t)((doff(j, 1, 0)) * 16), dxo, lane);
         // ---- layer 0: dx -> window-row gradients ----
         if (!LP) {
             lds_fill<I0::BYTES, kBwdWaves>(lw, a.p.img[0]);

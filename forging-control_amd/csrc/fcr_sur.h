@@ -197,7 +197,6 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void sur_bwd_kern
     nb.rc = wave_rsrc(a.cseq + (size_t)wave * SG::SEQ, SG::SEQ * 16);
     nb.rx = wave_rsrc(a.xw + (size_t)wave * kL * kWave, (size_t)kL * kWave * 8);
     nb.rd = wave_rsrc(a.dseq + (size_t)wave * SG::DSEQ, SG::DSEQ * 16);
-    f32x4 *dseq_w = a.dseq + (size_t)wave * SG::DSEQ;
     auto hoff = [&](int l, int t) { return (uint32_t)(((size_t)l * kL + t) * qcell * 16); };
     auto doff = [&](int lfrom, int t) { return ((size_t)(2 - lfrom) * kL + t) * qcell; };
     auto next_of = [&](int l, int t) {   // the cell processed after (l, t)
@@ -241,23 +240,23 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void sur_bwd_kern
         const DgOut d = dg_at(2, kL - 1);
         bwd_cell<HS, false, false, false, false, true, false, false, false, true, true>(
             L1.fb, L1.tb, lane, dh_out, dh, dc, dxo, unused0, unused1, ci, next_of(2, kL - 1), sp, &d);
-        store_quads<HS>(dseq_w + doff(2, kL - 1), dxo, lane);
+        buf_store_quads<HS>(nb.rd, (uint32_t)((doff(2, kL - 1)) * 16), dxo, lane);
     }
     for (int t = kL - 2; t >= 2; --t) {
         const DgOut d = dg_at(2, t);
         bwd_cell<HS, false, false, false, false, true, false, false, true, true, true>(
             L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0, unused1, ci, next_of(2, t), sp, &d);
-        store_quads<HS>(dseq_w + doff(2, t), dxo, lane);
+        buf_store_quads<HS>(nb.rd, (uint32_t)((doff(2, t)) * 16), dxo, lane);
     }
     {
         const DgOut d1 = dg_at(2, 1);
         bwd_cell<HS, false, false, false, false, false, false, false, true, true, true>(
             L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0, unused1, ci, next_of(2, 1), sp, &d1);
-        store_quads<HS>(dseq_w + doff(2, 1), dxo, lane);
+        buf_store_quads<HS>(nb.rd, (uint32_t)((doff(2, 1)) * 16), dxo, lane);
         const DgOut d0 = dg_at(2, 0);
         bwd_cell<HS, false, false, true, false, true, true, false, true, true, true>(
             L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0, unused1, ci, next_of(2, 0), sp, &d0);
-        store_quads<HS>(dseq_w + doff(2, 0), dxo, lane);
+        buf_store_quads<HS>(nb.rd, (uint32_t)((doff(2, 0)) * 16), dxo, lane);
     }
     // ---- layer 1 ----
     lds_fill<I1::BYTES, kBwdWaves>(lw, a.p.img[1]);
@@ -268,17 +267,17 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void sur_bwd_kern
         const DgOut d = dg_at(1, t);
         bwd_cell<HS, false, true, false, false, true, true, false, true, true, true>(
             L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0, unused1, ci, next_of(1, t), sp, &d);
-        store_quads<HS>(dseq_w + doff(1, t), dxo, lane);
+        buf_store_quads<HS>(nb.rd, (uint32_t)((doff(1, t)) * 16), dxo, lane);
     }
     {
         const DgOut d1 = dg_at(1, 1);
         bwd_cell<HS, false, true, false, false, false, true, false, true, true, true>(
             L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0, unused1, ci, next_of(1, 1), sp, &d1);
-        store_quads<HS>(dseq_w + doff(1, 1), dxo, lane);
+        buf_store_quads<HS>(nb.rd, (uint32_t)((doff(1, 1)) * 16), dxo, lane);
         const DgOut d0 = dg_at(1, 0);
         bwd_cell<HS, false, true, true, true, true, true, false, true, true, true>(
             L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0, unused1, ci, next_of(1, 0), sp, &d0);
-        store_quads<HS>(dseq_w + doff(1, 0), dxo, lane);
+        buf_store_quads<HS>(nb.rd, (uint32_t)((doff(1, 0)) * 16), dxo, lane);
     }
     // ---- layer 0: the window-row gradients are dL/dx ----
     lds_fill<I0::BYTES, kBwdWaves>(lw, a.p.img[0]);
