@@ -244,10 +244,18 @@ def grad_check(sim, ctrl, X, S, N, dev, precision, B_check=None):
                     "above_1e-5": int((e[~reg] > 1e-5).sum())}
             a, r = a[reg], r[reg]
         err[k] = float((a - r).abs().max() / den)
+    # the reference's own arithmetic (stock torch fp32, same oracle, same device) against the same fp64: the
+    # fp32 noise floor of this batch, beside which the HIP errors above are to be read
+    ref32 = T.loss_and_grads_chunked(params, X, u.detach(), S, N, ALPHA, device=dev, dtype=torch.float32,
+                                     chunk=16384 if H <= 64 else 2048)
+    err32 = {}
+    for k in ("loss", "prediction", "xhat", "g_W_inp", "g_b_inp", "g_W_out"):
+        r = ref[k].reshape(-1)
+        err32[k] = float((ref32[k].reshape(-1).double() - r).abs().max() / r.abs().max().clamp_min(1e-300))
     for p in ctrl.parameters():
         p.grad = None
     grads = ("g_u0", "g_W_inp", "g_b_inp", "g_W_out")
-    return {"grad_max_rel_err": max(err[k] for k in grads),
+    return {"grad_max_rel_err": max(err[k] for k in grads), "torch_fp32_err": err32,
             "out_max_rel_err": max(err[k] for k in ("loss", "prediction", "xhat")),
             "per_tensor": err, "batch": B, "g_u0_kink_band": band,
             "compared": "loss/prediction/xhat and the parameter gradients over every trajectory; g_u0 outside the band",
@@ -275,6 +283,11 @@ def main():
     ap.add_argument("--small-limit", type=int, default=None,
                     help="fcr_set_small_batch_limit: B at or below it runs the small-batch kernels (0 = never; "
                          "default: the library's, 8192)")
+    ap.add_argument("--wide-keep-budget", default=None,
+                    help="H > 52: bytes of kept windows the workspace may hold (fcr_set_wide_keep_budget), in GiB, or "
+                         "'max' = the device's free memory less 8 GiB. The library default keeps what fits in half the "
+                         "free memory (within 40%% of HBM); a job that owns the GPU opts in to more: fewer windows "
+                         "recomputed in the backward")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal of the N > 1 path on a 1-GPU box: every rank on cuda:0, gloo process group "
                          "(launcher, barriers, grad all-reduce, max-over-ranks timing); not a scaling number")
@@ -300,6 +313,14 @@ def main():
             dist.init_process_group("nccl", device_id=dev, timeout=pg_timeout)
         world = dist.get_world_size()
     B, N, H = args.batch, args.horizon, args.hidden
+    keep_budget = None
+    if args.wide_keep_budget is not None:
+        if args.wide_keep_budget == "max":
+            free, _ = torch.cuda.mem_get_info(dev)
+            keep_budget = max(0, free - (8 << 30))
+        else:
+            keep_budget = int(float(args.wide_keep_budget) * (1 << 30))
+        fca._native.set_wide_keep_budget(keep_budget)
     if args.small_limit is not None:
         fca._native.set_small_batch_limit(args.small_limit)
     # which kernel family runs (include/fcr.h, fcr_set_small_batch_limit)
@@ -422,6 +443,10 @@ def main():
                                    f"ctrl 3-50-1, {prec_label}" + (", HIP-graph replay" if captured is not None else ""),
                        "batch_per_gpu": B, "global_batch": B * world,
                        "horizon": N, "hidden": H, "parallelism": f"dp{world}", "world_size": world,
+                       **({"wide_keep_budget_gib": round(keep_budget / 2**30, 1),
+                           "workspace_gib": round(fca._native.workspace_bytes(
+                               fca.rollout.make_dims(B, N, H, 3, 50, ALPHA), True) / 2**30, 1)}
+                          if keep_budget is not None else {}),
                        **({"rehearsal": "--share-gpu: every rank on cuda:0 over gloo (path check, not a scaling "
                                         "number)"} if args.share_gpu else {})},
             "roofline": roof,
@@ -436,6 +461,8 @@ def main():
             "loss": float(loss.item()),
         }
         if args.grad_check != "off":
+            if keep_budget is not None:
+                torch.cuda.empty_cache()   # the kept windows' workspace back to the device for the checker's chunks
             t_gc = time.perf_counter()
             gc = grad_check(sim, ctrl, X, S, N, dev, args.precision)
             gc["seconds"] = round(time.perf_counter() - t_gc, 2)
