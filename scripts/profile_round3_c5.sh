@@ -18,6 +18,6 @@ echo trace ok
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/c5fetch -o c5 -- $C5 --steps 1 --warmup 1 --no-cpu-baseline --grad-check off > $O/c5fetch.log 2>&1
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/c5write -o c5 -- $C5 --steps 1 --warmup 1 --no-cpu-baseline --grad-check off > $O/c5write.log 2>&1
 echo pmc ok
-mkdir -p $O/c5 && ln -sfn $O/c5fetch $O/c5/fetch && ln -sfn $O/c5write $O/c5/write
+mkdir -p $O/c5 && ln -sfn ../c5fetch $O/c5/fetch && ln -sfn ../c5write $O/c5/write   # relative: valid on the box and here
 (cd $R && python3 scripts/pmc_c5_summary.py $TAG $O/c5 > $O/c5summary.log 2>&1)
 tail -20 $O/c5summary.log
