@@ -270,7 +270,7 @@ struct WideLayout {
     size_t Act, dH, dC, D[2], rowg, dv, fnn_part, wsc, rng, total;
     // split-f16 gate GEMM operands (fcr_wide.h: forward A per layer, backward A per weight, the cells'
     // operand rows XB [3][10][B][6H] (layer 0 rows 3H + kX16 long), the dgate rows [B][12H])
-    size_t fa[3], bih[3], XB, dGsp, consts;   // bih: layers >= 1 backward A [12H][2H]
+    size_t fa[3], bih[3], XB, dGsp, consts, rsc;   // bih: layers >= 1 backward A [12H][2H]
     size_t bt[3];     // hand-written gradient product (fcr_wbwd.h): W^T split [NO][4H] hi, then lo
     size_t bx0, E0;   // layer 0's backward A [12H][H + 8] and its product rows [B][H + 8]
     // kept windows (the last `keep` of N): the forward's gate pre-activations and c per cell
@@ -330,6 +330,7 @@ WideLayout make_wide(const fcr_dims *d, int with_backward, int keep = 0) {
         L.dGsp = take(F16 * B * 12 * H);
         L.E0 = take(F * B * ((H + 8 + 31) / 32 * 32));
         L.consts = take(F * 4);
+        L.rsc = take(F * (size_t)d->B);   // per-row dgate scales of the hand-written backward product
         L.Act = take(F * kLayers * kL * B * 4 * H);
         L.dH = take(F * B * H);
         L.dC = take(F * B * H);
@@ -449,7 +450,7 @@ int gemm16_bwd(rocblas_handle h, int B, int n, int H, const _Float16 *A, int lda
 struct WideSplit {
     const _Float16 *fa[kLayers], *bih[kLayers], *bt[kLayers];
     _Float16 *XB, *dGsp;
-    float *consts;
+    float *consts, *rsc;
     const _Float16 *bx0;
     float *E0;
 };
@@ -464,6 +465,7 @@ WideSplit wide_split(const WideLayout &L, char *base) {
     w.XB = (_Float16 *)(base + L.XB);
     w.dGsp = L.dGsp ? (_Float16 *)(base + L.dGsp) : nullptr;
     w.consts = L.consts ? (float *)(base + L.consts) : nullptr;
+    w.rsc = (L.rsc && w.bt[0]) ? (float *)(base + L.rsc) : nullptr;   // the hand-written product only
     w.bx0 = L.bx0 ? (const _Float16 *)(base + L.bx0) : nullptr;
     w.E0 = L.E0 ? (float *)(base + L.E0) : nullptr;
     return w;
@@ -556,16 +558,17 @@ constexpr int kRowgT = FCR_ROWG_T;
 template <bool PRE>
 int launch_cell_bwd(int B, int H, hipStream_t s, const float *act, const float *c, const float *c_prev,
                     const float *dH, const float *din, float *dC, float *dG, _Float16 *dgsp, const float *consts,
-                    int dh_scaled, int ldh, int ldx, const float *wih0 = nullptr, float *rowg = nullptr, int dg3 = 1) {
+                    int dh_scaled, int ldh, int ldx, const float *wih0 = nullptr, float *rowg = nullptr, int dg3 = 1,
+                    float *rsc = nullptr) {
     const int V = cell_vec(H);
     const dim3 grid((unsigned)(((size_t)B * (H / V) + 255) / 256)), blk(256);
-    if (rowg && (V != 4 || 64 % (H / V)))
+    if ((rowg || rsc) && (V != 4 || 64 % (H / V)))
         return fail(FCR_EINVAL, "wide_cell_bwd_kernel: in-kernel row gradient needs 64 %% (H / 4) == 0 (H = %d)", H);
     if (rowg) {   // layer 0: kRowgT trajectories per thread share one load of its W_ih0 rows
         const dim3 g0((unsigned)(((size_t)(B + kRowgT - 1) / kRowgT * (H / V) + 255) / 256));
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4, kRowgT>), g0, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, dg3, wih0, rowg);
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4, kRowgT>), g0, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, dg3, wih0, rowg, rsc);
     } else if (V == 4)
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, dg3);
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, dg3, nullptr, nullptr, rsc);
     else if (V == 2)
         hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 2>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, dg3);
     else
@@ -623,7 +626,8 @@ int launch_wgemm_cell(const WgArgs &wa, hipStream_t s) {
 // dX' (row-major [B][ldo], columns [0, NO)) = dGs W on the hand-written split-f16 kernel (fcr_wbwd.h), in the
 // dgates' scaled units like gemm16_bwd; bt = W^T split [NP][4H] hi then lo (NP packed rows; the product uses the
 // first NO <= NP of them), dGs = [hi 4H | lo 4H | (hi 4H)] rows
-int launch_wb(const _Float16 *bt, int NP, int NO, int H, int B, const _Float16 *dGs, float *dX, int ldo, hipStream_t s) {
+int launch_wb(const _Float16 *bt, int NP, int NO, int H, int B, const _Float16 *dGs, float *dX, int ldo, const float *rs,
+              hipStream_t s) {
     static bool attr_set = false;
     if (!attr_set) {
         const hipError_t e = hipFuncSetAttribute((const void *)wide_bwd_gemm_kernel,
@@ -639,6 +643,7 @@ int launch_wb(const _Float16 *bt, int NP, int NO, int H, int B, const _Float16 *
     wa.lda = 4 * H;
     wa.ldb = 12 * H;
     wa.lo_off = 4 * H;
+    wa.rs = rs;
     wa.ldo = ldo;
     wa.NB = B;
     wa.NO = NO;
@@ -851,17 +856,18 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
                                                 nullptr, sp.dGsp, sp.consts,
                                                 l < kLayers - 1 || t < kL - 1,   // (2, 9): the head's dH
                                                 ldh, 2 * H, rg ? wih[0] : nullptr,
-                                                rg ? a.rowg + (size_t)(j + t) * B * kIn : nullptr, sp.bt[0] ? 0 : 1)))
+                                                rg ? a.rowg + (size_t)(j + t) * B * kIn : nullptr, sp.bt[0] ? 0 : 1, sp.rsc)))
                     return rc;
                 if (l > 0 && sp.bt[l]) {   // [input gradient | dh_{t-1}] (t = 0: the former only), hand-written product
-                    if ((rc = launch_wb(sp.bt[l], 2 * H, t > 0 ? 2 * H : H, H, B, sp.dGsp, D[l - 1] + (size_t)t * 2 * cell, 2 * H, s)))
+                    if ((rc = launch_wb(sp.bt[l], 2 * H, t > 0 ? 2 * H : H, H, B, sp.dGsp, D[l - 1] + (size_t)t * 2 * cell, 2 * H,
+                                        sp.rsc, s)))
                         return rc;
                 } else if (l > 0) {   // [input gradient | dh_{t-1}] (t = 0: the former only) into D[l-1] row t
                     if ((rc = gemm16_bwd(h, B, t > 0 ? 2 * H : H, H, sp.bih[l], 2 * H, sp.dGsp, D[l - 1] + (size_t)t * 2 * cell,
                                          2 * H)))
                         return rc;
                 } else if (rg && sp.bt[0]) {   // layer 0, row gradient done: dh_{t-1} only (t = 0: nothing)
-                    if (t > 0 && (rc = launch_wb(sp.bt[0], H, H, H, B, sp.dGsp, sp.E0, LE, s))) return rc;
+                    if (t > 0 && (rc = launch_wb(sp.bt[0], H, H, H, B, sp.dGsp, sp.E0, LE, sp.rsc, s))) return rc;
                 } else if (rg) {   // layer 0, row gradient done: dh_{t-1} only (t = 0: nothing)
                     if (t > 0 && (rc = gemm16_bwd(h, B, H, H, sp.bx0, H8, sp.dGsp, sp.E0, LE))) return rc;
                 } else {

@@ -47,6 +47,7 @@ struct WbArgs {
     const _Float16 *Ahi, *Alo;   // [NO][lda]
     const _Float16 *B;           // dgate rows [B][ldb], hi at +0, lo at +lo_off halves
     float *out;                  // [B][ldo], columns [0, NO)
+    const float *rs;             // [B] per-row factor applied to the output (the dgate rows' own inverse scales), or null
     int lda, ldb, lo_off, ldo, NB, NO, K;
 };
 
@@ -146,10 +147,11 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_gemm_kernel(WbArgs a) 
         const int b = b0 + 16 * (kWbTN * wn + j) + fr;
         if (b >= a.NB) continue;
         float *row = a.out + (size_t)b * a.ldo;
+        const float f = a.rs ? a.rs[b] : 1.0f;
 #pragma unroll
         for (int i = 0; i < kWbTM; ++i) {
             const int col = m0 + 16 * (kWbTM * wm + i) + 4 * fq;
-            if (col < a.NO) *reinterpret_cast<f32x4 *>(row + col) = acc[i][j];
+            if (col < a.NO) *reinterpret_cast<f32x4 *>(row + col) = acc[i][j] * f;
         }
     }
 }

@@ -285,11 +285,15 @@ __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restr
                                      const float *__restrict__ c_prev, const float *__restrict__ dH,
                                      const float *__restrict__ din, float *dC, float *dG, _Float16 *dgsp,
                                      const float *__restrict__ consts, int dh_scaled, int ldh, int ldx, int B,
-                                     int H, int dg3, const float *__restrict__ wih0 = nullptr, float *rowg = nullptr) {
+                                     int H, int dg3, const float *__restrict__ wih0 = nullptr, float *rowg = nullptr,
+                                     float *rsc = nullptr) {
     using W = WideVec<V>;
     // with consts (split-f16 rollout) din, and dH unless it is the head's, come from gemm16_bwd in the
     // scaled units of the dgates: back by 1/scale = consts[0], one fp32 product each
-    const float c0 = consts ? consts[0] : 1.0f, mh = dh_scaled ? c0 : 1.0f;
+    // rsc (the hand-written product, fcr_wbwd.h): every trajectory row's dgates are split at their OWN power of two
+    // (2^(13-e), e = exponent of a bound on the row's |dgates|; its inverse to rsc[b], which the product applies to its
+    // output row), so the products come back in true units and din / dH need no unscaling
+    const float c0 = (consts && !rsc) ? consts[0] : 1.0f, mh = dh_scaled ? c0 : 1.0f;
     const int HV = H / V;
     // a thread owns V units of T consecutive trajectories (T > 1 only for layer 0's row gradient: its W_ih0
     // rows, 4 V kIn floats, are loaded once for the T trajectories instead of once per trajectory)
@@ -324,6 +328,27 @@ __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restr
         typename W::F cp = {}, dn = {}, dg[4], dco;
         if (c_prev) cp = W::ld(c_prev + idx);
         if (din) dn = W::ld(din + b * ldx + u);
+        // rsc: the row's power of two from a bound every dgate of it respects, |dgate| <= |dc_t| <= |dc| + |dh|, taken
+        // from the inputs (so the row reduction runs beside the gate arithmetic rather than after it); the row's H / V
+        // threads are one aligned segment of a wave (the host checks 64 % (H / V) == 0)
+        float rsc_up = 1.0f;
+        if (rsc) {
+            float mx = 0.0f;
+#pragma unroll
+            for (int k = 0; k < V; ++k) mx = fmaxf(mx, fabsf(dhv[k] * mh + dn[k] * c0) + fabsf(dcv[k]));
+            if (HV >= 16) {   // the first four levels on DPP inside 16-lane rows (as the row gradient's sums)
+                mx = fmaxf(mx, dpp_f32<0xB1>(mx));
+                mx = fmaxf(mx, dpp_f32<0x4E>(mx));
+                mx = fmaxf(mx, dpp_f32<0x141>(mx));
+                mx = fmaxf(mx, dpp_f32<0x140>(mx));
+                for (int o = 16; o < HV; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+            } else {
+                for (int o = 1; o < HV; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+            }
+            const int ex = mx > 0.0f ? __builtin_amdgcn_frexp_expf(mx) : 0;   // every |dgate| < 2^ex
+            rsc_up = __builtin_amdgcn_ldexpf(1.0f, 13 - ex);
+            if (u == 0) rsc[b] = __builtin_amdgcn_ldexpf(1.0f, ex - 13);
+        }
 #pragma unroll
         for (int k = 0; k < V; ++k) {
             const float i = PRE ? sigm(ai[k]) : ai[k], f = PRE ? sigm(af[k]) : af[k], g = PRE ? tanhf(ag[k]) : ag[k],
@@ -344,7 +369,7 @@ __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restr
         }
         if (dgsp) {   // split-f16 operand row [hi | lo | hi] of W^T dG, scaled into the f16 range (wide_bscale_kernel);
             // the hand-written product (fcr_wbwd.h) reads hi and lo once each: no third copy (dg3 = 0)
-            const float sc = consts[3];
+            const float sc = rsc ? rsc_up : consts[3];
             _Float16 *o16 = dgsp + b * 12 * H + u;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {

@@ -10,3 +10,4 @@ for p in fp32 f16 f16fwd; do
 done
 timeout -k 10 300 python -u scripts/bench_graphed.py > $O/graphed.log 2>&1 || { tail -20 $O/graphed.log; exit 1; }
 tail -8 $O/graphed.log
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_surrogate.py > $O/sur_tests.log 2>&1; rc=$?; tail -2 $O/sur_tests.log; exit $rc
