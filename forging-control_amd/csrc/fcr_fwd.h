@@ -34,6 +34,9 @@ __device__ __forceinline__ void rot_left(float (&w)[kL]) {
 #ifndef FCR_FWD_SPREAD
 #define FCR_FWD_SPREAD 1   // spread each tile pair's pointwise over the next pair's MFMA regions
 #endif
+#ifndef FCR_FWD_RDFIRST
+#define FCR_FWD_RDFIRST 0
+#endif
 
 // Issue-priority pacing of the two waves that share a SIMD (waves w and w+4 of the workgroup).
 //   FCR_FWD_PRIO 1: alternate the higher priority cell by cell;
@@ -115,6 +118,11 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
                 rd(r0 + 2, KLO, nh[0], nl[0]);
                 if (r1 + 2 < R1) rd(r1 + 2, KLO, nh[1], nl[1]);
             }
+#if FCR_FWD_RDFIRST
+            // the next region's reads issue ahead of this region's MFMAs (otherwise the scheduler places them
+            // behind most of the chain, and the next region opens on their LDS latency)
+            sched_fence();
+#endif
             const int ch = kOneAcc ? 0 : (kb - KLO) & 1;
 #if FCR_ABLATE == 1   // diagnostic: the fragment reads and operands stay, the MFMAs go
             acc[0][ch][0] += (float)ah[0][0] + (float)bh[kb][0];
