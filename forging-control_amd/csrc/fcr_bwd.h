@@ -25,7 +25,19 @@ struct CellIn {
     f32x4 c[Geo<HS>::HQ];   // c_{t-1}
     f32x4 d[Geo<HS>::HQ];   // din = dx of the layer above at t (layers 0, 1)
     f32x4 o[Geo<HS>::HQ];   // split record of the cell's own h_t (its tanh(c_t) = h_t / o_t: lstm_point_grad_h)
+    float S = 1.0f, Sd = 1.0f;   // carried scale (FCR_BWD_CARRY): dh, dc are held as dh S, dc S; Sd = 1 / S
 };
+
+// FCR_BWD_CARRY = 1: the rollout's backward carries dh and dc in units of a per-trajectory power of two S that is
+// re-centred only when the scaled bound leaves [2^9, 2^14), and forms the dgates unscaled by the exp2 pre-scale
+// (the product then returns kappa S W^T dG): the dgates need no multiply (18 % of the cell's VALU multiplies, 39 per
+// cell at H = 50), and the frexp / ldexp chain runs on the rare re-centring only. The surrogate's cells (DG) keep
+// the per-cell scale, whose dgate blocks they store with a power-of-two unscaling factor. Measured (round 3d,
+// profiles/round3d_carry_ab*.log): GPU suite green, results within 9e-8 of the per-cell scale, 30-42 fewer VALU per
+// cell and no faster (+0.1 / +0.8 % in two interleaved A/B runs): off by default.
+#ifndef FCR_BWD_CARRY
+#define FCR_BWD_CARRY 0
+#endif
 
 // Where the next cell's inputs live: buffer descriptors over this wave's own slab regions (SGPRs)
 // and byte offsets (SGPRs), so every load's address is one shared lane-offset VGPR.
@@ -133,6 +145,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     constexpr int KLO = (L0 && FIRST) ? G::XBLK : 0;
     constexpr int KHI = FIRST ? (L0 ? G::XBLK + 1 : G::KX1) : KB;
 
+    constexpr bool CARRY = FCR_BWD_CARRY && !DG;
     float up, down, sg0, sgg;   // the trajectory's power-of-two scale, set once the incoming dh is in
     float dgd = 0.0f;           // DG: down, or 0 when the trajectory has no gradient here (its dgates are zero)
 
@@ -206,19 +219,23 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     auto slot_grad = [&](int r, f32x4 a, float *va, float *vb) {
         f32x4 P;
         f32x2 Q;
-        if (OWN) lstm_point_grad_h<FIRST>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], rec_h<HS>(ci.o, r), P, Q);
-        else lstm_point_grad<FIRST>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], P, Q);
+        if (OWN) lstm_point_grad_h<FIRST, CARRY>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], rec_h<HS>(ci.o, r), P, Q);
+        else lstm_point_grad<FIRST, CARRY>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], P, Q);
         // torch LSTM semantics: dc = dc_carried + dh dh/dc; the carried dc of the cell below is dc f
         const float dcv = fmaf(dh[r], P[0], dc[r]);
         dc[r] = dcv * Q[1];
-        const float dcs = dcv * sg0;
-        va[0] = dcs;
+        if (CARRY) {   // dh, dc already in S units; the g row's -1/2 is in Q[0] (dcdg_half)
+            va[0] = va[1] = va[2] = dcv;
+            va[3] = dh[r];
+        } else {
+            const float dcs = dcv * sg0;
+            va[0] = va[1] = dcs;
+            va[2] = dcv * sgg;
+            va[3] = dh[r] * sg0;
+        }
         vb[0] = P[2];
-        va[1] = dcs;
         vb[1] = P[3];
-        va[2] = dcv * sgg;
         vb[2] = Q[0];
-        va[3] = dh[r] * sg0;
         vb[3] = P[1];
         // c_{t-1} quad of slots 4k..4k+3 consumed: the next cell's comes in
         if (NX_HC && (r & 3) == 3)
@@ -272,17 +289,39 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
         float m = 0.0f;
 #pragma unroll
         for (int r = 0; r < HS; ++r) {
-            dh[r] += DIN ? ci.d[r >> 2][r & 3] : ext[r];
+            const float din = DIN ? ci.d[r >> 2][r & 3] : ext[r];
+            dh[r] = CARRY ? fmaf(din, ci.S, dh[r]) : dh[r] + din;
             m = fmaxf(m, fabsf(dh[r]) + fabsf(dc[r]));
         }
-        m = fmaxf(m, __shfl_xor(m, 16));
-        m = fmaxf(m, __shfl_xor(m, 32));
-        const int e = max(__builtin_amdgcn_frexp_expf(m), -100);   // m < 2^e; all-zero -> e = 0
-        up = __builtin_amdgcn_ldexpf(1.0f, 13 - e);
-        down = __builtin_amdgcn_ldexpf(1.0f, e - 13);
-        sg0 = up * kInvNegLog2e;   // dgate scale of the i, f, o rows
-        sgg = sg0 * -0.5f;         // and of the g rows
-        if (DG) dgd = m > 0.0f ? down : 0.0f;
+        m = max_q(m);
+        if constexpr (CARRY) {
+            // keep S while the scaled bound m stays in [2^9, 2^14): every dgate is then below 2^16 (|dc/df| <=
+            // |c_{t-1}| / 4 <= 2.5, the other local derivatives <= 1) and far above f16's subnormals; else re-centre
+            // every lane of the wave at m in [2^12, 2^13), as the per-cell scale does (exact: powers of two)
+            const bool off = m >= 0x1p14f || (m < 0x1p9f && m > 0.0f);
+            if (__builtin_amdgcn_ballot_w64(off)) [[unlikely]] {
+                asm volatile("");   // a real branch: not if-converted into selects that run every cell
+                const int e = max(__builtin_amdgcn_frexp_expf(m), -100);   // m < 2^e
+                const float f = m > 0.0f ? __builtin_amdgcn_ldexpf(1.0f, 13 - e) : 1.0f;
+                const float fd = m > 0.0f ? __builtin_amdgcn_ldexpf(1.0f, e - 13) : 1.0f;
+#pragma unroll
+                for (int r = 0; r < HS; ++r) {
+                    dh[r] *= f;
+                    dc[r] *= f;
+                }
+                ci.S *= f;
+                ci.Sd *= fd;
+            }
+            down = ci.Sd * kInvNegLog2e;   // the product returns kappa S W^T dG: true units
+            up = sg0 = sgg = 0.0f;
+        } else {
+            const int e = max(__builtin_amdgcn_frexp_expf(m), -100);   // m < 2^e; all-zero -> e = 0
+            up = __builtin_amdgcn_ldexpf(1.0f, 13 - e);
+            down = __builtin_amdgcn_ldexpf(1.0f, e - 13);
+            sg0 = up * kInvNegLog2e;   // dgate scale of the i, f, o rows
+            sgg = sg0 * -0.5f;         // and of the g rows
+            if (DG) dgd = m > 0.0f ? down : 0.0f;
+        }
     }
     // OWN_REG: the next cell (t - 1, same phase) owns h_{t-1}, whose record this cell has in ci.h: kept in registers
     // for it instead of re-read from the slab (an L2 miss by then)
@@ -383,9 +422,10 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     }
     sched_fence();
     const unsigned long long t2 = stamp_now();
+    const float dnh = CARRY ? kInvNegLog2e : down;   // the next cell's dh (CARRY: stays in S units)
     if (L0) {
 #pragma unroll
-        for (int s = 0; s < HS; ++s) dh[s] = acc[s >> 2][s & 3] * down;
+        for (int s = 0; s < HS; ++s) dh[s] = acc[s >> 2][s & 3] * dnh;
         dxq = acc[HS >> 2][HS & 3] * down;
         dx4 = acc[(HS + 1) >> 2][(HS + 1) & 3] * down;
     } else {
@@ -396,7 +436,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
 #pragma unroll
         for (int s = 0; s < HS; ++s) {
             dxo[s] = acc[s >> 2][s & 3] * down;
-            dh[s] = acc[(HS + s) >> 2][(HS + s) & 3] * down;
+            dh[s] = acc[(HS + s) >> 2][(HS + s) & 3] * dnh;
         }
     }
 #if FCR_ABLATE == 5

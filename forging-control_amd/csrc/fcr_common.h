@@ -115,12 +115,33 @@ __device__ __forceinline__ float hardtanh(float v) { return fminf(fmaxf(v, -1.0f
 __device__ __forceinline__ float sel4(int q, float a, float b, float c, float d) {
     return q == 0 ? a : (q == 1 ? b : (q == 2 ? c : d));
 }
-// sum over the 4 lane groups that share one trajectory
-__device__ __forceinline__ float xor_sum_q(float v) {
-    v += __shfl_xor(v, 16);
-    v += __shfl_xor(v, 32);
-    return v;
+// Sum / max over the 4 lane groups that share one trajectory (lanes l, l^16, l^32, l^48). FCR_PERMLANE = 1:
+// gfx950's v_permlane16_swap / v_permlane32_swap (VALU half exchanges: with both operands the same value,
+// results [row0 row0 row2 row2] and [row1 row1 row3 row3] for 16-lane rows, [lo lo] and [hi hi] for halves),
+// so the reduction needs no LDS round trip; __shfl_xor is a ds_bpermute each. Same operands in the same
+// order as the xor form (commutative adds), so the results are bit for bit those of FCR_PERMLANE = 0 (GPU suite
+// green with it; the backward measured the same, +0.1..0.6 %, the swaps' hazard s_nops eat the LDS round trip:
+// off by default).
+#ifndef FCR_PERMLANE
+#define FCR_PERMLANE 0
+#endif
+template <bool MAX>
+__device__ __forceinline__ float reduce_q(float v) {
+    auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : a + b; };
+#if FCR_PERMLANE
+    const unsigned u = __builtin_bit_cast(unsigned, v);
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    v = op(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+    const unsigned w = __builtin_bit_cast(unsigned, v);
+    const auto s = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+    return op(__builtin_bit_cast(float, (unsigned)s[0]), __builtin_bit_cast(float, (unsigned)s[1]));
+#else
+    v = op(v, __shfl_xor(v, 16));
+    return op(v, __shfl_xor(v, 32));
+#endif
 }
+__device__ __forceinline__ float xor_sum_q(float v) { return reduce_q<false>(v); }
+__device__ __forceinline__ float max_q(float v) { return reduce_q<true>(v); }
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
 
 // After a workgroup barrier every wave runs the same instruction stream in lockstep, so the two

@@ -402,7 +402,24 @@ __device__ __forceinline__ void lstm_point_b(float c, float eo, float &h) {
 #endif
     h = lstm_h(c, eo);
 }
-template <bool FIRST>
+// -0.5 (i - gi g) = 0.5 (gi g - i): the g row's dc/dg with the -1/2 of its exp2 pre-scale (2 log2e against -log2e for
+// i, f, o; fcr_bwd.h, carried scale) folded in. (A v_fma_f32 with the div:2 output modifier would do it in one
+// instruction, but the hardware ignores omod while the kernel runs in IEEE mode, the compute default: measured, the
+// g rows' dgates came out doubled. FCR_OMOD = 1 keeps that form for a build without IEEE mode.)
+#ifndef FCR_OMOD
+#define FCR_OMOD 0
+#endif
+__device__ __forceinline__ float dcdg_half(float gi, float g, float i) {
+#if FCR_OMOD
+    float r;
+    asm("v_fma_f32 %0, %1, %2, -%3 div:2" : "=v"(r) : "v"(gi), "v"(g), "v"(i));
+    return r;
+#else
+    return 0.5f * fmaf(gi, g, -i);
+#endif
+}
+
+template <bool FIRST, bool GH = false>
 __device__ __forceinline__ void lstm_point_grad(f32x4 a, float c_prev, f32x4 &P, f32x2 &Q) {
 #if FCR_ABLATE == 2
     P = a;
@@ -419,7 +436,7 @@ __device__ __forceinline__ void lstm_point_grad(f32x4 a, float c_prev, f32x4 &P,
     const float tc = tanh_f(cn);
     const float h = o * tc;
     P = f32x4{fmaf(-h, tc, o), fmaf(-h, o, h), fmaf(-gi, i, gi), fmaf(-cf, f, cf)};
-    Q = f32x2{fmaf(-gi, g, i), f};
+    Q = f32x2{GH ? dcdg_half(gi, g, i) : fmaf(-gi, g, i), f};
 }
 
 // h of unit slot s from its split record (split_rec: hi at half s, lo at half HS + s of the record words):
@@ -445,7 +462,8 @@ __device__ __forceinline__ float rec_h(const f32x4 *rec, int s) {
 // instead of re-evaluated (exp2, rcp and three VALU): the same six local derivatives. h is the forward's h_t
 // as its split record holds it (fp32-accurate; f16-subnormal h only perturbs P by the record's absolute
 // 2^-25, below the gradients' fp32 level).
-template <bool FIRST>
+// GH: Q[0] = -dc/dg / 2 (dcdg_half) instead of dc/dg
+template <bool FIRST, bool GH = false>
 __device__ __forceinline__ void lstm_point_grad_h(f32x4 a, float c_prev, float h, f32x4 &P, f32x2 &Q) {
     const float i = sigm_pre(a[0]);
     const float f = sigm_pre(a[1]);
@@ -458,7 +476,7 @@ __device__ __forceinline__ void lstm_point_grad_h(f32x4 a, float c_prev, float h
     const float cf = FIRST ? 0.0f : f * c_prev;
     const float tc = h * d_o;
     P = f32x4{fmaf(-h, tc, o), fmaf(-h, o, h), fmaf(-gi, i, gi), fmaf(-cf, f, cf)};
-    Q = f32x2{fmaf(-gi, g, i), f};
+    Q = f32x2{GH ? dcdg_half(gi, g, i) : fmaf(-gi, g, i), f};
 }
 
 // host-side geometry of the forward fragment blocks (bytes), matching Geo16

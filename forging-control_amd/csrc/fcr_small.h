@@ -484,8 +484,7 @@ __device__ __forceinline__ BScale sb_scale(const CellIn<HS> &ci, const float (&e
         dh[r] += DIN ? ci.d[r >> 2][r & 3] : ext[r];
         m = fmaxf(m, fabsf(dh[r]) + fabsf(dc[r]));
     }
-    m = fmaxf(m, __shfl_xor(m, 16));
-    m = fmaxf(m, __shfl_xor(m, 32));
+    m = max_q(m);
     const int e = max(__builtin_amdgcn_frexp_expf(m), -100);   // m < 2^e; all-zero -> e = 0
     BScale b;
     b.sg0 = __builtin_amdgcn_ldexpf(1.0f, 13 - e) * kInvNegLog2e;
