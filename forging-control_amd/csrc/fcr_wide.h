@@ -280,6 +280,10 @@ template <int CTRL>
 __device__ __forceinline__ float dpp_f32(float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
+// FCR_WIDE_CREC = 1: with PRE, c_t is recomputed from the pre-activations and c_{t-1} rather than loaded
+#ifndef FCR_WIDE_CREC
+#define FCR_WIDE_CREC 1
+#endif
 template <bool PRE, int V, int T = 1>
 __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restrict__ act, const float *__restrict__ c,
                                      const float *__restrict__ c_prev, const float *__restrict__ dH,
@@ -324,9 +328,10 @@ __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restr
         if (b >= (size_t)B) break;   // uniform over the trajectory's H / V threads
         const float *a4 = act + b * 4 * H + u;
         const typename W::F ai = W::ld(a4), af = W::ld(a4 + H), ag = W::ld(a4 + 2 * H), ao = W::ld(a4 + 3 * H);
-        const typename W::F cv = W::ld(c + idx), dhv = W::ld(dH + b * ldh + u), dcv = W::ld(dC + idx);
-        typename W::F cp = {}, dn = {}, dg[4], dco;
+        const typename W::F dhv = W::ld(dH + b * ldh + u), dcv = W::ld(dC + idx);
+        typename W::F cp = {}, dn = {}, dg[4], dco, cv;
         if (c_prev) cp = W::ld(c_prev + idx);
+        if (!(PRE && FCR_WIDE_CREC)) cv = W::ld(c + idx);
         if (din) dn = W::ld(din + b * ldx + u);
         // rsc: the row's power of two from a bound every dgate of it respects, |dgate| <= |dc_t| <= |dc| + |dh|, taken
         // from the inputs (so the row reduction runs beside the gate arithmetic rather than after it); the row's H / V
@@ -353,7 +358,9 @@ __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restr
         for (int k = 0; k < V; ++k) {
             const float i = PRE ? sigm(ai[k]) : ai[k], f = PRE ? sigm(af[k]) : af[k], g = PRE ? tanhf(ag[k]) : ag[k],
                         o = PRE ? sigm(ao[k]) : ao[k];
-            const float tc = tanhf(cv[k]);
+            // c_t rebuilt as the forward's cell formed it (fcr_wgemm.h epilogue: f c_{t-1} + i g) instead of read: 1 of the
+            // ~14 KB a trajectory row moves through this HBM-bound kernel
+            const float tc = tanhf((PRE && FCR_WIDE_CREC) ? (c_prev ? f * cp[k] : 0.0f) + i * g : cv[k]);
             const float dh = dhv[k] * mh + dn[k] * c0;
             const float dct = dcv[k] + dh * o * (1.0f - tc * tc);
             dg[0][k] = dct * g * i * (1.0f - i);
