@@ -37,6 +37,11 @@ __device__ __forceinline__ void rot_left(float (&w)[kL]) {
 #ifndef FCR_FWD_RDFIRST
 #define FCR_FWD_RDFIRST 0
 #endif
+// FCR_FWD_TM = 1: layers 0 and 1 run time-major in one phase (layer 1 takes layer 0's h_t from registers instead of
+// re-reading it from the slab: -1.37 GB of HBM reads per launch at B = 65 536); layer 2 keeps its own phase
+#ifndef FCR_FWD_TM
+#define FCR_FWD_TM 0
+#endif
 
 // Issue-priority pacing of the two waves that share a SIMD (waves w and w+4 of the workgroup).
 //   FCR_FWD_PRIO 1: alternate the higher priority cell by cell;
@@ -276,6 +281,89 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
 #define SEQ_O(l, t) (oj + (uint32_t)(((l) * kL + (t)) * qcell * 16))
         const unsigned long long st_w1 = fstamp();
         st_head += st_w1 - st_w0;
+#if FCR_FWD_TM
+        // ---- layers 0 and 1 together, time-major (Functions.py:374): layer 1's input h_t leaves layer 0's cell
+        // already split in registers, so the slab holds it only for the backward; layer 1's fragments sit beside
+        // the resident layer 0 for the phase, layer 2's replace them after it ----
+        {
+            const unsigned long long st_f0 = fstamp();
+            if (!LP) {
+                lds_fill<G::FA1 * 4, kFwdWaves>(lw, a.p.fa[1]);   // its first barrier also publishes the resident blocks
+                stagger();
+            } else if (j == 0) {
+                __syncthreads();   // f16 mode: every layer resident, never refilled
+                stagger();
+            }
+            const unsigned long long st_f1 = fstamp();
+            st_fill += st_f1 - st_f0;
+            const float *lw1 = LP ? lwl[1] : lw;
+            float c1[HS], h1[HS];   // layer 1's c and the split record of its h
+            {
+                const float x0 = w0[0], x1 = w1[0];
+                rot_left(w0);
+                rot_left(w1);
+                fwd16_cell<HS, true, true, LP>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
+                split_rec<HS>(hout, hp);
+                if (STORE) {
+                    buf_store_quads<HS>(rh, SEQ_O(0, 0), hp, lane);
+                    if (FCR_ABLATE != 3) buf_st2(rx, lane * 8, (uint32_t)(j * kL * kWave * 8), f32x2{x0, x1});
+                    buf_store_quads<HS>(rc, SEQ_O(0, 0), c, lane);
+                }
+                fwd16_cell<HS, false, true, LP>(lw1, lane, 0.0f, 0.0f, hp, h1, c1, hout, turn);
+                split_rec<HS>(hout, h1);
+                buf_store_quads<HS>(rh, SEQ_O(1, 0), h1, lane);
+                if (STORE) buf_store_quads<HS>(rc, SEQ_O(1, 0), c1, lane);
+            }
+            for (int t = 1; t < kL; ++t) {
+                const float x0 = w0[0], x1 = w1[0];
+                rot_left(w0);
+                rot_left(w1);
+                fwd16_cell<HS, true, false, LP>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
+                split_rec<HS>(hout, hp);
+                if (STORE) {
+                    buf_store_quads<HS>(rh, SEQ_O(0, t), hp, lane);
+                    if (FCR_ABLATE != 3) buf_st2(rx, lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{x0, x1});
+                    if (t + 1 < kL) buf_store_quads<HS>(rc, SEQ_O(0, t), c, lane);   // c_9 is never a c_{t-1}
+                }
+                fwd16_cell<HS, false, false, LP>(lw1, lane, 0.0f, 0.0f, hp, h1, c1, hout, turn);
+                split_rec<HS>(hout, h1);
+                buf_store_quads<HS>(rh, SEQ_O(1, t), h1, lane);
+                if (STORE && t + 1 < kL) buf_store_quads<HS>(rc, SEQ_O(1, t), c1, lane);
+            }
+            st_l0 += fstamp() - st_f1;
+        }
+        // ---- layer 2: its input sequence (layer 1's h) streamed back from the slab, one cell ahead ----
+        {
+            constexpr int l = 2;
+            const unsigned long long st_f0 = fstamp();
+            if (!LP) {
+                lds_fill<G::FA1 * 4, kFwdWaves>(lw, a.p.fa[l]);
+                stagger();
+            }
+            const float *lwc = LP ? lwl[l] : lw;
+            st_fill += fstamp() - st_f0;
+            buf_load_quads<HS>(xc, rh, SEQ_O(l - 1, 0), lane);
+            buf_load_quads<HS>(xn, rh, SEQ_O(l - 1, 1), lane);
+            fwd16_cell<HS, false, true, LP>(lwc, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
+            split_rec<HS>(hout, hp);
+            if (STORE) buf_store_quads<HS>(rh, SEQ_O(l, 0), hp, lane);
+            if (STORE) buf_store_quads<HS>(rc, SEQ_O(l, 0), c, lane);
+#pragma unroll
+            for (int r = 0; r < HS; ++r) xc[r] = xn[r];
+#pragma unroll 3
+            for (int t = 1; t < kL; ++t) {
+                buf_load_quads<HS>(xn, rh, SEQ_O(l - 1, t + 1 < kL ? t + 1 : t), lane);
+                fwd16_cell<HS, false, false, LP>(lwc, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
+                if (t + 1 < kL) {   // h_9 of layer 2 only feeds the readout (fp32 hout)
+                    split_rec<HS>(hout, hp);
+                    if (STORE) buf_store_quads<HS>(rh, SEQ_O(l, t), hp, lane);
+                }
+                if (STORE && t + 1 < kL) buf_store_quads<HS>(rc, SEQ_O(l, t), c, lane);
+#pragma unroll
+                for (int r = 0; r < HS; ++r) xc[r] = xn[r];
+            }
+        }
+#else
         // ---- layer 0 over the window (Functions.py:374) ----
         if (j == 0) {
             __syncthreads();   // resident blocks are in place — layer 0 (and in f16 mode every layer) never refills
@@ -360,6 +448,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
                 for (int r = 0; r < HS; ++r) xc[r] = xn[r];
             }
         }
+#endif
 #undef SEQ_O
         // ---- readout fc(h_9 of layer 2) (Functions.py:377) ----
         float xo[kOut];
