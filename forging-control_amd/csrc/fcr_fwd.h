@@ -38,9 +38,11 @@ __device__ __forceinline__ void rot_left(float (&w)[kL]) {
 #define FCR_FWD_RDFIRST 0
 #endif
 // FCR_FWD_TM = 1: layers 0 and 1 run time-major in one phase (layer 1 takes layer 0's h_t from registers instead of
-// re-reading it from the slab: -1.37 GB of HBM reads per launch at B = 65 536); layer 2 keeps its own phase
+// re-reading it from the slab: -1.37 GB of HBM reads per launch at B = 65 536, and no prefetch loads or waits for
+// them); layer 2 keeps its own phase. Measured (profiles/round3d_fwd_tm_ab.log, one process, both orders): forward
+// 2.67 -> 2.52 and 2.61 -> 2.47 ms, bit-identical; f16 mode at B = 262 144 8.41 -> 8.29 ms
 #ifndef FCR_FWD_TM
-#define FCR_FWD_TM 0
+#define FCR_FWD_TM 1
 #endif
 
 // Issue-priority pacing of the two waves that share a SIMD (waves w and w+4 of the workgroup).
