@@ -300,6 +300,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             st_fill += st_f1 - st_f0;
             const float *lw1 = LP ? lwl[1] : lw;
             float c1[HS], h1[HS];   // layer 1's c and the split record of its h
+            float c2[LP ? HS : 1], h2[LP ? HS : 1];   // f16 mode: layer 2's
             {
                 const float x0 = w0[0], x1 = w1[0];
                 rot_left(w0);
@@ -313,8 +314,16 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
                 }
                 fwd16_cell<HS, false, true, LP>(lw1, lane, 0.0f, 0.0f, hp, h1, c1, hout, turn);
                 split_rec<HS>(hout, h1);
-                buf_store_quads<HS>(rh, SEQ_O(1, 0), h1, lane);
+                if (STORE || !LP) buf_store_quads<HS>(rh, SEQ_O(1, 0), h1, lane);   // f16 mode: layer 2 is in this phase
                 if (STORE) buf_store_quads<HS>(rc, SEQ_O(1, 0), c1, lane);
+                if constexpr (LP) {   // every layer resident: layer 2 joins the phase (its h_t from registers as well)
+                    fwd16_cell<HS, false, true, LP>(lwl[2], lane, 0.0f, 0.0f, h1, h2, c2, hout, turn);
+                    split_rec<HS>(hout, h2);
+                    if (STORE) {
+                        buf_store_quads<HS>(rh, SEQ_O(2, 0), h2, lane);
+                        buf_store_quads<HS>(rc, SEQ_O(2, 0), c2, lane);
+                    }
+                }
             }
             for (int t = 1; t < kL; ++t) {
                 const float x0 = w0[0], x1 = w1[0];
@@ -329,13 +338,23 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
                 }
                 fwd16_cell<HS, false, false, LP>(lw1, lane, 0.0f, 0.0f, hp, h1, c1, hout, turn);
                 split_rec<HS>(hout, h1);
-                buf_store_quads<HS>(rh, SEQ_O(1, t), h1, lane);
+                if (STORE || !LP) buf_store_quads<HS>(rh, SEQ_O(1, t), h1, lane);
                 if (STORE && t + 1 < kL) buf_store_quads<HS>(rc, SEQ_O(1, t), c1, lane);
+                if constexpr (LP) {
+                    fwd16_cell<HS, false, false, LP>(lwl[2], lane, 0.0f, 0.0f, h1, h2, c2, hout, turn);
+                    if (t + 1 < kL) {   // h_9 of layer 2 only feeds the readout (fp32 hout)
+                        split_rec<HS>(hout, h2);
+                        if (STORE) {
+                            buf_store_quads<HS>(rh, SEQ_O(2, t), h2, lane);
+                            buf_store_quads<HS>(rc, SEQ_O(2, t), c2, lane);
+                        }
+                    }
+                }
             }
             st_l0 += fstamp() - st_f1;
         }
         // ---- layer 2: its input sequence (layer 1's h) streamed back from the slab, one cell ahead ----
-        {
+        if constexpr (!LP) {
             constexpr int l = 2;
             const unsigned long long st_f0 = fstamp();
             if (!LP) {
