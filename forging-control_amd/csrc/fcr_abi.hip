@@ -85,13 +85,9 @@ int slot_tier(int H) { return H <= 16 ? 4 : (H <= 32 ? 8 : 13); }
 
 // H > 52: the backward's gradient products on the hand-written split-f16 kernel (fcr_wbwd.h) when its k-blocks
 // tile 4H and layer 0's window-row gradient is formed in the cell kernel (rowg_in_cell); rocBLAS otherwise.
-// FCR_WIDE_HWBWD=0 builds the rocBLAS path for comparison.
-#ifndef FCR_WIDE_HWBWD
-#define FCR_WIDE_HWBWD 1
-#endif
 bool wide_hwbwd_ok(int H) {
     const bool rowg_cell = H % 4 == 0 && 64 % (H / 4) == 0;   // rowg_in_cell (below)
-    return FCR_WIDE_HWBWD && H % 8 == 0 && rowg_cell;
+    return H % 8 == 0 && rowg_cell;
 }
 
 int check_dims(const fcr_dims *d) {
@@ -550,11 +546,8 @@ int launch_cell(int B, int H, hipStream_t s, const float *G, const float *c_prev
     return launch_check("wide_cell_kernel");
 }
 
-// trajectories per thread of layer 0's backward cell kernel (FCR_ROWG_T: 1 = one per thread, the old mapping)
-#ifndef FCR_ROWG_T
-#define FCR_ROWG_T 4
-#endif
-constexpr int kRowgT = FCR_ROWG_T;
+// trajectories per thread of layer 0's backward cell kernel (1, 4 and 8 measured within 2 ms at config 5, round 2f)
+constexpr int kRowgT = 4;
 template <bool PRE>
 int launch_cell_bwd(int B, int H, hipStream_t s, const float *act, const float *c, const float *c_prev,
                     const float *dH, const float *din, float *dC, float *dG, _Float16 *dgsp, const float *consts,
@@ -602,11 +595,8 @@ __global__ __launch_bounds__(256) void pack_all_kernel(PackAllArgs p) {
 
 // The split path's forward cells (every layer, H % 64 == 0): the cell's GEMM and update as one hand-written
 // kernel (fcr_wgemm.h): 262 us per cell against ~300 us for rocBLAS's GEMM + wide_cell_kernel (B = 65 536,
-// H = 256; DESIGN.md "Config 5"). FCR_WIDE_FUSED=0 builds the rocBLAS path for comparison.
-#ifndef FCR_WIDE_FUSED
-#define FCR_WIDE_FUSED 1
-#endif
-bool wide_fused_ok(int H) { return FCR_WIDE_FUSED && H % kWgU == 0; }
+// H = 256; DESIGN.md "Config 5"); rocBLAS gemm16_fwd + wide_cell_kernel for other H.
+bool wide_fused_ok(int H) { return H % kWgU == 0; }
 int launch_wgemm_cell(const WgArgs &wa, hipStream_t s) {
     static bool attr_set = false;
     if (!attr_set) {

@@ -25,19 +25,7 @@ struct CellIn {
     f32x4 c[Geo<HS>::HQ];   // c_{t-1}
     f32x4 d[Geo<HS>::HQ];   // din = dx of the layer above at t (layers 0, 1)
     f32x4 o[Geo<HS>::HQ];   // split record of the cell's own h_t (its tanh(c_t) = h_t / o_t: lstm_point_grad_h)
-    float S = 1.0f, Sd = 1.0f;   // carried scale (FCR_BWD_CARRY): dh, dc are held as dh S, dc S; Sd = 1 / S
 };
-
-// FCR_BWD_CARRY = 1: the rollout's backward carries dh and dc in units of a per-trajectory power of two S that is
-// re-centred only when the scaled bound leaves [2^9, 2^14), and forms the dgates unscaled by the exp2 pre-scale
-// (the product then returns kappa S W^T dG): the dgates need no multiply (18 % of the cell's VALU multiplies, 39 per
-// cell at H = 50), and the frexp / ldexp chain runs on the rare re-centring only. The surrogate's cells (DG) keep
-// the per-cell scale, whose dgate blocks they store with a power-of-two unscaling factor. Measured (round 3d,
-// profiles/round3d_carry_ab*.log): GPU suite green, results within 9e-8 of the per-cell scale, 30-42 fewer VALU per
-// cell and no faster (+0.1 / +0.8 % in two interleaved A/B runs): off by default.
-#ifndef FCR_BWD_CARRY
-#define FCR_BWD_CARRY 0
-#endif
 
 // Where the next cell's inputs live: buffer descriptors over this wave's own slab regions (SGPRs)
 // and byte offsets (SGPRs), so every load's address is one shared lane-offset VGPR.
@@ -100,15 +88,6 @@ constexpr float kInvNegLog2e = 1.0f / kNegLog2e;
 // OWN: the cell's own h_t record is in ci.o (every cell but the first of a window's layer-2 phase, whose h_9
 // only fed the readout): tanh(c_t) comes from it (lstm_point_grad_h) instead of being re-evaluated.
 // NX_OWN: the next cell's is fetched.
-#ifndef FCR_OWN_REG
-#define FCR_OWN_REG 1
-#endif
-#ifndef FCR_BWD_LAUNDER
-#define FCR_BWD_LAUNDER 1
-#endif
-#ifndef FCR_PRIO
-#define FCR_PRIO 1
-#endif
 #ifndef FCR_STAMP
 #define FCR_STAMP 0   // diagnostic: per-wave s_memtime sums of the cell's sections (ws tail)
 #endif
@@ -130,13 +109,11 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
                                          float &dx4, CellIn<HS> &ci, const NextIn &nx, Stamps &sp,
                                          const DgOut *dgo = nullptr) {
     const unsigned long long t0 = stamp_now();
-#if FCR_PRIO == 1
     // the two waves of a SIMD take turns at the higher issue priority, cell by cell, so neither runs
     // ahead of the other between the phase barriers (oldest-first arbitration otherwise skews them)
     if (sp.t[4] & 1) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
     sp.t[4] ^= 1;
-#endif
     using I = Img<HS, L0>;
     using G = Geo16<HS>;
     constexpr int KB = I::KB, NB = I::NB, KBB = I::KBB;
@@ -145,7 +122,6 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     constexpr int KLO = (L0 && FIRST) ? G::XBLK : 0;
     constexpr int KHI = FIRST ? (L0 ? G::XBLK + 1 : G::KX1) : KB;
 
-    constexpr bool CARRY = FCR_BWD_CARRY && !DG;
     float up, down, sg0, sgg;   // the trajectory's power-of-two scale, set once the incoming dh is in
     float dgd = 0.0f;           // DG: down, or 0 when the trajectory has no gradient here (its dgates are zero)
 
@@ -168,14 +144,13 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
         if (TAIL && KHI == KB) bh[KB - 1] = tail_operand<LP>(bh[KB - 1], bl[KB - 1]);
     }
 
-    // Recomputed forward tile r: its MFMA chain, issued two regions before its result is used (two
-    // accumulators over alternate k-blocks halve the dependent-MFMA chain).
+    // Recomputed forward tile r: its MFMA chain (one accumulator: a dependent 16x16x32 MFMA chain issues back to
+    // back, MI355X_MICROARCH.md), issued two regions before its result is used.
     auto fwd_tile = [&](int r, f32x4 &a) {
         // the lo image through its own (opaque) base: its reads then also fit the 16-bit ds offset
         uint32_t fbl = fb + LO;
         asm volatile("" : "+v"(fbl));
-        f32x4 a2 = {0.0f, 0.0f, 0.0f, 0.0f};
-        a = a2;
+        a = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int kb = KLO; kb < KHI; ++kb) {
             const uint32_t a0 = fb + 8u * (2 * kb) + r * TILE, a1 = fb + 8u * (2 * kb + 1) + r * TILE;
@@ -196,21 +171,8 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
                     al[4 + k] = l1[k];
                 }
             }
-#if FCR_ABLATE == 1
-            if (((kb - KLO) & 1) == 0) a[0] += (float)ah[0] + (float)bh[kb][0];
-            else a2[0] += (float)ah[1] + (float)bh[kb][1];
-#else
-            if (tail) {
-                if (kOneAcc || ((kb - KLO) & 1) == 0) a = mfma16(ah, bh[kb], a);
-                else a2 = mfma16(ah, bh[kb], a2);
-            } else if (kOneAcc || ((kb - KLO) & 1) == 0) {
-                a = mma_p<LP>(ah, al, bh[kb], bl[kb], a);
-            } else {
-                a2 = mma_p<LP>(ah, al, bh[kb], bl[kb], a2);
-            }
-#endif
+            a = tail ? mfma16(ah, bh[kb], a) : mma_p<LP>(ah, al, bh[kb], bl[kb], a);
         }
-        if (!kOneAcc && KHI - KLO > 1) a += a2;
     };
     // pointwise + cell gradient of slot r from its pre-activations -> the 4 dgates as (scaled factor,
     // local derivative) pairs, multiplied inside the split (split8p): (dc s, dc/di), (dc s, dc/df),
@@ -219,20 +181,15 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     auto slot_grad = [&](int r, f32x4 a, float *va, float *vb) {
         f32x4 P;
         f32x2 Q;
-        if (OWN) lstm_point_grad_h<FIRST, CARRY>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], rec_h<HS>(ci.o, r), P, Q);
-        else lstm_point_grad<FIRST, CARRY>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], P, Q);
+        if (OWN) lstm_point_grad_h<FIRST>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], rec_h<HS>(ci.o, r), P, Q);
+        else lstm_point_grad<FIRST>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], P, Q);
         // torch LSTM semantics: dc = dc_carried + dh dh/dc; the carried dc of the cell below is dc f
         const float dcv = fmaf(dh[r], P[0], dc[r]);
         dc[r] = dcv * Q[1];
-        if (CARRY) {   // dh, dc already in S units; the g row's -1/2 is in Q[0] (dcdg_half)
-            va[0] = va[1] = va[2] = dcv;
-            va[3] = dh[r];
-        } else {
-            const float dcs = dcv * sg0;
-            va[0] = va[1] = dcs;
-            va[2] = dcv * sgg;
-            va[3] = dh[r] * sg0;
-        }
+        const float dcs = dcv * sg0;
+        va[0] = va[1] = dcs;
+        va[2] = dcv * sgg;
+        va[3] = dh[r] * sg0;
         vb[0] = P[2];
         vb[1] = P[3];
         vb[2] = Q[0];
@@ -246,14 +203,6 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     };
     // forward MFMAs of slot pair kbb into fa[.][0..1]
     auto fwd_pair = [&](int kbb, f32x4 (&fp)[2]) {
-#if FCR_ABLATE == 5   // diagnostic: the pre-activations loaded (one 16-B record per slot and lane, cycling
-        // through the wave's h slab) instead of recomputed — what a stored-pre-activation backward would cost
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-            if (2 * kbb + u < HS)
-                fp[u] = buf_ld4(nx.rh, lane * 16, (uint32_t)sp.t[6] + (uint32_t)((2 * kbb + u) * 1024));
-        return;
-#endif
 #pragma unroll
         for (int u = 0; u < 2; ++u)
             if (2 * kbb + u < HS) fwd_tile(2 * kbb + u, fp[u]);
@@ -290,42 +239,20 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
 #pragma unroll
         for (int r = 0; r < HS; ++r) {
             const float din = DIN ? ci.d[r >> 2][r & 3] : ext[r];
-            dh[r] = CARRY ? fmaf(din, ci.S, dh[r]) : dh[r] + din;
+            dh[r] = dh[r] + din;
             m = fmaxf(m, fabsf(dh[r]) + fabsf(dc[r]));
         }
         m = max_q(m);
-        if constexpr (CARRY) {
-            // keep S while the scaled bound m stays in [2^9, 2^14): every dgate is then below 2^16 (|dc/df| <=
-            // |c_{t-1}| / 4 <= 2.5, the other local derivatives <= 1) and far above f16's subnormals; else re-centre
-            // every lane of the wave at m in [2^12, 2^13), as the per-cell scale does (exact: powers of two)
-            const bool off = m >= 0x1p14f || (m < 0x1p9f && m > 0.0f);
-            if (__builtin_amdgcn_ballot_w64(off)) [[unlikely]] {
-                asm volatile("");   // a real branch: not if-converted into selects that run every cell
-                const int e = max(__builtin_amdgcn_frexp_expf(m), -100);   // m < 2^e
-                const float f = m > 0.0f ? __builtin_amdgcn_ldexpf(1.0f, 13 - e) : 1.0f;
-                const float fd = m > 0.0f ? __builtin_amdgcn_ldexpf(1.0f, e - 13) : 1.0f;
-#pragma unroll
-                for (int r = 0; r < HS; ++r) {
-                    dh[r] *= f;
-                    dc[r] *= f;
-                }
-                ci.S *= f;
-                ci.Sd *= fd;
-            }
-            down = ci.Sd * kInvNegLog2e;   // the product returns kappa S W^T dG: true units
-            up = sg0 = sgg = 0.0f;
-        } else {
-            const int e = max(__builtin_amdgcn_frexp_expf(m), -100);   // m < 2^e; all-zero -> e = 0
-            up = __builtin_amdgcn_ldexpf(1.0f, 13 - e);
-            down = __builtin_amdgcn_ldexpf(1.0f, e - 13);
-            sg0 = up * kInvNegLog2e;   // dgate scale of the i, f, o rows
-            sgg = sg0 * -0.5f;         // and of the g rows
-            if (DG) dgd = m > 0.0f ? down : 0.0f;
-        }
+        const int e = max(__builtin_amdgcn_frexp_expf(m), -100);   // m < 2^e; all-zero -> e = 0
+        up = __builtin_amdgcn_ldexpf(1.0f, 13 - e);
+        down = __builtin_amdgcn_ldexpf(1.0f, e - 13);
+        sg0 = up * kInvNegLog2e;   // dgate scale of the i, f, o rows
+        sgg = sg0 * -0.5f;         // and of the g rows
+        if (DG) dgd = m > 0.0f ? down : 0.0f;
     }
     // OWN_REG: the next cell (t - 1, same phase) owns h_{t-1}, whose record this cell has in ci.h: kept in registers
     // for it instead of re-read from the slab (an L2 miss by then)
-    constexpr bool OWN_REG = FCR_OWN_REG && NX_OWN && !FIRST;
+    constexpr bool OWN_REG = NX_OWN && !FIRST;
     f32x4 hkeep[Geo<HS>::HQ];
     if constexpr (OWN_REG) {
 #pragma unroll
@@ -348,9 +275,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
 #pragma unroll
     for (int kbb = 0; kbb < KBB; ++kbb) {
         sched_fence();
-#if FCR_BWD_LAUNDER
         asm volatile("" : "+v"(fb), "+v"(tb));
-#endif
         uint32_t tbl = tb + LO;   // lo image base (opaque: keeps the reads' offsets inside 16 bits)
         asm volatile("" : "+v"(tbl));
         const int cu = kbb & 1, nu = cu ^ 1;
@@ -388,9 +313,6 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
             // of the cell (all fragments live at once); naming the accumulator keeps block kb-1's
             // MFMAs ahead of this point (issued ~NB*3 MFMAs ago: no hazard wait)
             if (kbb > 0) asm volatile("" : "+v"(acc[tau]));
-#if FCR_ABLATE == 1
-            acc[tau][0] += (float)ah[0] + (float)gh[cu][0];
-#else
             if (!two && !LP) {
                 // half block (odd HS: its second slot is padding, k 4..7 of every group zero): the
                 // hi·hi and hi·lo products share ONE MFMA over k = [W_hi d_hi | W_hi d_lo], then lo·hi
@@ -404,7 +326,6 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
             } else {
                 acc[tau] = mma_p<LP>(ah, al, gh[cu], gl[cu], acc[tau]);
             }
-#endif
         }
         if (kbb + 1 < KBB) {
             dgate_block(kbb + 1, fa[(kbb + 1) % 3], gh[nu], gl[nu]);
@@ -422,10 +343,9 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     }
     sched_fence();
     const unsigned long long t2 = stamp_now();
-    const float dnh = CARRY ? kInvNegLog2e : down;   // the next cell's dh (CARRY: stays in S units)
     if (L0) {
 #pragma unroll
-        for (int s = 0; s < HS; ++s) dh[s] = acc[s >> 2][s & 3] * dnh;
+        for (int s = 0; s < HS; ++s) dh[s] = acc[s >> 2][s & 3] * down;
         dxq = acc[HS >> 2][HS & 3] * down;
         dx4 = acc[(HS + 1) >> 2][(HS + 1) & 3] * down;
     } else {
@@ -436,13 +356,9 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
 #pragma unroll
         for (int s = 0; s < HS; ++s) {
             dxo[s] = acc[s >> 2][s & 3] * down;
-            dh[s] = acc[(HS + s) >> 2][(HS + s) & 3] * dnh;
+            dh[s] = acc[(HS + s) >> 2][(HS + s) & 3] * down;
         }
     }
-#if FCR_ABLATE == 5
-    sp.t[6] += HS * 1024;
-    if (sp.t[6] + HS * 1024 > sp.t[7]) sp.t[6] = 0;
-#endif
     if (FCR_STAMP) {
         const unsigned long long t3 = stamp_now();
         sp.t[0] += t1 - t0;
@@ -542,12 +458,6 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         return n;
     };
     Stamps sp = {{0, 0, 0, 0, (unsigned long long)((threadIdx.x >> 8) & 1), 0, 0, 0}};
-#if FCR_ABLATE == 5
-    sp.t[7] = seq_sz * 16 / 1024 * 1024;   // the h slab's whole KiB: the diagnostic's loads wrap inside it
-#endif
-#if FCR_PRIO == 2   // diagnostic: static priority for the second-dispatched half (MI355X_MICROARCH.md item 4)
-    if ((threadIdx.x >> 8) & 1) __builtin_amdgcn_s_setprio(1);
-#endif
     const unsigned long long tk0 = stamp_now();
     CellIn<HS> ci;
     {
@@ -608,7 +518,6 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         const unsigned long long tw1 = stamp_now();
         if (!LP) {
             lds_fill<I1::BYTES, kBwdWaves>(lw, a.p.img[2]);
-            stagger();
         }
         if (FCR_STAMP) {
             const unsigned long long tw2 = stamp_now();
@@ -640,7 +549,6 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         const unsigned long long tw3 = stamp_now();
         if (!LP) {
             lds_fill<I1::BYTES, kBwdWaves>(lw, a.p.img[1]);
-            stagger();
         }
         if (FCR_STAMP) sp.t[7] += stamp_now() - tw3;
 #pragma unroll
@@ -659,7 +567,6 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         // ---- layer 0: dx -> window-row gradients ----
         if (!LP) {
             lds_fill<I0::BYTES, kBwdWaves>(lw, a.p.img[0]);
-            stagger();
         }
 #pragma unroll
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;

@@ -22,24 +22,8 @@ constexpr int kOut = 4;          // [y_dot, p1, p2, z]
 constexpr int kCtrlIn = 3;       // [y_dot, z, ref]
 constexpr int kMS = 13;          // controller hidden slots (units 4m+q), hidden <= 52
 constexpr int kFnpStride = 8;    // floats per (m, q) controller record: W0 W1 W2 b wout 0 0 0
-#ifndef FCR_ABLATE
-#define FCR_ABLATE 0   // diagnostic builds only (scripts/ablate.sh): 1 = no MFMAs, 2 = no cell pointwise,
-                       // 3 = no slab traffic (sequence loads return opaque registers, stores go)
-#endif
-#ifndef FCR_FWD_WAVES
-#define FCR_FWD_WAVES 8
-#endif
-constexpr int kFwdWaves = FCR_FWD_WAVES;  // waves per forward workgroup (8 = 2 per SIMD)
-#ifndef FCR_BWD_WAVES
-#define FCR_BWD_WAVES 8
-#endif
-constexpr int kBwdWaves = FCR_BWD_WAVES;   // waves per backward workgroup (8 = 2 per SIMD)
-// One accumulator per gate tile (a dependent 16x16x32 MFMA chain issues back to back, MI355X_MICROARCH.md)
-// instead of two over alternate k-blocks, whose final sum costs packed-f32 adds beside the MFMAs.
-#ifndef FCR_ONEACC
-#define FCR_ONEACC 1
-#endif
-constexpr bool kOneAcc = FCR_ONEACC;
+constexpr int kFwdWaves = 8;     // waves per forward workgroup (2 per SIMD)
+constexpr int kBwdWaves = 8;     // waves per backward workgroup (2 per SIMD)
 constexpr float kP1Max = 2.122366f;  // Functions.py:1411 (32e6 / p1 max_abs_)
 constexpr float kP2Max = 1.036233f;  // Functions.py:1411 (32e6 / p2 max_abs_)
 
@@ -115,46 +99,18 @@ __device__ __forceinline__ float hardtanh(float v) { return fminf(fmaxf(v, -1.0f
 __device__ __forceinline__ float sel4(int q, float a, float b, float c, float d) {
     return q == 0 ? a : (q == 1 ? b : (q == 2 ? c : d));
 }
-// Sum / max over the 4 lane groups that share one trajectory (lanes l, l^16, l^32, l^48). FCR_PERMLANE = 1:
-// gfx950's v_permlane16_swap / v_permlane32_swap (VALU half exchanges: with both operands the same value,
-// results [row0 row0 row2 row2] and [row1 row1 row3 row3] for 16-lane rows, [lo lo] and [hi hi] for halves),
-// so the reduction needs no LDS round trip; __shfl_xor is a ds_bpermute each. Same operands in the same
-// order as the xor form (commutative adds), so the results are bit for bit those of FCR_PERMLANE = 0 (GPU suite
-// green with it; the backward measured the same, +0.1..0.6 %, the swaps' hazard s_nops eat the LDS round trip:
-// off by default).
-#ifndef FCR_PERMLANE
-#define FCR_PERMLANE 0
-#endif
+// Sum / max over the 4 lane groups that share one trajectory (lanes l, l^16, l^32, l^48). (gfx950's
+// v_permlane16/32_swap form measured +0.1..0.6 % in the backward, round 3d: the swaps' hazard s_nops eat the LDS
+// round trip of the two ds_bpermutes.)
 template <bool MAX>
 __device__ __forceinline__ float reduce_q(float v) {
     auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : a + b; };
-#if FCR_PERMLANE
-    const unsigned u = __builtin_bit_cast(unsigned, v);
-    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
-    v = op(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
-    const unsigned w = __builtin_bit_cast(unsigned, v);
-    const auto s = __builtin_amdgcn_permlane32_swap(w, w, false, false);
-    return op(__builtin_bit_cast(float, (unsigned)s[0]), __builtin_bit_cast(float, (unsigned)s[1]));
-#else
     v = op(v, __shfl_xor(v, 16));
     return op(v, __shfl_xor(v, 32));
-#endif
 }
 __device__ __forceinline__ float xor_sum_q(float v) { return reduce_q<false>(v); }
 __device__ __forceinline__ float max_q(float v) { return reduce_q<true>(v); }
 __device__ __forceinline__ void sched_fence() { __builtin_amdgcn_sched_barrier(0); }
-
-// After a workgroup barrier every wave runs the same instruction stream in lockstep, so the two
-// waves sharing a SIMD stall at the same points. Delaying the second half of the workgroup by
-// FCR_STAGGER x 64 cycles offsets them (MI355X_MICROARCH.md, "try a stagger").
-#ifndef FCR_STAGGER
-#define FCR_STAGGER 0
-#endif
-__device__ __forceinline__ void stagger() {
-#if FCR_STAGGER > 0
-    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= (int)(blockDim.x >> 7)) __builtin_amdgcn_s_sleep(FCR_STAGGER);
-#endif
-}
 
 // An LDS pointer the compiler cannot see through: stops it from hoisting loop-invariant LDS reads
 // (e.g. the 65 controller parameters) out of the window loop into registers it does not have.
@@ -178,28 +134,15 @@ __device__ __forceinline__ f32x4 lds_quad(const float *lw, int idx, int lane) {
     return *reinterpret_cast<const f32x4 *>(hi + (byte - kSplit));
 }
 
-// FCR_ABLATE == 3: a register the compiler cannot see through, in place of a load
-__device__ __forceinline__ float ablate_val(uint32_t seed) {
-    float v;   // values in [-1, 1) like the h and c they replace (operand-dependent MFMA power)
-    asm volatile("v_cvt_f32_ubyte0 %0, %1" : "=v"(v) : "v"(seed * 2654435761u));
-    return fmaf(v, 1.0f / 128.0f, -1.0f);
-}
-
 // Raw buffer loads through a wave-uniform descriptor (base and size from SGPR values only, so no
 // waterfall loop): the per-lane part is a 32-bit voffset, the rest an SGPR soffset.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void *base, size_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, (int)(uint32_t)bytes, 0x00020000);
 }
 __device__ __forceinline__ f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-#if FCR_ABLATE == 3
-    return f32x4{ablate_val(voff), ablate_val(voff + soff), ablate_val(voff ^ soff), ablate_val(voff - soff)};
-#endif
     return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0));
 }
 __device__ __forceinline__ f32x2 buf_ld2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-#if FCR_ABLATE == 3
-    return f32x2{ablate_val(voff), ablate_val(voff + soff)};
-#endif
     return __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, 0));
 }
 // Quad k of a unit-slot vector with only its first n (1..4) slots loaded: a padding lane of a partial
@@ -207,9 +150,6 @@ __device__ __forceinline__ f32x2 buf_ld2(__amdgpu_buffer_rsrc_t r, uint32_t voff
 template <int n>
 __device__ __forceinline__ f32x4 buf_ldq(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     f32x4 q = {0.0f, 0.0f, 0.0f, 0.0f};
-#if FCR_ABLATE == 3
-    return buf_ld4(r, voff, soff);
-#endif
     if (n == 4) {
         q = buf_ld4(r, voff, soff);
     } else if (n == 3) {
@@ -236,10 +176,6 @@ template <int HS, int k>
 constexpr uint32_t quad_soff() { return (uint32_t)k * kWave * 16; }
 
 __device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, f32x2 v) {
-#if FCR_ABLATE == 3
-    asm volatile("" ::"v"(v[0]), "v"(v[1]));
-    return;
-#endif
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int, v), r,
                                           (int)voff, (int)soff, 0);
 }
@@ -281,10 +217,6 @@ __device__ __forceinline__ void lds_fill(float *lw, const float *__restrict__ sr
 // the chip holds). A cell is Geo<HS>::QC quads; ceil(HS/4) memory instructions per cell.
 template <int HS>
 __device__ __forceinline__ void store_quads(f32x4 *dst, const float (&v)[HS], int lane) {
-#if FCR_ABLATE == 3
-    for (int k = 0; k < HS; ++k) asm volatile("" ::"v"(v[k]));
-    return;
-#endif
     constexpr int FQ = HS / 4, TS = HS % 4;
 #pragma unroll
     for (int k = 0; k < FQ; ++k) dst[k * kWave + lane] = f32x4{v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]};
@@ -302,10 +234,6 @@ __device__ __forceinline__ void store_quads(f32x4 *dst, const float (&v)[HS], in
 }
 template <int HS>
 __device__ __forceinline__ void load_quads(float (&v)[HS], const f32x4 *src, int lane) {
-#if FCR_ABLATE == 3
-    for (int k = 0; k < HS; ++k) v[k] = ablate_val(lane + 64 * k + (uint32_t)(uintptr_t)src);
-    return;
-#endif
     constexpr int FQ = HS / 4, TS = HS % 4;
 #pragma unroll
     for (int k = 0; k < FQ; ++k) {
@@ -322,11 +250,6 @@ __device__ __forceinline__ void load_quads(float (&v)[HS], const f32x4 *src, int
 // quad_voff, the cell's offset an SGPR soffset — no per-access 64-bit address arithmetic
 template <int HS, int k = 0>
 __device__ __forceinline__ void buf_store_quads(__amdgpu_buffer_rsrc_t r, uint32_t off, const float (&v)[HS], int lane) {
-#if FCR_ABLATE == 3
-    if constexpr (k == 0)
-        for (int e = 0; e < HS; ++e) asm volatile("" ::"v"(v[e]));
-    return;
-#endif
     if constexpr (k < Geo<HS>::HQ) {
         constexpr int n = quad_n<HS, k>();
         const uint32_t vo = quad_voff<HS, k>(lane), so = off + quad_soff<HS, k>();

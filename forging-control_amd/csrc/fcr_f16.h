@@ -71,15 +71,10 @@ __device__ __forceinline__ f16x8 lds_frag16(const float *lw, int idx, int lane) 
     return __builtin_bit_cast(f16x8, lds_quad(lw, idx, lane));
 }
 
-// The splits below write f16 halves with v_fma_mixlo/mixhi_f16. FCR_MIX_ASM = 1 emits them as inline asm
-// (2 instructions per value); the compiler's hazard recognizer does not look inside inline asm, so an
-// asm write may land on a VGPR that an MFMA issued just before still reads as its A/B operand (a WAR
-// hazard the compiler pads with s_nop for its own instructions). FCR_MIX_ASM = 0 writes the same
-// arithmetic as (_Float16)fmaf(a, b, c), which the backend selects as v_fma_mix* (~2.5 instructions per
-// value) with the hazard handled.
-#ifndef FCR_MIX_ASM
-#define FCR_MIX_ASM 0
-#endif
+// The splits below are plain (_Float16)fmaf(a, b, c), which the backend selects as v_fma_mix* (~2.5
+// instructions per value) with the MFMA operand hazards padded. (An inline-asm v_fma_mixlo/mixhi pair is 2, but
+// the hazard recognizer does not look inside inline asm: an asm write of a VGPR an MFMA issued just before still
+// reads went out unpadded, DESIGN.md §2 "Inline asm and MFMA hazards".)
 // (hi, lo) of the products a·b for two values; hi = f16(a·b), lo = f16(a·b - hi), the product exact in the fma
 __device__ __forceinline__ void mix_pair(float a0, float b0, float a1, float b1, unsigned &hp, unsigned &lp) {
     typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
@@ -109,30 +104,18 @@ __device__ __forceinline__ void split8(const float (&v)[8], f16x8 &hi, f16x8 &lo
     }
 }
 
-// s·v -> (hi, lo) halves, 8 at a time, on the mixed-precision FMA: per pair of values one
-// v_fma_mixlo/mixhi pair forms hi = f16(s·v) straight into a packed register and one more forms
-// lo = f16(s·v - hi) (the product is exact inside the fma) — 2 instructions per value, scale included,
-// against ~3.5 for the scalar conversions the compiler emits for split8.
+// s·v -> (hi, lo) halves, 8 at a time, on the mixed-precision FMA: hi = f16(s·v) goes straight into a packed
+// register and lo = f16(s·v - hi) (the product is exact inside the fma) — ~2.5 instructions per value, scale
+// included, against ~3.5 for the scalar conversions the compiler emits for split8.
 __device__ __forceinline__ void split8s(const float (&v)[8], float s, f16x8 &hi, f16x8 &lo) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     u32x4 h, l;
-#if !FCR_MIX_ASM
     // a constant s = 1 would fold the fma away and lose the v_fma_mix form (cvt/sub/cvt instead)
     asm("" : "+v"(s));
-#endif
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         unsigned hp, lp;
-#if FCR_MIX_ASM
-        asm("v_fma_mixlo_f16 %0, %1, %2, 0\n\t"
-            "v_fma_mixhi_f16 %0, %3, %2, 0"
-            : "=&v"(hp) : "v"(v[2 * p]), "v"(s), "v"(v[2 * p + 1]));
-        asm("v_fma_mixlo_f16 %0, %1, %2, -%4 op_sel_hi:[0,0,1]\n\t"
-            "v_fma_mixhi_f16 %0, %3, %2, -%4 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
-            : "=&v"(lp) : "v"(v[2 * p]), "v"(s), "v"(v[2 * p + 1]), "v"(hp));
-#else
         mix_pair(v[2 * p], s, v[2 * p + 1], s, hp, lp);
-#endif
         h[p] = hp;
         l[p] = lp;
     }
@@ -146,15 +129,7 @@ __device__ __forceinline__ void cvt8s(const float (&v)[8], float s, f16x8 &hi) {
     u32x4 h;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-#if FCR_MIX_ASM
-        unsigned hp;
-        asm("v_fma_mixlo_f16 %0, %1, %2, 0\n\t"
-            "v_fma_mixhi_f16 %0, %3, %2, 0"
-            : "=&v"(hp) : "v"(v[2 * p]), "v"(s), "v"(v[2 * p + 1]));
-        h[p] = hp;
-#else
         h[p] = mix_hi(v[2 * p], s, v[2 * p + 1], s);
-#endif
     }
     hi = __builtin_bit_cast(f16x8, h);
 }
@@ -168,16 +143,7 @@ __device__ __forceinline__ void split8p(const float (&a)[8], const float (&b)[8]
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         unsigned hp, lp;
-#if FCR_MIX_ASM
-        asm("v_fma_mixlo_f16 %0, %1, %2, 0\n\t"
-            "v_fma_mixhi_f16 %0, %3, %4, 0"
-            : "=&v"(hp) : "v"(a[2 * p]), "v"(b[2 * p]), "v"(a[2 * p + 1]), "v"(b[2 * p + 1]));
-        asm("v_fma_mixlo_f16 %0, %1, %2, -%5 op_sel_hi:[0,0,1]\n\t"
-            "v_fma_mixhi_f16 %0, %3, %4, -%5 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
-            : "=&v"(lp) : "v"(a[2 * p]), "v"(b[2 * p]), "v"(a[2 * p + 1]), "v"(b[2 * p + 1]), "v"(hp));
-#else
         mix_pair(a[2 * p], b[2 * p], a[2 * p + 1], b[2 * p + 1], hp, lp);
-#endif
         h[p] = hp;
         l[p] = lp;
     }
@@ -189,15 +155,7 @@ __device__ __forceinline__ void cvt8p(const float (&a)[8], const float (&b)[8], 
     u32x4 h;
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
-#if FCR_MIX_ASM
-        unsigned hp;
-        asm("v_fma_mixlo_f16 %0, %1, %2, 0\n\t"
-            "v_fma_mixhi_f16 %0, %3, %4, 0"
-            : "=&v"(hp) : "v"(a[2 * p]), "v"(b[2 * p]), "v"(a[2 * p + 1]), "v"(b[2 * p + 1]));
-        h[p] = hp;
-#else
         h[p] = mix_hi(a[2 * p], b[2 * p], a[2 * p + 1], b[2 * p + 1]);
-#endif
     }
     hi = __builtin_bit_cast(f16x8, h);
 }
@@ -375,11 +333,6 @@ __device__ __forceinline__ float lstm_h(float c, float eo) {
 }
 template <bool FIRST>
 __device__ __forceinline__ void lstm_point(f32x4 a, float c_prev, float &c, float &h) {
-#if FCR_ABLATE == 2   // diagnostic: the cell pointwise goes
-    c = a[0] + c_prev;
-    h = a[1];
-    return;
-#endif
     c = lstm_gi_c<FIRST>(a, c_prev);
     h = lstm_h(c, __builtin_amdgcn_exp2f(a[3]));
 }
@@ -387,45 +340,14 @@ __device__ __forceinline__ void lstm_point(f32x4 a, float c_prev, float &c, floa
 // tile pair's pointwise over the next pair's MFMA regions: A = gates and c (and e_o), B = h from (c, e_o)
 template <bool FIRST>
 __device__ __forceinline__ void lstm_point_a(f32x4 a, float c_prev, float &c, float &eo) {
-#if FCR_ABLATE == 2
-    c = a[0] + c_prev;
-    eo = a[1];
-    return;
-#endif
     c = lstm_gi_c<FIRST>(a, c_prev);
     eo = __builtin_amdgcn_exp2f(a[3]);
 }
 __device__ __forceinline__ void lstm_point_b(float c, float eo, float &h) {
-#if FCR_ABLATE == 2
-    h = eo;
-    return;
-#endif
     h = lstm_h(c, eo);
 }
-// -0.5 (i - gi g) = 0.5 (gi g - i): the g row's dc/dg with the -1/2 of its exp2 pre-scale (2 log2e against -log2e for
-// i, f, o; fcr_bwd.h, carried scale) folded in. (A v_fma_f32 with the div:2 output modifier would do it in one
-// instruction, but the hardware ignores omod while the kernel runs in IEEE mode, the compute default: measured, the
-// g rows' dgates came out doubled. FCR_OMOD = 1 keeps that form for a build without IEEE mode.)
-#ifndef FCR_OMOD
-#define FCR_OMOD 0
-#endif
-__device__ __forceinline__ float dcdg_half(float gi, float g, float i) {
-#if FCR_OMOD
-    float r;
-    asm("v_fma_f32 %0, %1, %2, -%3 div:2" : "=v"(r) : "v"(gi), "v"(g), "v"(i));
-    return r;
-#else
-    return 0.5f * fmaf(gi, g, -i);
-#endif
-}
-
-template <bool FIRST, bool GH = false>
+template <bool FIRST>
 __device__ __forceinline__ void lstm_point_grad(f32x4 a, float c_prev, f32x4 &P, f32x2 &Q) {
-#if FCR_ABLATE == 2
-    P = a;
-    Q = f32x2{c_prev, a[0]};
-    return;
-#endif
     const float i = sigm_pre(a[0]);
     const float f = sigm_pre(a[1]);
     const float g = tanh_pre(a[2]);
@@ -436,7 +358,7 @@ __device__ __forceinline__ void lstm_point_grad(f32x4 a, float c_prev, f32x4 &P,
     const float tc = tanh_f(cn);
     const float h = o * tc;
     P = f32x4{fmaf(-h, tc, o), fmaf(-h, o, h), fmaf(-gi, i, gi), fmaf(-cf, f, cf)};
-    Q = f32x2{GH ? dcdg_half(gi, g, i) : fmaf(-gi, g, i), f};
+    Q = f32x2{fmaf(-gi, g, i), f};
 }
 
 // h of unit slot s from its split record (split_rec: hi at half s, lo at half HS + s of the record words):
@@ -462,8 +384,7 @@ __device__ __forceinline__ float rec_h(const f32x4 *rec, int s) {
 // instead of re-evaluated (exp2, rcp and three VALU): the same six local derivatives. h is the forward's h_t
 // as its split record holds it (fp32-accurate; f16-subnormal h only perturbs P by the record's absolute
 // 2^-25, below the gradients' fp32 level).
-// GH: Q[0] = -dc/dg / 2 (dcdg_half) instead of dc/dg
-template <bool FIRST, bool GH = false>
+template <bool FIRST>
 __device__ __forceinline__ void lstm_point_grad_h(f32x4 a, float c_prev, float h, f32x4 &P, f32x2 &Q) {
     const float i = sigm_pre(a[0]);
     const float f = sigm_pre(a[1]);
@@ -476,7 +397,7 @@ __device__ __forceinline__ void lstm_point_grad_h(f32x4 a, float c_prev, float h
     const float cf = FIRST ? 0.0f : f * c_prev;
     const float tc = h * d_o;
     P = f32x4{fmaf(-h, tc, o), fmaf(-h, o, h), fmaf(-gi, i, gi), fmaf(-cf, f, cf)};
-    Q = f32x2{GH ? dcdg_half(gi, g, i) : fmaf(-gi, g, i), f};
+    Q = f32x2{fmaf(-gi, g, i), f};
 }
 
 // host-side geometry of the forward fragment blocks (bytes), matching Geo16

@@ -25,54 +25,20 @@ __device__ __forceinline__ void rot_left(float (&w)[kL]) {
 // column 4 in lane group 0); otherwise x = the split record of the layer-below h_t. hp = the split
 // record of h_{t-1} (fcr_f16.h, split_rec); hout = this cell's h (fp32). FIRST: t = 0 (h_{t-1} = 0: those
 // k-blocks are skipped). The B operands are split once per cell and shared by all tiles. Tiles go in
-// pairs, each with two accumulators over alternate k-blocks: four independent MFMA chains per
-// scheduling region (one region per k-block, the next block's four fragment reads in flight), and the
-// cell update of the previous pair issued in the first region of the next, beside its MFMAs.
-#ifndef FCR_FWD_PRIO
-#define FCR_FWD_PRIO 1
-#endif
-#ifndef FCR_FWD_SPREAD
-#define FCR_FWD_SPREAD 1   // spread each tile pair's pointwise over the next pair's MFMA regions
-#endif
-#ifndef FCR_FWD_RDFIRST
-#define FCR_FWD_RDFIRST 0
-#endif
-// FCR_FWD_TM = 1: layers 0 and 1 run time-major in one phase (layer 1 takes layer 0's h_t from registers instead of
-// re-reading it from the slab: -1.37 GB of HBM reads per launch at B = 65 536, and no prefetch loads or waits for
-// them); layer 2 keeps its own phase. Measured (profiles/round3d_fwd_tm_ab.log, one process, both orders): forward
-// 2.67 -> 2.52 and 2.61 -> 2.47 ms, bit-identical; f16 mode at B = 262 144 8.41 -> 8.29 ms
-#ifndef FCR_FWD_TM
-#define FCR_FWD_TM 1
-#endif
-
-// Issue-priority pacing of the two waves that share a SIMD (waves w and w+4 of the workgroup).
-//   FCR_FWD_PRIO 1: alternate the higher priority cell by cell;
-//   FCR_FWD_PRIO 2: the younger wave always has it;
-//   FCR_FWD_PRIO 3: the wave that is AHEAD of its partner (cells done, published in LDS) yields it.
-// Every layer phase ends at a workgroup barrier (the fragment refill), so a wave that runs ahead only
-// waits there while its partner runs alone on the SIMD.
+// pairs, one accumulator each (a dependent 16x16x32 MFMA chain issues back to back): one scheduling region
+// per k-block with the next block's fragment reads in flight, and the previous pair's cell update spread over
+// this pair's regions beside its MFMAs.
+// Issue-priority pacing of the two waves that share a SIMD (waves w and w+4 of the workgroup): they alternate the
+// higher priority cell by cell. Every layer phase ends at a workgroup barrier (the fragment refill), so a wave that
+// runs ahead only waits there while its partner runs alone on the SIMD. (Giving it always to the younger wave, or
+// taking it from the wave that is ahead of its partner by published progress, measured 3 % slower: DESIGN.md §6.)
 struct Pace {
     unsigned turn;
-    volatile int *prog;   // [8] per-wave cell counters (FCR_FWD_PRIO 3)
-    int me, cnt, other;
 };
 __device__ __forceinline__ void pace_cell(Pace &p) {
-#if FCR_FWD_PRIO == 1
     if (p.turn & 1) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
     p.turn ^= 1;
-#elif FCR_FWD_PRIO == 2
-    if (p.me >= 4) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
-#elif FCR_FWD_PRIO == 3
-    ++p.cnt;
-    if (p.cnt > p.other) __builtin_amdgcn_s_setprio(0);
-    else __builtin_amdgcn_s_setprio(1);
-    p.prog[p.me] = p.cnt;
-    p.other = __builtin_amdgcn_readfirstlane(p.prog[p.me ^ 4]);   // used at the next cell
-#else
-    (void)p;
-#endif
 }
 
 // R0, R1: the tile (unit slot) range this wave computes — the whole cell by default; the small-batch
@@ -110,9 +76,7 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
     for (int p = P0; p < P1; ++p) {
         const int r0 = 2 * p, r1 = 2 * p + 1;
         const bool two = r1 < R1;
-        f32x4 acc[2][2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) acc[u][0] = acc[u][1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        f32x4 acc[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
 #pragma unroll
         for (int kb = KLO; kb < KHI; ++kb) {
             sched_fence();
@@ -125,26 +89,14 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
                 rd(r0 + 2, KLO, nh[0], nl[0]);
                 if (r1 + 2 < R1) rd(r1 + 2, KLO, nh[1], nl[1]);
             }
-#if FCR_FWD_RDFIRST
-            // the next region's reads issue ahead of this region's MFMAs (otherwise the scheduler places them
-            // behind most of the chain, and the next region opens on their LDS latency)
-            sched_fence();
-#endif
-            const int ch = kOneAcc ? 0 : (kb - KLO) & 1;
-#if FCR_ABLATE == 1   // diagnostic: the fragment reads and operands stay, the MFMAs go
-            acc[0][ch][0] += (float)ah[0][0] + (float)bh[kb][0];
-            if (two) acc[1][ch][0] += (float)ah[1][0] + (float)bh[kb][1];
-#else
             if (TAIL && kb == KB - 1) {
-                acc[0][ch] = mfma16(ah[0], bh[kb], acc[0][ch]);
-                if (two) acc[1][ch] = mfma16(ah[1], bh[kb], acc[1][ch]);
+                acc[0] = mfma16(ah[0], bh[kb], acc[0]);
+                if (two) acc[1] = mfma16(ah[1], bh[kb], acc[1]);
             } else {
-                acc[0][ch] = mma_p<LP>(ah[0], al[0], bh[kb], bl[kb], acc[0][ch]);
-                if (two) acc[1][ch] = mma_p<LP>(ah[1], al[1], bh[kb], bl[kb], acc[1][ch]);
+                acc[0] = mma_p<LP>(ah[0], al[0], bh[kb], bl[kb], acc[0]);
+                if (two) acc[1] = mma_p<LP>(ah[1], al[1], bh[kb], bl[kb], acc[1]);
             }
-#endif
             if (p > P0) {
-#if FCR_FWD_SPREAD
                 // the previous pair's pointwise, spread over this pair's regions beside its MFMAs
                 // (R >= 3: gates of slot r0 | gates of slot r1 | both h; R = 2: both gates | both h)
                 const int qr = kb - KLO;
@@ -156,12 +108,6 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
                     lstm_point_b(c[r0 - 2], po[0], hout[r0 - 2]);
                     lstm_point_b(c[r1 - 2], po[1], hout[r1 - 2]);
                 }
-#else
-                if (kb == KLO) {
-                    lstm_point<FIRST>(prev[0], c[r0 - 2], c[r0 - 2], hout[r0 - 2]);
-                    lstm_point<FIRST>(prev[1], c[r1 - 2], c[r1 - 2], hout[r1 - 2]);
-                }
-#endif
             }
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
@@ -169,8 +115,8 @@ __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lan
                 al[u] = nl[u];
             }
         }
-        prev[0] = kOneAcc ? acc[0][0] : acc[0][0] + acc[0][1];
-        prev[1] = kOneAcc ? acc[1][0] : acc[1][0] + acc[1][1];
+        prev[0] = acc[0];
+        prev[1] = acc[1];
     }
     sched_fence();
     lstm_point<FIRST>(prev[0], c[2 * P1 - 2], c[2 * P1 - 2], hout[2 * P1 - 2]);
@@ -244,20 +190,9 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
     const __amdgpu_buffer_rsrc_t rc = wave_rsrc(a.cseq + wseq, (size_t)N * kLayers * kL * qcell * 16);
     const __amdgpu_buffer_rsrc_t rx = wave_rsrc(a.xw + (size_t)wave * N * kL * kWave, (size_t)N * kL * kWave * 8);
 
-    unsigned long long st_fill = 0, st_l0 = 0, st_l12 = 0, st_head = 0, st_drain = 0, st_skew1 = 0, st_dma = 0;
+    unsigned long long st_fill = 0, st_l0 = 0, st_l2 = 0, st_head = 0;
     Pace turn;
     turn.turn = (threadIdx.x >> 8) & 1;   // waves w and w+4 share a SIMD: start out of phase
-    turn.me = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    turn.cnt = turn.other = 0;
-#if FCR_FWD_PRIO == 3
-    // (diagnostic only: a static __shared__ array shifts the dynamic LDS base, which the b128 fragment
-    // reads need 16-B aligned — 32 B keeps it aligned)
-    __shared__ __attribute__((aligned(16))) int prog[kFwdWaves];
-    turn.prog = prog;
-    if (lane == 0) prog[turn.me] = 0;
-#else
-    turn.prog = nullptr;
-#endif
     const unsigned long long st_k0 = fstamp();
     for (int j = 0; j < N; ++j) {
         const unsigned long long st_w0 = fstamp();
@@ -283,19 +218,13 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
 #define SEQ_O(l, t) (oj + (uint32_t)(((l) * kL + (t)) * qcell * 16))
         const unsigned long long st_w1 = fstamp();
         st_head += st_w1 - st_w0;
-#if FCR_FWD_TM
         // ---- layers 0 and 1 together, time-major (Functions.py:374): layer 1's input h_t leaves layer 0's cell
         // already split in registers, so the slab holds it only for the backward; layer 1's fragments sit beside
         // the resident layer 0 for the phase, layer 2's replace them after it ----
         {
             const unsigned long long st_f0 = fstamp();
-            if (!LP) {
-                lds_fill<G::FA1 * 4, kFwdWaves>(lw, a.p.fa[1]);   // its first barrier also publishes the resident blocks
-                stagger();
-            } else if (j == 0) {
-                __syncthreads();   // f16 mode: every layer resident, never refilled
-                stagger();
-            }
+            if (!LP) lds_fill<G::FA1 * 4, kFwdWaves>(lw, a.p.fa[1]);   // its first barrier also publishes the resident blocks
+            else if (j == 0) __syncthreads();   // f16 mode: every layer resident, never refilled
             const unsigned long long st_f1 = fstamp();
             st_fill += st_f1 - st_f0;
             const float *lw1 = LP ? lwl[1] : lw;
@@ -309,7 +238,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
                 split_rec<HS>(hout, hp);
                 if (STORE) {
                     buf_store_quads<HS>(rh, SEQ_O(0, 0), hp, lane);
-                    if (FCR_ABLATE != 3) buf_st2(rx, lane * 8, (uint32_t)(j * kL * kWave * 8), f32x2{x0, x1});
+                    buf_st2(rx, lane * 8, (uint32_t)(j * kL * kWave * 8), f32x2{x0, x1});
                     buf_store_quads<HS>(rc, SEQ_O(0, 0), c, lane);
                 }
                 fwd16_cell<HS, false, true, LP>(lw1, lane, 0.0f, 0.0f, hp, h1, c1, hout, turn);
@@ -333,7 +262,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
                 split_rec<HS>(hout, hp);
                 if (STORE) {
                     buf_store_quads<HS>(rh, SEQ_O(0, t), hp, lane);
-                    if (FCR_ABLATE != 3) buf_st2(rx, lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{x0, x1});
+                    buf_st2(rx, lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{x0, x1});
                     if (t + 1 < kL) buf_store_quads<HS>(rc, SEQ_O(0, t), c, lane);   // c_9 is never a c_{t-1}
                 }
                 fwd16_cell<HS, false, false, LP>(lw1, lane, 0.0f, 0.0f, hp, h1, c1, hout, turn);
@@ -357,12 +286,10 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
         if constexpr (!LP) {
             constexpr int l = 2;
             const unsigned long long st_f0 = fstamp();
-            if (!LP) {
-                lds_fill<G::FA1 * 4, kFwdWaves>(lw, a.p.fa[l]);
-                stagger();
-            }
-            const float *lwc = LP ? lwl[l] : lw;
-            st_fill += fstamp() - st_f0;
+            lds_fill<G::FA1 * 4, kFwdWaves>(lw, a.p.fa[l]);
+            const float *lwc = lw;
+            const unsigned long long st_f1 = fstamp();
+            st_fill += st_f1 - st_f0;
             buf_load_quads<HS>(xc, rh, SEQ_O(l - 1, 0), lane);
             buf_load_quads<HS>(xn, rh, SEQ_O(l - 1, 1), lane);
             fwd16_cell<HS, false, true, LP>(lwc, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
@@ -383,93 +310,8 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
 #pragma unroll
                 for (int r = 0; r < HS; ++r) xc[r] = xn[r];
             }
+            st_l2 += fstamp() - st_f1;
         }
-#else
-        // ---- layer 0 over the window (Functions.py:374) ----
-        if (j == 0) {
-            __syncthreads();   // resident blocks are in place — layer 0 (and in f16 mode every layer) never refills
-            stagger();
-        }
-        {
-            const float x0 = w0[0], x1 = w1[0];
-            rot_left(w0);
-            rot_left(w1);
-            fwd16_cell<HS, true, true, LP>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
-            split_rec<HS>(hout, hp);
-            buf_store_quads<HS>(rh, SEQ_O(0, 0), hp, lane);
-            if (STORE) {
-                if (FCR_ABLATE != 3) buf_st2(rx, lane * 8, (uint32_t)(j * kL * kWave * 8), f32x2{x0, x1});
-                buf_store_quads<HS>(rc, SEQ_O(0, 0), c, lane);
-            }
-        }
-        for (int t = 1; t < kL; ++t) {
-            const float x0 = w0[0], x1 = w1[0];
-            rot_left(w0);
-            rot_left(w1);
-            fwd16_cell<HS, true, false, LP>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
-            split_rec<HS>(hout, hp);
-            buf_store_quads<HS>(rh, SEQ_O(0, t), hp, lane);
-            if (STORE) {
-                if (FCR_ABLATE != 3) buf_st2(rx, lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{x0, x1});
-                if (t + 1 < kL) buf_store_quads<HS>(rc, SEQ_O(0, t), c, lane);   // c_9 is never a c_{t-1}
-            }
-        }
-        // ---- layers 1, 2: input sequence streamed back from the slab, one cell ahead ----
-#pragma unroll
-        for (int l = 1; l < kLayers; ++l) {
-            const bool keep_h = l == 1 || STORE;   // layer 2's h_t is only the backward's h_{t-1}
-            const unsigned long long st_f0 = fstamp();
-            if (l == 1) st_l0 += st_f0 - st_w1;
-            if (!LP) {
-#if FCR_STAMP   // diagnostic: split the refill into store drain, barrier skew, DMA, barrier skew
-                const unsigned long long s0 = fstamp();
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                const unsigned long long s1 = fstamp();
-                __builtin_amdgcn_s_barrier();
-                const unsigned long long s2 = fstamp();
-                {
-                    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-                    for (int c = wv; c < G::FA1 * 4 / 1024; c += kFwdWaves)
-                        __builtin_amdgcn_global_load_lds(
-                            (const __attribute__((address_space(1))) void *)((const char *)a.p.fa[l] + c * 1024 + lane * 16),
-                            (__attribute__((address_space(3))) void *)((__attribute__((address_space(3))) char *)lw + c * 1024), 16, 0, 0);
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                const unsigned long long s3 = fstamp();
-                __builtin_amdgcn_s_barrier();
-                st_drain += s1 - s0;
-                st_skew1 += s2 - s1;
-                st_dma += s3 - s2;
-#else
-                lds_fill<G::FA1 * 4, kFwdWaves>(lw, a.p.fa[l]);
-#endif
-                stagger();
-            }
-            const float *lwc = LP ? lwl[l] : lw;
-            const unsigned long long st_f1 = fstamp();
-            st_fill += st_f1 - st_f0;
-            buf_load_quads<HS>(xc, rh, SEQ_O(l - 1, 0), lane);
-            buf_load_quads<HS>(xn, rh, SEQ_O(l - 1, 1), lane);
-            fwd16_cell<HS, false, true, LP>(lwc, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
-            split_rec<HS>(hout, hp);
-            if (keep_h) buf_store_quads<HS>(rh, SEQ_O(l, 0), hp, lane);
-            if (STORE) buf_store_quads<HS>(rc, SEQ_O(l, 0), c, lane);
-#pragma unroll
-            for (int r = 0; r < HS; ++r) xc[r] = xn[r];
-#pragma unroll 3
-            for (int t = 1; t < kL; ++t) {
-                buf_load_quads<HS>(xn, rh, SEQ_O(l - 1, t + 1 < kL ? t + 1 : t), lane);
-                fwd16_cell<HS, false, false, LP>(lwc, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
-                if (!(l == 2 && t + 1 == kL)) {   // h_9 of layer 2 only feeds the readout (fp32 hout)
-                    split_rec<HS>(hout, hp);
-                    if (keep_h) buf_store_quads<HS>(rh, SEQ_O(l, t), hp, lane);
-                }
-                if (STORE && t + 1 < kL) buf_store_quads<HS>(rc, SEQ_O(l, t), c, lane);
-#pragma unroll
-                for (int r = 0; r < HS; ++r) xc[r] = xn[r];
-            }
-        }
-#endif
 #undef SEQ_O
         // ---- readout fc(h_9 of layer 2) (Functions.py:377) ----
         float xo[kOut];
@@ -517,11 +359,9 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
         o[0] = st_head;
         o[1] = st_l0;
         o[2] = st_fill;
-        o[3] = st_l12;
+        o[3] = st_l2;
         o[4] = fstamp() - st_k0;
-        o[5] = st_drain;
-        o[6] = st_skew1;
-        o[7] = st_dma;
+        o[5] = o[6] = o[7] = 0;
     }
 #endif
 }

@@ -191,9 +191,6 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
     f32x2 *xw_wave = a.xw + (size_t)grp * N * kL * kWave;
     Pace turn;
     turn.turn = 0;
-    turn.me = w;
-    turn.cnt = turn.other = 0;
-    turn.prog = nullptr;
     unsigned long long sc[6] = {0, 0, 0, 0, 0, 0};   // FCR_STAMP: cells, exchanges, refills, count, head+readout, refill+first load
     const unsigned long long sk0 = fstamp();
     __syncthreads();

@@ -83,11 +83,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void sur_fwd_kern
 #define SEQ_O(l, t) ((uint32_t)(((l) * kL + (t)) * qcell * 16))
     Pace turn;
     turn.turn = (threadIdx.x >> 8) & 1;
-    turn.me = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    turn.cnt = turn.other = 0;
-    turn.prog = nullptr;
     __syncthreads();
-    stagger();
     // ---- layer 0 (Model_NN/Functions.py:327) ----
     {
         const float x0 = w0[0], x1 = w1[0];
@@ -117,7 +113,6 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void sur_fwd_kern
 #pragma unroll
     for (int l = 1; l < kLayers; ++l) {
         lds_fill<G::FA1 * 4, kFwdWaves>(lw, a.p.fa[l]);
-        stagger();
         buf_load_quads<HS>(xc, rh, SEQ_O(l - 1, 0), lane);
         buf_load_quads<HS>(xn, rh, SEQ_O(l - 1, 1), lane);
         fwd16_cell<HS, false, true, false>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
@@ -233,7 +228,6 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void sur_bwd_kern
     float unused0, unused1;
     // ---- layer 2 ----
     lds_fill<I1::BYTES, kBwdWaves>(lw, a.p.img[2]);
-    stagger();
 #pragma unroll
     for (int r = 0; r < HS; ++r) dh[r] = dc[r] = dab[r] = 0.0f;
     {
@@ -260,7 +254,6 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void sur_bwd_kern
     }
     // ---- layer 1 ----
     lds_fill<I1::BYTES, kBwdWaves>(lw, a.p.img[1]);
-    stagger();
 #pragma unroll
     for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
     for (int t = kL - 1; t >= 2; --t) {
@@ -281,7 +274,6 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void sur_bwd_kern
     }
     // ---- layer 0: the window-row gradients are dL/dx ----
     lds_fill<I0::BYTES, kBwdWaves>(lw, a.p.img[0]);
-    stagger();
 #pragma unroll
     for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
     float *gx = (a.g_x && valid) ? a.g_x + (size_t)b * kL * kIn : nullptr;

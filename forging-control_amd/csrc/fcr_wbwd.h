@@ -1,6 +1,6 @@
 // fcr_wbwd.h — H > 52 (config 5): the backward cell's gradient product [input grad | dh_{t-1}] = dG · [W_ih | W_hh]
-// as ONE hand-written split-f16 MFMA GEMM (in place of rocBLAS gemm16_bwd's Cijk kernels; FCR_WIDE_HWBWD,
-// fcr_abi.hip). Reference: the autograd backward of nn.LSTM inside loss.backward() (Functions.py:325, :655).
+// as ONE hand-written split-f16 MFMA GEMM (in place of rocBLAS gemm16_bwd's Cijk kernels where the shapes allow,
+// fcr_abi.hip wide_hwbwd_ok). Reference: the autograd backward of nn.LSTM inside loss.backward() (Functions.py:325, :655).
 //
 // out[b][n] = sum_r dG[b][r] W[r][n] over the 4H gate rows r, fp32-accurate from f16 halves: with dG = dG_hi +
 // dG_lo (the cell kernel's split of dG * scale, wide_cell_bwd_kernel) and W = W_hi + W_lo,
@@ -27,10 +27,7 @@ namespace fcr {
 constexpr int kWbM = 256;                 // output columns per workgroup
 constexpr int kWbN = 128;                 // trajectories per workgroup
 constexpr int kWbK = 32;                  // k per step
-#ifndef FCR_WB_WM
-#define FCR_WB_WM 4   // waves along the output columns (x 2 along the trajectories)
-#endif
-constexpr int kWbWM = FCR_WB_WM, kWbWN = 2;
+constexpr int kWbWM = 4, kWbWN = 2;       // waves along the output columns x along the trajectories
 constexpr int kWbWaves = kWbWM * kWbWN;
 constexpr int kWbTM = kWbM / kWbWM / 16, kWbTN = kWbN / kWbWN / 16;   // D tiles per wave
 constexpr int kWbThreads = 64 * kWbWaves;

@@ -1,7 +1,7 @@
 // fcr_wgemm.h — H > 52 (config 5): one LSTM cell of the whole batch as ONE hand-written split-f16 MFMA GEMM
 // with the cell update in its epilogue (in place of rocBLAS gemm16_fwd + wide_cell_kernel, every layer).
-// On by default (FCR_WIDE_FUSED=1, fcr_abi.hip) for every layer when H % 64 == 0: at config 5 it takes the
-// step from 703 to 657 ms (forward 219 -> 180 ms), equal to the rocBLAS path within 2e-7 relative.
+// Used for every layer when H % 64 == 0: at config 5 it took the step from 703 to 657 ms (forward 219 -> 180
+// ms), equal to the rocBLAS path within 2e-7 relative.
 //
 // Product: G[b][r] = sum_k XB[b][k] A[r][k], the K-concatenated split operands of fcr_wide.h (A = [Wih_hi |
 // Wih_hi | Wih_lo | Whh_hi | Whh_hi | Whh_lo] rows r = gate*H + unit, XB = [x_hi | x_lo | x_hi | h_hi | h_lo |
@@ -12,19 +12,19 @@
 //
 // Tile walk: 4 waves (2 x 2), each 128 rows (32 units) x 64 trajectories = 8 x 4 D tiles (LDS reads 0.023
 // B per MFMA flop, under the 0.031 one CU's LDS sustains at the MFMA peak); K in steps of 32 (one 16x16x32
-// f16 k-block), A and XB chunks staged global -> registers -> LDS, double-buffered, one barrier per step;
+// f16 k-block), A and XB chunks staged into LDS by LDS-DMA through a 3-stage ring, one barrier per step;
 // 72 KB of LDS (the epilogue's tiles) lets two workgroups share a CU, so one's epilogue and barriers
 // overlap the other's MFMAs. LDS rows are 64 B; their 16-B chunks are XOR-swizzled by (row >> 1) & 3, so
 // the 8 rows of a ds_read_b128 phase land on distinct 16-B bank groups. (8 waves x 128 x 32 measured the
 // same; K steps of 64 at one workgroup per CU 13 % slower; B fragments loaded straight from global memory
 // into registers (64-B row pieces) 22 % slower; a second register set for a two-step prefetch 5 % slower.
 // Diagnostic builds bound the loop: cache-hot operand loads gain 6 %, no loads and LDS stores at all 33 %:
-// the staging (LDS write traffic and the wait before it), not HBM, is what the loop loses to. The stages
-// are filled by LDS-DMA (global_load_lds, FCR_WG_DMA): 2 % faster than the register round trip; a 3-stage
-// ring with the next step's fragment reads overlapping the MFMAs measured 5 % slower. A 3-stage ring with
-// two steps of DMA prefetch and a bare s_barrier (FCR_WG_STAGES=3, default since round 2f): forward 191.9
-// -> 188.0 ms at config 5, bit-identical — the loop is not waiting on HBM latency so much as on its
-// per-step barrier and LDS traffic.)
+// the staging (LDS write traffic and the wait before it), not HBM, is what the loop loses to. LDS-DMA
+// (global_load_lds) was 2 % faster than the register round trip; a 3-stage ring with the next step's fragment
+// reads overlapping the MFMAs 5 % slower; the 3-stage ring with two steps of DMA prefetch and a bare
+// s_barrier (round 2f) took the config-5 forward from 191.9 to 188.0 ms, bit-identical — the loop is not
+// waiting on HBM latency so much as on its per-step barrier and LDS traffic. The register-staged and 2-stage
+// forms are in the history.)
 #pragma once
 #include "fcr_common.h"
 #include "fcr_f16.h"
@@ -34,34 +34,19 @@ namespace fcr {
 constexpr int kWgU = 64;                  // units per workgroup
 constexpr int kWgM = 4 * kWgU;            // A rows per workgroup
 constexpr int kWgN = 128;                 // trajectories per workgroup
-#ifndef FCR_WG_K
-#define FCR_WG_K 32
-#endif
-constexpr int kWgK = FCR_WG_K;            // K per step: 32 keeps the workgroup at 72 KB of LDS, two per CU
+constexpr int kWgK = 32;                  // K per step: 32 keeps the workgroup at 72 KB of LDS, two per CU
 constexpr int kWgC = kWgK / 8;            // 16-B chunks per LDS row
-#ifndef FCR_WG_WAVES
-#define FCR_WG_WAVES 4
-#endif
-constexpr int kWgWaves = FCR_WG_WAVES;
-#ifndef FCR_WG_DMA
-#define FCR_WG_DMA 1
-#endif    // 2 x kWgWC waves; each 128 rows x kWgN / kWgWC trajectories
+constexpr int kWgWaves = 4;               // 2 x kWgWC waves; each 128 rows x kWgN / kWgWC trajectories
 constexpr int kWgWC = kWgWaves / 2;
 constexpr int kWgNT = kWgN / kWgWC / 16;  // D tiles per wave along the trajectories
 constexpr int kWgThreads = 64 * kWgWaves;
-static_assert(kWgWaves == 4 || kWgWaves == 8, "wave layout");
 constexpr int kWgStageA = kWgM * kWgK * 2;   // bytes
 constexpr int kWgStageB = kWgN * kWgK * 2;
 constexpr int kWgEpi = kWgN * ((kWgU + 4) * 4 + 2 * (kWgU + 8) * 2);   // the epilogue's c / hi / lo tiles
-#ifndef FCR_WG_STAGES
-#define FCR_WG_STAGES 3
-#endif
-// LDS stages of the DMA mainloop: 2 = one step of prefetch; 3 = two steps (the ring fits in the 72 KB the
-// epilogue's tiles take anyway), the stage wait is vmcnt(pieces of one step), not vmcnt(0)
-constexpr int kWgStages = FCR_WG_STAGES;
-static_assert(kWgStages == 2 || kWgStages == 3, "stages");
+// LDS stages of the DMA mainloop: 3 = two steps of prefetch (the ring fits in the 72 KB the epilogue's tiles take
+// anyway), the stage wait is vmcnt(pieces of one step), not vmcnt(0)
+constexpr int kWgStages = 3;
 constexpr int kWgLds = kWgStages * (kWgStageA + kWgStageB) > kWgEpi ? kWgStages * (kWgStageA + kWgStageB) : kWgEpi;
-static_assert(kWgK == 32 || kWgK == 64, "K step");
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -80,12 +65,9 @@ struct WgArgs {
 
 // byte offset of 16-B chunk c of LDS row r in a stage; the swizzle puts the 8 rows of a fragment read's
 // 8-lane phase on the 8 distinct 16-B slots of a 128-B bank line
-__device__ __forceinline__ uint32_t wg_off(int r, int c) {
-    if constexpr (kWgC == 8) return (uint32_t)(r * 128 + ((c ^ (r & 7)) << 4));
-    else return (uint32_t)(r * 64 + ((c ^ ((r >> 1) & 3)) << 4));
-}
+__device__ __forceinline__ uint32_t wg_off(int r, int c) { return (uint32_t)(r * 64 + ((c ^ ((r >> 1) & 3)) << 4)); }
 
-__global__ __launch_bounds__(kWgThreads, 8 / kWgWaves) void wide_gemm_cell_kernel(WgArgs a) {
+__global__ __launch_bounds__(kWgThreads, 2) void wide_gemm_cell_kernel(WgArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -101,7 +83,6 @@ __global__ __launch_bounds__(kWgThreads, 8 / kWgWaves) void wide_gemm_cell_kerne
     const int b0 = (wg / ny) * kWgN;                   // first trajectory
     const int nk = a.K / kWgK;
 
-#if FCR_WG_DMA
     // LDS-DMA staging (global_load_lds, 16 B per lane): one wave instruction fills one 1 KB piece of a stage
     // = 16 rows x 64 B; lane i lands at +16 i, i.e. row i >> 2, slot i & 3, so it fetches the global chunk
     // that the row's swizzle puts in that slot. A stage is 16 A pieces + 8 B pieces, 6 per wave.
@@ -140,7 +121,6 @@ __global__ __launch_bounds__(kWgThreads, 8 / kWgWaves) void wide_gemm_cell_kerne
 #pragma unroll
         for (int n = 0; n < kWgNT; ++n) acc[m][n] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     const int fr = lane & 15, fq = lane >> 4;
-#if FCR_WG_STAGES == 3
     // two steps of prefetch: stage ks is waited for with step ks + 1's pieces still in flight (vmcnt counts
     // this wave's DMA in issue order), and the barrier is a bare s_barrier: __syncthreads()'s release fence
     // would drain every outstanding load (vmcnt(0)). The empty asm statements keep the compiler's LDS
@@ -173,109 +153,6 @@ __global__ __launch_bounds__(kWgThreads, 8 / kWgWaves) void wide_gemm_cell_kerne
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-#else
-    dma(0, 0);
-    for (int ks = 0; ks < nk; ++ks) {
-        const int buf = ks & 1;
-        // stage ks landed (every wave drains its own DMA; the barrier publishes them all), stage ks - 1
-        // retired. The wait is explicit: the compiler's LDS-DMA tracking is not relied on for it
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        const char *base = lds + buf * (kWgStageA + kWgStageB);
-        f16x8 af[8], bf[kWgNT];
-#pragma unroll
-        for (int n = 0; n < kWgNT; ++n)
-            bf[n] = *reinterpret_cast<const f16x8 *>(base + kWgStageA + wg_off(16 * (kWgNT * wc + n) + fr, fq));
-#pragma unroll
-        for (int m = 0; m < 8; ++m) af[m] = *reinterpret_cast<const f16x8 *>(base + wg_off(128 * wr + 16 * m + fr, fq));
-        if (ks + 1 < nk) dma(ks + 1, buf ^ 1);   // after this step's reads: they need not wait for it
-#pragma unroll
-        for (int m = 0; m < 8; ++m)
-#pragma unroll
-            for (int n = 0; n < kWgNT; ++n) acc[m][n] = mfma16(af[m], bf[n], acc[m][n]);
-    }
-    __syncthreads();
-#endif
-#else
-    // global -> register chunk assignment: A 256 rows x kWgC chunks, XB 128 rows x kWgC chunks
-    constexpr int NA = kWgM * kWgC / kWgThreads, NB = kWgN * kWgC / kWgThreads, RS = kWgThreads / kWgC;
-    const int cch = tid % kWgC;
-    const _Float16 *gA[NA];
-    uint32_t oA[NA];
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-        const int r = tid / kWgC + RS * i;            // LDS row = 4 * unit + gate
-        const int grow = (r & 3) * H + u0 + (r >> 2);  // torch row gate * H + unit
-        gA[i] = a.A + (size_t)grow * a.lda + cch * 8;
-        oA[i] = wg_off(r, cch);
-    }
-    const _Float16 *gB[NB];
-    uint32_t oB[NB];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-        const int r = tid / kWgC + RS * i;
-        int b = b0 + r;
-        if (b >= a.B) b = a.B - 1;                     // tail rows recompute the last trajectory (not stored)
-        gB[i] = a.XB + (size_t)b * a.ldb + cch * 8;
-        oB[i] = (uint32_t)kWgStageA + wg_off(r, cch);
-    }
-    // one step ahead: step ks + 1's chunks are loaded into registers before step ks's MFMAs and stored to
-    // the other LDS stage after them (a second register set, two steps ahead, measured slower: 272 vs 259 us)
-    u32x4 ra[NA], rb[NB];
-    auto gload = [&](int ks) {
-#pragma unroll
-        for (int i = 0; i < NA; ++i) ra[i] = *reinterpret_cast<const u32x4 *>(gA[i] + ks * kWgK);
-#pragma unroll
-        for (int i = 0; i < NB; ++i) rb[i] = *reinterpret_cast<const u32x4 *>(gB[i] + ks * kWgK);
-    };
-    auto lstore = [&](int buf) {
-        char *base = lds + buf * (kWgStageA + kWgStageB);
-#pragma unroll
-        for (int i = 0; i < NA; ++i) *reinterpret_cast<u32x4 *>(base + oA[i]) = ra[i];
-#pragma unroll
-        for (int i = 0; i < NB; ++i) *reinterpret_cast<u32x4 *>(base + oB[i]) = rb[i];
-    };
-
-    f32x4 acc[8][kWgNT];
-#pragma unroll
-    for (int m = 0; m < 8; ++m)
-#pragma unroll
-        for (int n = 0; n < kWgNT; ++n) acc[m][n] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-
-    // fragment reads: A tile m rows 128 wr + 16 m + (lane & 15), k chunk 4 kb + (lane >> 4); B likewise
-    const int fr = lane & 15, fq = lane >> 4;
-    gload(0);
-    lstore(0);
-    __syncthreads();
-    for (int ks = 0; ks < nk; ++ks) {
-        const int buf = ks & 1;
-        if (ks + 1 < nk) gload(ks + 1);
-        const char *base = lds + buf * (kWgStageA + kWgStageB);
-#pragma unroll
-        for (int kb = 0; kb < kWgK / 32; ++kb) {
-            f16x8 bf[kWgNT];
-#pragma unroll
-            for (int n = 0; n < kWgNT; ++n) {
-                const int r = 16 * (kWgNT * wc + n) + fr;
-                bf[n] = *reinterpret_cast<const f16x8 *>(base + kWgStageA + wg_off(r, 4 * kb + fq));
-            }
-#pragma unroll
-            for (int m = 0; m < 8; ++m) {
-                const int r = 128 * wr + 16 * m + fr;
-                const f16x8 af = *reinterpret_cast<const f16x8 *>(base + wg_off(r, 4 * kb + fq));
-#pragma unroll
-                for (int n = 0; n < kWgNT; ++n) acc[m][n] = mfma16(af, bf[n], acc[m][n]);
-            }
-        }
-        if (ks + 1 < nk) lstore(buf ^ 1);
-        __syncthreads();
-    }
-
-#endif
-#ifdef FCR_WG_NOEPI   // diagnostic: the mainloop alone (one store per tile keeps it live)
-    if (a.B < 0) for (int m = 0; m < 8; ++m) a.c_out[m] = acc[m][0][0] + acc[m][kWgNT - 1][0];
-    return;
-#endif
     // ---- epilogue: the cell update (wide_cell_kernel's arithmetic) on the accumulators, through LDS ----
     // A lane holds (trajectory, unit) pairs scattered over 16 rows; the slabs want whole rows. So the c_prev
     // tile comes in by rows, each lane updates its pairs in LDS tiles [trajectory][unit] (rows padded by 16 B:

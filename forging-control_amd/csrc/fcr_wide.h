@@ -272,18 +272,13 @@ __global__ void wide_head_kernel(WideArgs a, int j) {
 // act: the gate activations (i, f, g, o) kept by the recompute, or with PRE their pre-activations (the
 // split-f16 rollout keeps the GEMM output per cell instead of writing a second 4H-wide array), from which
 // the activations are rebuilt with the forward's arithmetic. dG (fp32) may be null when only dgsp is used.
-#ifndef FCR_ROWG_DPP
-#define FCR_ROWG_DPP 0
-#endif
 // a lane's value moved by a DPP pattern within its 16-lane row (every lane has a source: no bound control)
 template <int CTRL>
 __device__ __forceinline__ float dpp_f32(float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
-// FCR_WIDE_CREC = 1: with PRE, c_t is recomputed from the pre-activations and c_{t-1} rather than loaded
-#ifndef FCR_WIDE_CREC
-#define FCR_WIDE_CREC 1
-#endif
+// With PRE, c_t is recomputed from the pre-activations and c_{t-1} rather than loaded (round 3d: bit-identical,
+// backward -2.4 % at config 5).
 template <bool PRE, int V, int T = 1>
 __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restrict__ act, const float *__restrict__ c,
                                      const float *__restrict__ c_prev, const float *__restrict__ dH,
@@ -331,7 +326,7 @@ __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restr
         const typename W::F dhv = W::ld(dH + b * ldh + u), dcv = W::ld(dC + idx);
         typename W::F cp = {}, dn = {}, dg[4], dco, cv;
         if (c_prev) cp = W::ld(c_prev + idx);
-        if (!(PRE && FCR_WIDE_CREC)) cv = W::ld(c + idx);
+        if (!PRE) cv = W::ld(c + idx);
         if (din) dn = W::ld(din + b * ldx + u);
         // rsc: the row's power of two from a bound every dgate of it respects, |dgate| <= |dc_t| <= |dc| + |dh|, taken
         // from the inputs (so the row reduction runs beside the gate arithmetic rather than after it); the row's H / V
@@ -360,7 +355,7 @@ __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restr
                         o = PRE ? sigm(ao[k]) : ao[k];
             // c_t rebuilt as the forward's cell formed it (fcr_wgemm.h epilogue: f c_{t-1} + i g) instead of read: 1 of the
             // ~14 KB a trajectory row moves through this HBM-bound kernel
-            const float tc = tanhf((PRE && FCR_WIDE_CREC) ? (c_prev ? f * cp[k] : 0.0f) + i * g : cv[k]);
+            const float tc = tanhf(PRE ? (c_prev ? f * cp[k] : 0.0f) + i * g : cv[k]);
             const float dh = dhv[k] * mh + dn[k] * c0;
             const float dct = dcv[k] + dh * o * (1.0f - tc * tc);
             dg[0][k] = dct * g * i * (1.0f - i);
@@ -403,22 +398,10 @@ __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restr
                 for (int e = 0; e < V; ++e)
 #pragma unroll
                     for (int cc = 0; cc < kIn; ++cc) pc[cc] = fmaf(dg[k][e], wr[k][e * kIn + cc], pc[cc]);
-#if FCR_ROWG_DPP
-            // 16-lane partial sums on DPP (VALU, no LDS path): quad xor 1, xor 2, then the half-row and row
-            // mirrors pair the quads and the 8-lane halves; 16 and 32 on the bpermute path (HV >= 16 here)
-#pragma unroll
-            for (int cc = 0; cc < kIn; ++cc) {
-                pc[cc] += dpp_f32<0xB1>(pc[cc]);
-                pc[cc] += dpp_f32<0x4E>(pc[cc]);
-                pc[cc] += dpp_f32<0x141>(pc[cc]);
-                pc[cc] += dpp_f32<0x140>(pc[cc]);
-                for (int o = 16; o < HV; o <<= 1) pc[cc] += __shfl_xor(pc[cc], o);
-            }
-#else
+            // (a DPP form of the first four butterfly levels measured within the noise, round 2g)
 #pragma unroll
             for (int cc = 0; cc < kIn; ++cc)
                 for (int o = 1; o < HV; o <<= 1) pc[cc] += __shfl_xor(pc[cc], o);
-#endif
             if (u == 0)
 #pragma unroll
                 for (int cc = 0; cc < kIn; ++cc) rowg[b * kIn + cc] += pc[cc];

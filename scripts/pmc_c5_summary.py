@@ -1,10 +1,11 @@
-"""Config-5 PMC summary (scripts/profile_round3.sh): HBM bytes per launch of the main H = 256 kernels, and the
+"""Config-5 PMC summary (scripts/profile.sh TAG c5|c5max): HBM bytes per launch of the main H = 256 kernels, and the
 HBM bytes of one whole backward pass (every dispatch from wide_bscale_kernel to the ctrl_grad_kernel after it),
 FETCH_SIZE / WRITE_SIZE in separate passes with the gfx950 correction (2 x FETCH + WRITE, MI355X_MICROARCH.md).
-    python scripts/pmc_c5_summary.py TAG DIR  ->  profiles/TAG_c5_pmc.json"""
+    python scripts/pmc_c5_summary.py TAG DIR  ->  profiles/TAG_c5_pmc.json, profiles/TAG_c5_kernel_stats.csv"""
 import csv
 import glob
 import json
+import shutil
 import sys
 
 tag, root = sys.argv[1], sys.argv[2]
@@ -51,5 +52,8 @@ if passes.get("FETCH_SIZE") is not None and passes.get("WRITE_SIZE") is not None
 out["_note"] = ("rocprofv3 PMC passes of bench.py --hidden 256 --horizon 25 --batch 65536 (config 5), KB; "
                 "hbm_bytes_corrected = 2*FETCH + WRITE (gfx950). bwd_pass = every dispatch of the last profiled "
                 "backward pass, wide_bscale_kernel .. ctrl_grad_kernel.")
+stats = glob.glob(f"{root}/trace/**/*kernel_stats.csv", recursive=True)
+if stats:
+    shutil.copy(stats[0], f"profiles/{tag}_c5_kernel_stats.csv")
 json.dump(out, open(f"profiles/{tag}_c5_pmc.json", "w"), indent=1)
 print(json.dumps(out, indent=1))

@@ -1,16 +1,23 @@
-"""Summarise a round profile (scripts/profile_round.sh) into profiles/<tag>_pmc.json and
-profiles/<tag>_kernel_stats.csv: HBM bytes per launch (FETCH_SIZE / WRITE_SIZE passes, gfx950 correction),
-MFMA / VALU / LDS instructions per launch and per wave-cell, and the clock each kernel ran at."""
+"""Summarise a profile (scripts/profile.sh) into profiles/<tag>_pmc.json and profiles/<tag>_kernel_stats.csv: HBM
+bytes per launch (FETCH_SIZE / WRITE_SIZE passes, gfx950 correction), MFMA / VALU / LDS instructions per launch and
+per wave-cell, and the clock each kernel ran at.
+    python scripts/pmc_summary.py TAG DIR [bench.py --batch/--horizon/--precision arguments]"""
+import argparse
 import csv
 import glob
 import json
 import shutil
-import sys
 
-tag = sys.argv[1]
-root = sys.argv[2]
+ap = argparse.ArgumentParser()
+ap.add_argument("tag")
+ap.add_argument("root")
+ap.add_argument("--batch", type=int, default=65536)
+ap.add_argument("--horizon", type=int, default=10)
+ap.add_argument("--precision", default="fp32")
+args = ap.parse_args()
+tag, root = args.tag, args.root
 KERNELS = ("fcr_fwd_kernel", "fcr_bwd_kernel")
-B, N, L, LAYERS, TILE = 65536, 10, 10, 3, 16   # bench.py defaults (config 2)
+B, N, L, LAYERS, TILE = args.batch, args.horizon, 10, 3, 16
 WAVES = (B + TILE - 1) // TILE
 
 
@@ -63,7 +70,7 @@ for name in KERNELS:
         d["clock_ghz_est"] = d["GRBM_GUI_ACTIVE_per_launch"] / 8 / (d["rocprof_avg_ms"] * 1e-3) / 1e9
     if d.get("mfma_flop_per_launch") and d.get("rocprof_avg_ms"):
         d["mfma_tflops_executed"] = d["mfma_flop_per_launch"] / (d["rocprof_avg_ms"] * 1e-3) / 1e12
-out["_note"] = ("rocprofv3 PMC passes of bench.py B=65536 N=10 H=50 (scripts/profile_round.sh): FETCH_SIZE and "
+out["_note"] = (f"rocprofv3 PMC passes of bench.py B={B} N={N} H=50 {args.precision} (scripts/profile.sh): FETCH_SIZE and "
                 "WRITE_SIZE in separate passes, KB; hbm_bytes_corrected = 2*FETCH (gfx950 reports half of wide "
                 "coalesced reads, MI355X_MICROARCH.md HBM) + WRITE. Instruction counts are wave-instructions per "
                 "launch; per wave-cell = / (B/16 waves * N windows * 10 steps * 3 layers).")
