@@ -229,7 +229,11 @@ def grad_check(sim, ctrl, X, S, N, dev, precision, B_check=None):
     # every output over ALL trajectories (continuous across the ReLU/Hardtanh/constraint kinks) and the full-batch
     # parameter gradients (flips included); per-trajectory g_u0 outside the kink band (trajectories whose fp64
     # rollout passes within 1e-5 of a kink, where an fp32 mask may flip one term's slope: tests/test_gpu_fullsize.py),
-    # the band reported on its own
+    # the band reported on its own beside stock torch fp32's error there
+    # the reference's own arithmetic (stock torch fp32, same oracle, same device) against the same fp64: the fp32
+    # noise floor of this batch, beside which the HIP errors are to be read
+    ref32 = T.loss_and_grads_chunked(params, X, u.detach(), S, N, ALPHA, device=dev, dtype=torch.float32,
+                                     chunk=16384 if H <= 64 else 2048)
     reg = T.kink_margin(params, X.double(), ref["xhat"].reshape(B, N, 4)) > 1e-5
     got["prediction"] = got["prediction"].reshape(B, N)
     err = {}
@@ -240,18 +244,23 @@ def grad_check(sim, ctrl, X, S, N, dev, precision, B_check=None):
         den = r.abs().max().clamp_min(1e-300)
         if k == "g_u0":
             e = (a - r).abs() / den
-            band = {"trajectories": int((~reg).sum()), "max_rel_err": float(e[~reg].max()) if (~reg).any() else 0.0,
-                    "above_1e-5": int((e[~reg] > 1e-5).sum())}
+            e32 = (ref32[k].reshape(v.shape).double() - r).abs() / den
+            hip_b = float(e[~reg].max()) if (~reg).any() else 0.0
+            t32_b = float(e32[~reg].max()) if (~reg).any() else 0.0
+            band = {"trajectories": int((~reg).sum()), "max_rel_err": hip_b, "above_1e-5": int((e[~reg] > 1e-5).sum()),
+                    "torch_fp32_max_rel_err": t32_b, "torch_fp32_above_1e-5": int((e32[~reg] > 1e-5).sum()),
+                    "bound": max(1e-5, 2.0 * t32_b),
+                    "bound_def": "max(1e-5, 2 x stock torch fp32's own band error on this batch)"}
+            band["within_bound"] = hip_b <= band["bound"]
             a, r = a[reg], r[reg]
         err[k] = float((a - r).abs().max() / den)
-    # the reference's own arithmetic (stock torch fp32, same oracle, same device) against the same fp64: the
-    # fp32 noise floor of this batch, beside which the HIP errors above are to be read
-    ref32 = T.loss_and_grads_chunked(params, X, u.detach(), S, N, ALPHA, device=dev, dtype=torch.float32,
-                                     chunk=16384 if H <= 64 else 2048)
     err32 = {}
-    for k in ("loss", "prediction", "xhat", "g_W_inp", "g_b_inp", "g_W_out"):
+    for k in ("loss", "prediction", "xhat", "g_W_inp", "g_b_inp", "g_W_out", "g_u0"):
         r = ref[k].reshape(-1)
-        err32[k] = float((ref32[k].reshape(-1).double() - r).abs().max() / r.abs().max().clamp_min(1e-300))
+        a32 = ref32[k].reshape(-1).double()
+        if k == "g_u0":
+            a32, r = a32[reg], r[reg]
+        err32[k] = float((a32 - r).abs().max() / ref[k].abs().max().clamp_min(1e-300))
     for p in ctrl.parameters():
         p.grad = None
     grads = ("g_u0", "g_W_inp", "g_b_inp", "g_W_out")
@@ -281,10 +290,10 @@ def main():
                     help="time the step as NeuralNetwork.captured_step replays it (one HIP graph per step; the "
                          "launch-bound small batches, e.g. the reference's B = 15); 1 GPU")
     ap.add_argument("--small-limit", type=int, default=None,
-                    help="fcr_set_small_batch_limit: B at or below it runs the small-batch kernels (0 = never; "
+                    help="MPCLoss(small_batch_limit=...): B at or below it runs the small-batch kernels (0 = never; "
                          "default: the library's, 8192)")
     ap.add_argument("--wide-keep-budget", default=None,
-                    help="H > 52: bytes of kept windows the workspace may hold (fcr_set_wide_keep_budget), in GiB, or "
+                    help="H > 52: bytes of kept windows the workspace may hold (MPCLoss(wide_keep_budget=...)), in GiB, or "
                          "'max' = the device's free memory less 8 GiB. The library default keeps what fits in half the "
                          "free memory (within 40%% of HBM); a job that owns the GPU opts in to more: fewer windows "
                          "recomputed in the backward")
@@ -320,17 +329,14 @@ def main():
             keep_budget = max(0, free - (8 << 30))
         else:
             keep_budget = int(float(args.wide_keep_budget) * (1 << 30))
-        fca._native.set_wide_keep_budget(keep_budget)
-    if args.small_limit is not None:
-        fca._native.set_small_batch_limit(args.small_limit)
-    # which kernel family runs (include/fcr.h, fcr_set_small_batch_limit)
-    small = args.precision == "fp32" and 17 <= H <= 52 and B <= fca._native.small_batch_limit()
 
     sim, ctrl = load_weights(dev, H)
     if world > 1:
         fca.distributed.broadcast_params(ctrl)
     opt = torch.optim.AdamW(ctrl.parameters(), lr=1e-4)     # UL/Main.py:195
-    loss_fn = fca.MPCLoss(prediction_horizon=N, alpha=ALPHA, precision=args.precision)
+    # this loss's own kernel options (include/fcr.h fcr_options; None = the library's defaults)
+    loss_fn = fca.MPCLoss(prediction_horizon=N, alpha=ALPHA, precision=args.precision,
+                          small_batch_limit=args.small_limit, wide_keep_budget=keep_budget)
     sync = fca.distributed.GradAllReduce() if world > 1 else None
     X, S = synth_batch(B, dev, 1000 + rank)
     stream = torch.cuda.current_stream(dev)      # the stream the C ABI launches on
@@ -362,6 +368,8 @@ def main():
         for _ in range(args.warmup):
             step()
     torch.cuda.synchronize()
+    call = loss_fn.last_call   # what the warm-up steps ran: kernel families, workspace, kept windows (H > 52)
+    small = call is not None and call.forward == "small"
 
     # timed region: K steps; HIP events on the launching stream bracket the fused forward and backward of
     # EVERY timed step (the per-kernel times come from the same steps as ms_per_step)
@@ -443,10 +451,12 @@ def main():
                                    f"ctrl 3-50-1, {prec_label}" + (", HIP-graph replay" if captured is not None else ""),
                        "batch_per_gpu": B, "global_batch": B * world,
                        "horizon": N, "hidden": H, "parallelism": f"dp{world}", "world_size": world,
-                       **({"wide_keep_budget_gib": round(keep_budget / 2**30, 1),
-                           "workspace_gib": round(fca._native.workspace_bytes(
-                               fca.rollout.make_dims(B, N, H, 3, 50, ALPHA), True) / 2**30, 1)}
-                          if keep_budget is not None else {}),
+                       "kernels": {"forward": call.forward, "backward": call.backward} if call else None,
+                       **({"wide_keep_budget_gib": round(keep_budget / 2**30, 1) if keep_budget is not None
+                           else "library default (half the free memory at first sizing, <= 40% of HBM)",
+                           "workspace_gib": round(call.workspace_bytes / 2**30, 1),
+                           "kept_windows": call.kept_windows}
+                          if H > 52 and call is not None else {}),
                        **({"rehearsal": "--share-gpu: every rank on cuda:0 over gloo (path check, not a scaling "
                                         "number)"} if args.share_gpu else {})},
             "roofline": roof,

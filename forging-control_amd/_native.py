@@ -14,15 +14,17 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", _LIB_NAME)
 
 FCR_OK = 0
-ABI_VERSION = 4
+ABI_VERSION = 5
 PRECISION_FP32, PRECISION_F16, PRECISION_F16_FWD = 0, 1, 2
 ERRORS = {-1: "FCR_EINVAL", -2: "FCR_EWORKSPACE", -3: "FCR_EHIP", -4: "FCR_EUNSUPPORTED"}
 
 # Every symbol include/fcr.h declares (tests check the .so exports exactly these).
-EXPORTS = ("fcr_workspace_size", "fcr_forward", "fcr_backward", "fcr_lstm_workspace_size", "fcr_lstm_forward",
-           "fcr_lstm_backward", "fcr_plant_rk4", "fcr_closed_loop_run", "fcr_window_gather", "fcr_fnn_workspace_size",
-           "fcr_fnn_forward", "fcr_fnn_backward", "fcr_set_small_batch_limit", "fcr_set_wide_keep_budget", "fcr_last_kernels",
-           "fcr_last_error", "fcr_abi_version")
+EXPORTS = ("fcr_workspace_size", "fcr_wide_kept_windows", "fcr_forward", "fcr_backward", "fcr_lstm_workspace_size",
+           "fcr_lstm_forward", "fcr_lstm_backward", "fcr_plant_rk4", "fcr_closed_loop_run", "fcr_window_gather",
+           "fcr_fnn_workspace_size", "fcr_fnn_forward", "fcr_fnn_backward", "fcr_set_small_batch_limit",
+           "fcr_get_small_batch_limit", "fcr_set_wide_keep_budget", "fcr_get_wide_keep_budget", "fcr_last_error",
+           "fcr_abi_version")
+OPT_INHERIT, KEEP_AUTO = -2, -1
 
 
 class FcrDims(ctypes.Structure):
@@ -32,6 +34,22 @@ class FcrDims(ctypes.Structure):
         ("ctrl_in", ctypes.c_int32), ("ctrl_hidden", ctypes.c_int32), ("alpha", ctypes.c_float),
         ("precision", ctypes.c_int32),
     ]
+
+
+class FcrOptions(ctypes.Structure):
+    """fcr_options (include/fcr.h): the per-call kernel options; `kernels` is written by each call."""
+    _fields_ = [("small_batch_limit", ctypes.c_int32), ("kernels", ctypes.c_int32), ("wide_keep_budget", ctypes.c_int64)]
+
+
+def make_options(small_batch_limit=None, wide_keep_budget=None) -> FcrOptions:
+    """Per-call options: None inherits the process-wide default; wide_keep_budget "auto" = the library's policy."""
+    keep = OPT_INHERIT if wide_keep_budget is None else KEEP_AUTO if wide_keep_budget == "auto" else int(wide_keep_budget)
+    if wide_keep_budget is not None and keep < KEEP_AUTO:
+        raise ValueError(f"wide_keep_budget must be >= 0 bytes, 'auto' or None, got {wide_keep_budget!r}")
+    small = OPT_INHERIT if small_batch_limit is None else int(small_batch_limit)
+    if small < 0 and small_batch_limit is not None:
+        raise ValueError(f"small_batch_limit must be >= 0 or None, got {small_batch_limit!r}")
+    return FcrOptions(small, 0, keep)
 
 
 class FcrWeights(ctypes.Structure):
@@ -82,12 +100,15 @@ def load() -> ctypes.CDLL:
                 "(hipcc --offload-arch=gfx950). There is no fallback path.")
         lib = ctypes.CDLL(LIB_PATH)
         vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
-        lib.fcr_workspace_size.argtypes = [ctypes.POINTER(FcrDims), i32, ctypes.POINTER(sz)]
+        po = ctypes.POINTER(FcrOptions)
+        lib.fcr_workspace_size.argtypes = [ctypes.POINTER(FcrDims), po, i32, ctypes.POINTER(sz)]
         lib.fcr_workspace_size.restype = i32
-        lib.fcr_forward.argtypes = [ctypes.POINTER(FcrDims), ctypes.POINTER(FcrWeights),
+        lib.fcr_wide_kept_windows.argtypes = [ctypes.POINTER(FcrDims), sz, ctypes.POINTER(ctypes.c_int32)]
+        lib.fcr_wide_kept_windows.restype = i32
+        lib.fcr_forward.argtypes = [ctypes.POINTER(FcrDims), po, ctypes.POINTER(FcrWeights),
                                     vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, sz, vp]
         lib.fcr_forward.restype = i32
-        lib.fcr_backward.argtypes = [ctypes.POINTER(FcrDims), vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp]
+        lib.fcr_backward.argtypes = [ctypes.POINTER(FcrDims), po, vp, vp, vp, vp, vp, vp, vp, vp, vp, sz, vp]
         lib.fcr_backward.restype = i32
         lib.fcr_plant_rk4.argtypes = [i32, i32, ctypes.c_double, i32, i32, vp, vp, vp, vp]
         lib.fcr_plant_rk4.restype = i32
@@ -110,10 +131,12 @@ def load() -> ctypes.CDLL:
         lib.fcr_fnn_backward.restype = i32
         lib.fcr_set_small_batch_limit.argtypes = [i32]
         lib.fcr_set_small_batch_limit.restype = i32
+        lib.fcr_get_small_batch_limit.argtypes = []
+        lib.fcr_get_small_batch_limit.restype = i32
         lib.fcr_set_wide_keep_budget.argtypes = [ctypes.c_int64]
         lib.fcr_set_wide_keep_budget.restype = ctypes.c_int64
-        lib.fcr_last_kernels.argtypes = []
-        lib.fcr_last_kernels.restype = i32
+        lib.fcr_get_wide_keep_budget.argtypes = []
+        lib.fcr_get_wide_keep_budget.restype = ctypes.c_int64
         lib.fcr_last_error.argtypes = []
         lib.fcr_last_error.restype = ctypes.c_char_p
         lib.fcr_abi_version.argtypes = []
@@ -131,36 +154,40 @@ def check(rc: int, what: str) -> None:
 
 
 def set_small_batch_limit(max_batch: int) -> int:
-    """fcr_set_small_batch_limit: B <= max_batch runs the small-batch kernels (0 = never); returns the old limit."""
+    """fcr_set_small_batch_limit: the process-wide DEFAULT small-batch limit (B <= it runs the small-batch kernels,
+    0 = never) of calls whose options inherit it; returns the old value. Per call: MPCLoss(small_batch_limit=...)."""
     return int(load().fcr_set_small_batch_limit(int(max_batch)))
 
 
+def small_batch_limit() -> int:
+    """The process-wide default small-batch limit (fcr_get_small_batch_limit: read-only)."""
+    return int(load().fcr_get_small_batch_limit())
+
+
 def set_wide_keep_budget(nbytes: int) -> int:
-    """fcr_set_wide_keep_budget (H > 52): bytes of kept windows a backward-enabled workspace may add, so their
-    backward skips the recompute (< 0 = default: half the device memory free at its first sizing, at most 40 %
-    of the device; 0 = none); returns the old budget. Process-wide."""
+    """fcr_set_wide_keep_budget (H > 52): the process-wide DEFAULT bytes of kept windows a backward-enabled workspace
+    may add, so their backward skips the recompute (< 0 = the library's policy: half the device memory free at its
+    first sizing, at most 40 % of the device; 0 = none); returns the old budget. Per call: MPCLoss(wide_keep_budget=...)."""
     return int(load().fcr_set_wide_keep_budget(int(nbytes)))
+
+
+def wide_keep_budget() -> int:
+    """The process-wide default keep budget (fcr_get_wide_keep_budget: read-only)."""
+    return int(load().fcr_get_wide_keep_budget())
 
 
 KERNEL_FAMILIES = {0: None, 1: "small", 2: "fused", 3: "wide"}
 
 
-def last_kernels() -> tuple:
-    """fcr_last_kernels: (forward family, backward family) the process last launched — "small", "fused",
-    "wide" or None."""
-    v = int(load().fcr_last_kernels())
-    return KERNEL_FAMILIES[v & 0xF], KERNEL_FAMILIES[(v >> 4) & 0xF]
-
-
-def small_batch_limit() -> int:
-    """The current small-batch limit (fcr_set_small_batch_limit's value)."""
-    cur = set_small_batch_limit(0)
-    set_small_batch_limit(cur)
-    return cur
-
-
-def workspace_bytes(dims: FcrDims, with_backward: bool) -> int:
+def workspace_bytes(dims: FcrDims, with_backward: bool, opts: FcrOptions | None = None) -> int:
     out = ctypes.c_size_t(0)
-    check(load().fcr_workspace_size(ctypes.byref(dims), int(bool(with_backward)), ctypes.byref(out)),
-          "fcr_workspace_size")
+    check(load().fcr_workspace_size(ctypes.byref(dims), ctypes.byref(opts) if opts is not None else None,
+                                    int(bool(with_backward)), ctypes.byref(out)), "fcr_workspace_size")
+    return int(out.value)
+
+
+def kept_windows(dims: FcrDims, ws_bytes: int) -> int:
+    """fcr_wide_kept_windows: windows (of N) a backward-enabled H > 52 workspace of ws_bytes keeps."""
+    out = ctypes.c_int32(0)
+    check(load().fcr_wide_kept_windows(ctypes.byref(dims), int(ws_bytes), ctypes.byref(out)), "fcr_wide_kept_windows")
     return int(out.value)

@@ -212,22 +212,19 @@ int launch_bwd(const BwdArgs &ba, const Layout &L, bool lp, hipStream_t s) {
 }
 
 // Small-batch kernels (fcr_small.h): one workgroup of ceil(HS/4) waves per 16-trajectory group.
-// Used for the fp32-accurate mode at HS = 8, 13 when B <= g_small_max_batch (fcr_set_small_batch_limit):
-// below one wave per SIMD the fused kernels run at one wave's sequential latency.
-// Process-wide (not thread-local): torch runs a CUDA tensor's backward on its autograd worker thread, so a
-// per-thread limit set by the caller would reach the forward only. A change between a forward and its
-// backward is harmless: both families keep one workspace layout, and a mixed pair is valid (tested).
+// Used for the fp32-accurate mode at HS = 8, 13 when B <= the call's small-batch limit (fcr_options; the
+// process-wide default g_small_max_batch when it inherits): below one wave per SIMD the fused kernels run at one
+// wave's sequential latency. A change between a forward and its backward is harmless: both families keep one
+// workspace layout, and a mixed pair is valid (tested).
 std::atomic<int> g_small_max_batch{8192};
-// fcr_last_kernels: the family the last fcr_forward (bits 0-3) and fcr_backward (bits 4-7) launched, process-wide
-std::atomic<int> g_last_kernels{0};
-void note_kernels(int shift, int family) {
-    int cur = g_last_kernels.load(std::memory_order_relaxed);
-    while (!g_last_kernels.compare_exchange_weak(cur, (cur & ~(0xf << shift)) | (family << shift))) {
-    }
+int small_limit_of(const fcr_options *o) {
+    return (o && o->small_batch_limit >= 0) ? o->small_batch_limit : g_small_max_batch.load(std::memory_order_relaxed);
 }
-bool use_small(const fcr_dims *d, const Layout &L) {
-    return d->precision == FCR_PRECISION_FP32 && (L.HS == 8 || L.HS == 13) &&
-           d->B <= g_small_max_batch.load(std::memory_order_relaxed);
+bool use_small(const fcr_dims *d, const Layout &L, const fcr_options *o) {
+    return d->precision == FCR_PRECISION_FP32 && (L.HS == 8 || L.HS == 13) && d->B <= small_limit_of(o);
+}
+void note_kernels(fcr_options *o, int family) {
+    if (o) o->kernels = family;
 }
 
 template <int HS, bool STORE>
@@ -361,8 +358,12 @@ float *kept_c(const WideLayout &L, char *base, const fcr_dims *d, int j) {
     return (float *)(base + L.KC) + (size_t)(j - (d->N - L.keep)) * kLayers * kL * d->B * d->H;
 }
 // fcr_set_wide_keep_budget: bytes of kept windows fcr_workspace_size may add; < 0 = the default policy
-// (wide_default_cap). Process-wide, like the small-batch limit.
+// (wide_default_cap). The process-wide default of fcr_options.wide_keep_budget.
 std::atomic<long long> g_wide_keep_budget{-1};
+long long keep_budget_of(const fcr_options *o) {
+    if (o && o->wide_keep_budget != FCR_OPT_INHERIT) return o->wide_keep_budget < 0 ? -1 : o->wide_keep_budget;
+    return g_wide_keep_budget.load();
+}
 
 // Default cap of a backward-enabled wide workspace: half of the memory that was FREE on the device the first
 // time one was sized there (cached per device, so the count does not drift as torch's cache holds the last
@@ -1245,10 +1246,20 @@ int fcr_set_small_batch_limit(int32_t max_batch) {
     return g_small_max_batch.exchange(max_batch < 0 ? 0 : max_batch);
 }
 
-int fcr_last_kernels(void) { return g_last_kernels.load(); }
+int fcr_get_small_batch_limit(void) { return g_small_max_batch.load(); }
 
 int64_t fcr_set_wide_keep_budget(int64_t bytes) {
     return g_wide_keep_budget.exchange(bytes < 0 ? -1 : bytes);
+}
+
+int64_t fcr_get_wide_keep_budget(void) { return g_wide_keep_budget.load(); }
+
+int fcr_wide_kept_windows(const fcr_dims *dims, size_t ws_bytes, int32_t *kept) {
+    int rc = check_dims(dims);
+    if (rc) return rc;
+    if (!kept) return fail(FCR_EINVAL, "kept is NULL");
+    *kept = is_wide(dims) ? wide_keep_fit(dims, ws_bytes) : 0;
+    return FCR_OK;
 }
 
 #if FCR_STAMP
@@ -1258,7 +1269,7 @@ size_t fcr_debug_dseq_offset(const fcr_dims *d) { return make_layout(d, 1).dseq;
 size_t fcr_debug_dxrow_offset(const fcr_dims *d) { return make_layout(d, 1).dxrow; }
 #endif
 
-int fcr_workspace_size(const fcr_dims *dims, int with_backward, size_t *bytes) {
+int fcr_workspace_size(const fcr_dims *dims, const fcr_options *opts, int with_backward, size_t *bytes) {
     int rc = check_dims(dims);
     if (rc) return rc;
     if (!bytes) return fail(FCR_EINVAL, "bytes is NULL");
@@ -1269,7 +1280,7 @@ int fcr_workspace_size(const fcr_dims *dims, int with_backward, size_t *bytes) {
     int keep = 0;
     if (with_backward) {   // kept windows within the budget (fcr_set_wide_keep_budget)
         const size_t base = make_wide(dims, 1, 0).total;
-        long long budget = g_wide_keep_budget.load();
+        long long budget = keep_budget_of(opts);
         if (budget < 0) {   // default: the whole workspace within wide_default_cap()
             const long long cap = wide_default_cap();
             budget = cap > (long long)base ? cap - (long long)base : 0;
@@ -1280,7 +1291,7 @@ int fcr_workspace_size(const fcr_dims *dims, int with_backward, size_t *bytes) {
     return FCR_OK;
 }
 
-int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const float *u0,
+int fcr_forward(const fcr_dims *d, fcr_options *opts, const fcr_weights *w, const float *X, const float *u0,
                 const float *states, const float *noise, float *loss, float *cost, float *command,
                 float *error, float *prediction, float *xhat, int with_backward, void *ws,
                 size_t ws_bytes, void *stream) {
@@ -1297,7 +1308,7 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
     if (is_wide(d)) {
         const size_t need = make_wide(d, with_backward).total;
         if (ws_bytes < need) return fail(FCR_EWORKSPACE, "fcr_forward: ws has %zu bytes, needs %zu", ws_bytes, need);
-        note_kernels(0, FCR_KERNELS_WIDE);
+        note_kernels(opts, FCR_KERNELS_WIDE);
         return wide_forward(d, w, X, u0, states, noise, loss, cost, command, error, prediction, xhat, with_backward,
                             (char *)ws, ws_bytes, (hipStream_t)stream);
     }
@@ -1365,8 +1376,8 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
 #if FCR_STAMP
     fa.stamp = (unsigned long long *)(base + L.stamp) + (size_t)L.nw_pad * 8;
 #endif
-    const bool small = use_small(d, L);
-    note_kernels(0, small ? FCR_KERNELS_SMALL : FCR_KERNELS_FUSED);
+    const bool small = use_small(d, L, opts);
+    note_kernels(opts, small ? FCR_KERNELS_SMALL : FCR_KERNELS_FUSED);
     if (small) {
         if (L.HS == 8) rc = with_backward ? launch_sfwd_t<8, true>(fa, L, s) : launch_sfwd_t<8, false>(fa, L, s);
         else rc = with_backward ? launch_sfwd_t<13, true>(fa, L, s) : launch_sfwd_t<13, false>(fa, L, s);
@@ -1385,7 +1396,7 @@ int fcr_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const f
     return launch_check("loss_reduce_kernel");
 }
 
-int fcr_backward(const fcr_dims *d, const float *X, const float *states, const float *prediction,
+int fcr_backward(const fcr_dims *d, fcr_options *opts, const float *X, const float *states, const float *prediction,
                  const float *dloss, float *g_u0, float *g_w_inp, float *g_b_inp, float *g_w_out,
                  void *ws, size_t ws_bytes, void *stream) {
     int rc = check_dims(d);
@@ -1396,7 +1407,7 @@ int fcr_backward(const fcr_dims *d, const float *X, const float *states, const f
     if (is_wide(d)) {
         const size_t need = make_wide(d, 1).total;
         if (ws_bytes < need) return fail(FCR_EWORKSPACE, "fcr_backward: ws has %zu bytes, needs %zu", ws_bytes, need);
-        note_kernels(4, FCR_KERNELS_WIDE);
+        note_kernels(opts, FCR_KERNELS_WIDE);
         return wide_backward(d, X, states, prediction, dloss, g_u0, g_w_inp, g_b_inp, g_w_out, (char *)ws, ws_bytes,
                              (hipStream_t)stream);
     }
@@ -1426,8 +1437,9 @@ int fcr_backward(const fcr_dims *d, const float *X, const float *states, const f
     ba.stamp = (unsigned long long *)(base + L.stamp);
 #endif
     ba.p = packed_ptrs(L, base);
-    note_kernels(4, use_small(d, L) ? FCR_KERNELS_SMALL : FCR_KERNELS_FUSED);
-    if (use_small(d, L)) {
+    const bool small = use_small(d, L, opts);
+    note_kernels(opts, small ? FCR_KERNELS_SMALL : FCR_KERNELS_FUSED);
+    if (small) {
         rc = L.HS == 8 ? launch_sbwd_t<8>(ba, L, s) : launch_sbwd_t<13>(ba, L, s);
     } else {
         switch (L.HS) {

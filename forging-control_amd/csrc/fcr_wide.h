@@ -277,6 +277,10 @@ template <int CTRL>
 __device__ __forceinline__ float dpp_f32(float v) {
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
+// the per-row dgate scale's headroom exponent (wide_cell_bwd_kernel rsc): the forget-gate row of a kL-step window
+// reaches (kL - 1) / 4 * 2^kWideDgExp, which must stay a finite f16
+constexpr int kWideDgExp = 13;
+static_assert((kL - 1) * (1 << kWideDgExp) / 4 < 65504, "f16 overflow of the forget-gate dgates: lower kWideDgExp");
 // With PRE, c_t is recomputed from the pre-activations and c_{t-1} rather than loaded (round 3d: bit-identical,
 // backward -2.4 % at config 5).
 template <bool PRE, int V, int T = 1>
@@ -328,9 +332,12 @@ __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restr
         if (c_prev) cp = W::ld(c_prev + idx);
         if (!PRE) cv = W::ld(c + idx);
         if (din) dn = W::ld(din + b * ldx + u);
-        // rsc: the row's power of two from a bound every dgate of it respects, |dgate| <= |dc_t| <= |dc| + |dh|, taken
-        // from the inputs (so the row reduction runs beside the gate arithmetic rather than after it); the row's H / V
-        // threads are one aligned segment of a wave (the host checks 64 % (H / V) == 0)
+        // rsc: the row's power of two 2^(13-ex) from m = max(|dc| + |dh|) >= |dc_t| (taken from the inputs, so the row
+        // reduction runs beside the gate arithmetic rather than after it; the row's H / V threads are one aligned
+        // segment of a wave, the host checks 64 % (H / V) == 0). The i, g, o rows are |dc_t| or |dh| times a local
+        // derivative <= 1, so below 2^13 scaled; the forget row is dc_t c_{t-1} f (1 - f), and |c_{t-1}| <= t <= kL - 1
+        // (|c_t| <= |c_{t-1}| + 1 from c = 0), so it stays below (kL - 1) / 4 * 2^13 (18 432 at kL = 10): inside f16's
+        // 65 504, with that margin only (kWideDgExp)
         float rsc_up = 1.0f;
         if (rsc) {
             float mx = 0.0f;
@@ -346,8 +353,8 @@ __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restr
                 for (int o = 1; o < HV; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
             }
             const int ex = mx > 0.0f ? __builtin_amdgcn_frexp_expf(mx) : 0;   // every |dgate| < 2^ex
-            rsc_up = __builtin_amdgcn_ldexpf(1.0f, 13 - ex);
-            if (u == 0) rsc[b] = __builtin_amdgcn_ldexpf(1.0f, ex - 13);
+            rsc_up = __builtin_amdgcn_ldexpf(1.0f, kWideDgExp - ex);
+            if (u == 0) rsc[b] = __builtin_amdgcn_ldexpf(1.0f, ex - kWideDgExp);
         }
 #pragma unroll
         for (int k = 0; k < V; ++k) {

@@ -52,6 +52,15 @@ class GradAllReduce:
     def __init__(self, group=None):
         self.group = group
         self._warned = False
+        self._flag_rows = {}   # has-gradient pattern -> its flag tensor on the device (built once, not per step)
+
+    def _flags(self, pattern, like):
+        key = (pattern, like.dtype, like.device)
+        t = self._flag_rows.get(key)
+        if t is None:
+            t = torch.tensor([float(h) for h in pattern], dtype=like.dtype, device=like.device)
+            self._flag_rows[key] = t
+        return t
 
     def __call__(self, module: torch.nn.Module, b_local: int | None = None, b_global: int | None = None,
                  loss: torch.Tensor | None = None):
@@ -64,8 +73,8 @@ class GradAllReduce:
             warnings.warn("GradAllReduce called without the shard size: assuming equal shards (1/world)")
             self._warned = True
         pieces = [p.grad.reshape(-1) if p.grad is not None else torch.zeros_like(p).reshape(-1) for p in params]
-        pieces.append(torch.tensor([float(p.grad is not None) for p in params], dtype=pieces[0].dtype,
-                                   device=pieces[0].device))
+        pattern = tuple(p.grad is not None for p in params)
+        pieces.append(self._flags(pattern, pieces[0]))
         if loss is not None:
             pieces.append(loss.detach().reshape(1).to(pieces[0].dtype))
         if count:
@@ -79,8 +88,8 @@ class GradAllReduce:
         dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
         # a rank that ran the step produces gradients for the same parameters as every other such rank, so it
         # keeps its own pattern (no host sync); only a rank without any gradient reads the flags
-        if any(p.grad is not None for p in params):
-            flags = [float(p.grad is not None) for p in params]
+        if any(pattern):
+            flags = [float(h) for h in pattern]
         else:
             flags = flat[off_flags:off_flags + nflag].tolist()
         if count:

@@ -118,15 +118,25 @@ class MPCLoss(nn.Module):
     shapes. ``enable_noise`` draws ``randn_like(x0) * 0.01`` per horizon step from the device's default
     generator in the reference's order (Functions.py:1401, 1439); a pre-drawn ``noise`` (B, N, 4) can be
     passed instead. After each call ``self.last_trajectory`` holds the (B, N, 4) LSTM predictions.
+
+    Kernel options of THIS loss (include/fcr.h fcr_options, carried from each forward to its backward; None inherits
+    the process-wide default): ``small_batch_limit`` — B at or below it runs the small-batch kernels (0 = never);
+    ``wide_keep_budget`` — H > 52, bytes of kept windows the workspace may add ("auto": the library's policy).
+    ``self.last_call`` (a :class:`~.rollout.CallInfo`) reports the kernel families the last call's passes launched
+    and its workspace.
     """
 
-    def __init__(self, prediction_horizon=10, alpha=0.1, precision="fp32"):
+    def __init__(self, prediction_horizon=10, alpha=0.1, precision="fp32", small_batch_limit=None,
+                 wide_keep_budget=None):
         super().__init__()
         self.N = prediction_horizon
         self.alpha = alpha
         self.precision = precision     # "fp32" (reference-accurate), "f16fwd" (config 3) or "f16" (include/fcr.h)
+        self.small_batch_limit = small_batch_limit
+        self.wide_keep_budget = wide_keep_budget
         self.activation = nn.ReLU()
         self.last_trajectory = None
+        self.last_call = None
 
     def forward(self, simulator: nn.Module, controller: nn.Module, input_controller: torch.Tensor,
                 output_controller: torch.Tensor, states: torch.Tensor, device: torch.device,
@@ -142,9 +152,12 @@ class MPCLoss(nn.Module):
             noise = torch.stack([torch.randn(B, 4, device=X.device) * 0.01 for _ in range(self.N)], dim=1)
         elif not enable_noise:
             noise = None
+        from . import _native
+        from .rollout import CallInfo
+        self.last_call = CallInfo(_native.make_options(self.small_batch_limit, self.wide_keep_budget))
         loss, cost, command, error, prediction, xhat = rollout(
             X, output_controller, states, _controller_params(controller), _simulator_params(simulator),
-            self.N, self.alpha, noise, self.precision)
+            self.N, self.alpha, noise, self.precision, self.last_call)
         self.last_trajectory = xhat
         return loss, {"loss": cost, "command": command, "error": error, "prediction": prediction}
 
@@ -259,13 +272,16 @@ class NeuralNetwork:
         n_batches = 0
         for X, _, z in data_loader:
             X, z = X.to(device), z.to(device)
+            if X.shape[0] == 0:   # an empty shard: join the all-reduce and step, as the eager loop does
+                step.skip_empty(X, z)
+                continue
             loss, *f = step(X, z)
             total = loss.clone() if total is None else total + loss
             for k, v in zip(keys, f):
                 feats[k].append(v.clone())
             n_batches += 1
         avg = float(total.item()) / n_batches if n_batches else 0.0
-        return avg, {k: torch.cat(v, dim=0) for k, v in feats.items()}
+        return avg, {k: torch.cat(v, dim=0) if v else torch.empty(0, device=device) for k, v in feats.items()}
 
     @staticmethod
     def validate_model(data_loader, model, loss_function, device):

@@ -104,6 +104,16 @@ class CapturedStep:
         self.replays += 1
         return self._out
 
+    def skip_empty(self, *batch):
+        """An EMPTY shard (more ranks than trajectories in a short last batch): no body, but with a ``grad_sync``
+        hook the rank still joins the all-reduce (which gives it everyone's gradient) and steps, exactly as
+        ``train_model``'s eager loop does — the other ranks' all-reduce would otherwise wait for it forever."""
+        if self.grad_sync is None:
+            return
+        self.optimizer.zero_grad(set_to_none=True)
+        self.grad_sync(*batch)
+        self.optimizer.step()
+
     def __call__(self, *batch):
         if not batch or not all(isinstance(t, torch.Tensor) and t.is_cuda for t in batch):
             raise RuntimeError("CapturedStep: the batch must be ROCm device tensors")

@@ -35,30 +35,44 @@ def _dev_f32(t, name):
     return t.contiguous()
 
 
+class CallInfo:
+    """What one rollout call ran: its per-call options (fcr_options, carried from the forward to its backward, which
+    torch may run on its autograd thread) and the kernel family each pass launched."""
+
+    def __init__(self, opts):
+        self.opts = opts
+        self.forward = self.backward = None   # "small", "fused" or "wide" once the pass has run
+        self.workspace_bytes = 0
+        self.kept_windows = 0
+
+
 class RolloutFn(torch.autograd.Function):
     """Inputs: X (B,3), u0 (B,1), states (B,10,5), noise (B,N,4) or None, controller params
-    (W_inp, b_inp, W_out), LSTM weights (w_ih0..2, w_hh0..2, fc_w, fc_b), N, alpha.
+    (W_inp, b_inp, W_out), LSTM weights (w_ih0..2, w_hh0..2, fc_w, fc_b), N, alpha, precision, and a CallInfo
+    (the call's fcr_options in, the kernel families out).
     Outputs: loss (0-d), cost (B,), command (B,), error (B,), prediction (B*N,), xhat (B,N,4)."""
 
     @staticmethod
     def forward(ctx, X, u0, states, noise, W_inp, b_inp, W_out, w_ih0, w_ih1, w_ih2, w_hh0, w_hh1,
-                w_hh2, fc_w, fc_b, N, alpha, precision=0):
+                w_hh2, fc_w, fc_b, N, alpha, precision=0, info=None):
         lib = _native.load()
         dev = X.device
         B = X.shape[0]
         H = w_hh0.shape[1]
         dims = make_dims(B, N, H, 3, W_inp.shape[0], alpha, precision=precision)
         need_grad = any(ctx.needs_input_grad[i] for i in (1, 4, 5, 6))
+        if info is None:
+            info = CallInfo(_native.make_options())
+        opts = info.opts
         try:
-            ws = torch.empty(_native.workspace_bytes(dims, need_grad), dtype=torch.uint8, device=dev)
+            ws = torch.empty(_native.workspace_bytes(dims, need_grad, opts), dtype=torch.uint8, device=dev)
         except torch.cuda.OutOfMemoryError:
-            # H > 52: the kept windows (fcr_set_wide_keep_budget) did not fit beside the caller's tensors; the
-            # floor workspace recomputes every window instead (the kernels derive the count from ws_bytes)
-            prev = _native.set_wide_keep_budget(0)
-            try:
-                ws = torch.empty(_native.workspace_bytes(dims, need_grad), dtype=torch.uint8, device=dev)
-            finally:
-                _native.set_wide_keep_budget(prev)
+            # H > 52: the kept windows did not fit beside the caller's tensors; the floor workspace recomputes every
+            # window instead (the kernels derive the count from ws_bytes). This call's options only.
+            floor = _native.FcrOptions(opts.small_batch_limit, 0, 0)
+            ws = torch.empty(_native.workspace_bytes(dims, need_grad, floor), dtype=torch.uint8, device=dev)
+        info.workspace_bytes = ws.numel()
+        info.kept_windows = _native.kept_windows(dims, ws.numel()) if need_grad else 0
         f32 = dict(dtype=torch.float32, device=dev)
         loss = torch.empty((), **f32)
         cost = torch.empty(B, **f32)
@@ -76,10 +90,11 @@ class RolloutFn(torch.autograd.Function):
         w.fc_w, w.fc_b = keep[9].data_ptr(), keep[10].data_ptr()
         Xc, u0c, stc = X.contiguous(), u0.contiguous(), states.contiguous()
         nzc = noise.contiguous() if noise is not None else None
-        _native.check(lib.fcr_forward(ctypes.byref(dims), ctypes.byref(w), _ptr(Xc), _ptr(u0c), _ptr(stc),
-                                      _ptr(nzc), _ptr(loss), _ptr(cost), _ptr(command), _ptr(error),
+        _native.check(lib.fcr_forward(ctypes.byref(dims), ctypes.byref(opts), ctypes.byref(w), _ptr(Xc), _ptr(u0c),
+                                      _ptr(stc), _ptr(nzc), _ptr(loss), _ptr(cost), _ptr(command), _ptr(error),
                                       _ptr(prediction), _ptr(xhat), int(need_grad), _ptr(ws), ws.numel(),
                                       _stream(dev)), "fcr_forward")
+        info.forward, info.backward = _native.KERNEL_FAMILIES[opts.kernels], None
         ctx.mark_non_differentiable(cost, command, error, prediction, xhat)
         # only loss carries a gradient: without this autograd launches a zero-fill kernel per output
         # before every backward (six per step, ~3 us each at the reference's B = 15)
@@ -87,6 +102,7 @@ class RolloutFn(torch.autograd.Function):
         if need_grad:
             ctx.ws = ws
             ctx.dims = dims
+            ctx.info = info
             ctx.save_for_backward(Xc, stc, prediction)
             ctx.ctrl_shapes = (W_inp.shape, b_inp.shape, W_out.shape)
         return loss, cost, command, error, prediction, xhat
@@ -95,7 +111,7 @@ class RolloutFn(torch.autograd.Function):
     def backward(ctx, g_loss, *unused):
         if g_loss is None:   # (materialize_grads off) nothing flowed into loss
             ctx.ws = None
-            return (None,) * 18
+            return (None,) * 19
         lib = _native.load()
         Xc, stc, prediction = ctx.saved_tensors
         dev = Xc.device
@@ -107,21 +123,26 @@ class RolloutFn(torch.autograd.Function):
         g_bi = torch.empty(s_bi, **f32)
         g_wo = torch.empty(s_wo, **f32)
         dl = g_loss.detach().to(torch.float32).reshape(1).contiguous()
-        _native.check(lib.fcr_backward(ctypes.byref(ctx.dims), _ptr(Xc), _ptr(stc), _ptr(prediction), _ptr(dl),
-                                       _ptr(g_u0), _ptr(g_wi), _ptr(g_bi), _ptr(g_wo), _ptr(ctx.ws),
-                                       ctx.ws.numel(), _stream(dev)), "fcr_backward")
+        info = ctx.info
+        # the forward's options (this call's, not process state): the autograd thread sees what the caller set
+        opts = _native.FcrOptions(info.opts.small_batch_limit, 0, info.opts.wide_keep_budget)
+        _native.check(lib.fcr_backward(ctypes.byref(ctx.dims), ctypes.byref(opts), _ptr(Xc), _ptr(stc),
+                                       _ptr(prediction), _ptr(dl), _ptr(g_u0), _ptr(g_wi), _ptr(g_bi), _ptr(g_wo),
+                                       _ptr(ctx.ws), ctx.ws.numel(), _stream(dev)), "fcr_backward")
+        info.backward = _native.KERNEL_FAMILIES[opts.kernels]
         ctx.ws = None   # release the activation slab as early as autograd lets us
-        return (None, g_u0, None, None, g_wi, g_bi, g_wo) + (None,) * 11
+        return (None, g_u0, None, None, g_wi, g_bi, g_wo) + (None,) * 12
 
 
 PRECISIONS = {"fp32": _native.PRECISION_FP32, "f16": _native.PRECISION_F16, "f16fwd": _native.PRECISION_F16_FWD}
 
 
-def rollout(X, u0, states, ctrl_params, lstm_params, N, alpha, noise=None, precision="fp32"):
+def rollout(X, u0, states, ctrl_params, lstm_params, N, alpha, noise=None, precision="fp32", info=None):
     """Functional entry: ctrl_params = (W_inp, b_inp, W_out), lstm_params = (w_ih[3], w_hh[3], fc_w, fc_b).
     precision: "fp32" (fp32-accurate, the default), "f16fwd" (config 3: f16 gate products in the forward,
     fp32-accurate backward, include/fcr.h FCR_PRECISION_F16_FWD) or "f16" (f16 gate products in both passes,
-    FCR_PRECISION_F16)."""
+    FCR_PRECISION_F16). info: a CallInfo with this call's fcr_options (None: every option inherits the process
+    default); the kernel families it ran are recorded in it."""
     if precision not in PRECISIONS:
         raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {precision!r}")
     w_ih, w_hh, fc_w, fc_b = lstm_params
@@ -145,4 +166,4 @@ def rollout(X, u0, states, ctrl_params, lstm_params, N, alpha, noise=None, preci
                            None if noise is None else _dev_f32(noise, "noise"),
                            *[_dev_f32(t, "controller param") for t in ctrl_params],
                            *[_dev_f32(t, "lstm weight") for t in list(w_ih) + list(w_hh) + [fc_w, fc_b]],
-                           int(N), float(alpha), PRECISIONS[precision])
+                           int(N), float(alpha), PRECISIONS[precision], info)

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define FCR_ABI_VERSION 4
+#define FCR_ABI_VERSION 5
 
 enum {
     FCR_OK = 0,
@@ -84,8 +84,35 @@ typedef struct fcr_weights {
     const float *fc_b;       /* LSTMModel.fc.bias   (out_dim)                                    */
 } fcr_weights;
 
-/* Bytes of scratch a forward (+ backward when with_backward != 0) needs for `dims`. */
-int fcr_workspace_size(const fcr_dims *dims, int with_backward, size_t *bytes);
+/* Per-call kernel options of fcr_workspace_size / fcr_forward / fcr_backward (ABI v5). NULL = every field at
+ * FCR_OPT_INHERIT. Two users of the library in one process (a training rollout and a validation rollout beside it,
+ * on different streams or threads) each pass their own and see nothing of the other's; the process-wide setters
+ * below only supply the defaults a field set to FCR_OPT_INHERIT takes. A forward and its backward should be given the
+ * same options (both kernel families keep one workspace layout, so a mix is valid, only slower).
+ *   small_batch_limit  B <= it runs the small-batch kernels (fp32-accurate mode, H 17..52), 0 = never;
+ *                      negative (FCR_OPT_INHERIT): fcr_set_small_batch_limit's value
+ *   wide_keep_budget   H > 52, read by fcr_workspace_size only: bytes of kept windows the workspace may add;
+ *                      FCR_KEEP_AUTO (-1) the library's policy (fcr_set_wide_keep_budget below), FCR_OPT_INHERIT (-2)
+ *                      the process-wide setting
+ *   kernels            OUT, written by fcr_forward / fcr_backward: the kernel family the call launched
+ *                      (FCR_KERNELS_SMALL, _FUSED or _WIDE) */
+#define FCR_OPT_INHERIT (-2)
+#define FCR_KEEP_AUTO (-1)
+#define FCR_KERNELS_SMALL 1
+#define FCR_KERNELS_FUSED 2
+#define FCR_KERNELS_WIDE 3
+typedef struct fcr_options {
+    int32_t small_batch_limit;
+    int32_t kernels;
+    int64_t wide_keep_budget;
+} fcr_options;
+
+/* Bytes of scratch a forward (+ backward when with_backward != 0) needs for `dims` (and, H > 52, opts' keep budget). */
+int fcr_workspace_size(const fcr_dims *dims, const fcr_options *opts, int with_backward, size_t *bytes);
+
+/* H > 52: how many of the N windows a backward-enabled workspace of ws_bytes keeps (the forward and the backward
+ * each derive this count from the ws_bytes they are given; 0 for H <= 52). */
+int fcr_wide_kept_windows(const fcr_dims *dims, size_t ws_bytes, int32_t *kept);
 
 /*
  * Forward rollout = MPCLoss.forward (Functions.py:1353-1472).
@@ -100,7 +127,7 @@ int fcr_workspace_size(const fcr_dims *dims, int with_backward, size_t *bytes);
  * with_backward != 0 keeps the activations fcr_backward needs in `ws` (which must then not be
  * reused until fcr_backward has run).
  */
-int fcr_forward(const fcr_dims *dims, const fcr_weights *w,
+int fcr_forward(const fcr_dims *dims, fcr_options *opts, const fcr_weights *w,
                 const float *X, const float *u0, const float *states, const float *noise,
                 float *loss, float *cost, float *command, float *error,
                 float *prediction, float *xhat,
@@ -114,7 +141,7 @@ int fcr_forward(const fcr_dims *dims, const fcr_weights *w,
  * reference computes them but nothing reads them: UL/Main.py:195 optimises only the controller).
  * Parameter gradients are OVERWRITTEN (not accumulated); reduction order is fixed (deterministic).
  */
-int fcr_backward(const fcr_dims *dims,
+int fcr_backward(const fcr_dims *dims, fcr_options *opts,
                  const float *X, const float *states, const float *prediction,
                  const float *dloss,
                  float *g_u0, float *g_w_inp, float *g_b_inp, float *g_w_out,
@@ -224,23 +251,14 @@ int fcr_lstm_backward(const fcr_dims *dims, const fcr_weights *w, const float *d
                       void *ws, size_t ws_bytes, void *stream);
 
 /*
- * Kernel choice for small batches (fp32-accurate mode, H 17..52): B <= max_batch runs the small-batch
- * kernels, which split each 16-trajectory group's cell over the four waves of a workgroup (the reference
- * trains at B = 15, UL/Main.py:84,297); larger B runs the fused one-wave-per-group kernels. Default 8192;
- * 0 = never. Both kernel families keep the same workspace
- * layout, so a change between a forward and its backward is harmless. Returns the previous limit.
- * PROCESS-WIDE (an atomic, not per thread): torch runs the backward of device tensors on its autograd worker
- * thread, so a per-thread setting made by the caller would reach only the forward.
+ * Process-wide DEFAULTS of the per-call options (a field set to FCR_OPT_INHERIT takes them).
+ * Small batches (fp32-accurate mode, H 17..52): B <= max_batch runs the small-batch kernels, which split each
+ * 16-trajectory group's cell over the four waves of a workgroup (the reference trains at B = 15, UL/Main.py:84,297);
+ * larger B runs the fused one-wave-per-group kernels. Default 8192; 0 = never (negative clamps to 0). Returns the
+ * previous value; fcr_get_small_batch_limit reads it without changing it.
  */
 int fcr_set_small_batch_limit(int32_t max_batch);
-
-/* Which kernel family the last fcr_forward (bits 0-3) and fcr_backward (bits 4-7) of the process launched:
- * FCR_KERNELS_SMALL (the small-batch kernels), _FUSED (the fused one-wave-per-group kernels) or _WIDE (H > 52,
- * the batch-wide GEMM path); 0 before the first call. A debug query (tests assert the intended family ran). */
-#define FCR_KERNELS_SMALL 1
-#define FCR_KERNELS_FUSED 2
-#define FCR_KERNELS_WIDE 3
-int fcr_last_kernels(void);
+int fcr_get_small_batch_limit(void);
 
 /*
  * H > 52 (the batch-wide GEMM path): how many bytes of "kept windows" fcr_workspace_size(with_backward = 1)
@@ -248,14 +266,14 @@ int fcr_last_kernels(void);
  * floor); a kept window instead holds the forward's gate pre-activations and c for all its 30 cells
  * (30 B 5H floats: 10 GB at B = 65 536, H = 256 — torch's autograd keeps at least that for every window),
  * so its backward skips the recompute (config 5: a third of the step). The last windows are kept, as many
- * as the budget allows; fcr_forward / fcr_backward derive the count from the ws_bytes they are given.
- * bytes < 0 (default): as many as keep the whole workspace within half of the memory that was free on the
- * device when a workspace was first sized there (cached per device: a stable count from call to call), and
- * within 40 % of the device's total memory; 0: keep none. The workspace stays allocated from the forward until
- * its backward has run (torch: until RolloutFn.backward releases it).
- * Process-wide. Returns the previous budget.
+ * as the budget allows (fcr_wide_kept_windows).
+ * bytes < 0 (FCR_KEEP_AUTO, the default): as many as keep the whole workspace within half of the memory that was
+ * free on the device when a workspace was first sized there (cached per device: a stable count from call to call),
+ * and within 40 % of the device's total memory; 0: keep none. The workspace stays allocated from the forward until
+ * its backward has run (torch: until RolloutFn.backward releases it). Returns the previous budget.
  */
 int64_t fcr_set_wide_keep_budget(int64_t bytes);
+int64_t fcr_get_wide_keep_budget(void);
 
 /* Thread-local description of the last error (never NULL). */
 const char *fcr_last_error(void);

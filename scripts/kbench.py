@@ -27,9 +27,10 @@ _n = fca._native
 def bind(path):
     lib = ctypes.CDLL(os.path.abspath(path))
     vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
-    lib.fcr_workspace_size.argtypes = [ctypes.POINTER(_n.FcrDims), i32, ctypes.POINTER(sz)]
-    lib.fcr_forward.argtypes = [ctypes.POINTER(_n.FcrDims), ctypes.POINTER(_n.FcrWeights)] + [vp] * 10 + [i32, vp, sz, vp]
-    lib.fcr_backward.argtypes = [ctypes.POINTER(_n.FcrDims)] + [vp] * 8 + [vp, sz, vp]
+    po = ctypes.POINTER(_n.FcrOptions)   # ABI v5 (include/fcr.h)
+    lib.fcr_workspace_size.argtypes = [ctypes.POINTER(_n.FcrDims), po, i32, ctypes.POINTER(sz)]
+    lib.fcr_forward.argtypes = [ctypes.POINTER(_n.FcrDims), po, ctypes.POINTER(_n.FcrWeights)] + [vp] * 10 + [i32, vp, sz, vp]
+    lib.fcr_backward.argtypes = [ctypes.POINTER(_n.FcrDims), po] + [vp] * 8 + [vp, sz, vp]
     lib.fcr_last_error.restype = ctypes.c_char_p
     return lib
 
@@ -44,8 +45,11 @@ def main(return_state=False):
     ap.add_argument("--sustain", type=int, default=0, help="then time this many back-to-back launches per lib")
     ap.add_argument("--precision", type=int, default=0, help="0 = fp32-accurate, 1 = f16 (config 3)")
     ap.add_argument("--keep-budget", type=int, default=None,
-                    help="fcr_set_wide_keep_budget bytes (H > 52: kept windows skip the backward recompute)")
+                    help="fcr_options.wide_keep_budget bytes (H > 52: kept windows skip the backward recompute)")
+    ap.add_argument("--small-limit", type=int, default=None, help="fcr_options.small_batch_limit")
     a = ap.parse_args()
+    opts = _n.make_options(a.small_limit, a.keep_budget)
+    o = ctypes.byref(opts)
     dev = torch.device("cuda", 0)
     B, N, H = a.batch, a.horizon, a.hidden
     sim, ctrl = load_weights(dev, H)
@@ -63,12 +67,8 @@ def main(return_state=False):
     libs = [bind(p) for p in a.libs]
     need = []
     for lib in libs:
-        if a.keep_budget is not None and hasattr(lib, "fcr_set_wide_keep_budget"):
-            lib.fcr_set_wide_keep_budget.argtypes = [ctypes.c_int64]
-            lib.fcr_set_wide_keep_budget.restype = ctypes.c_int64
-            lib.fcr_set_wide_keep_budget(a.keep_budget)
         nb = ctypes.c_size_t()
-        lib.fcr_workspace_size(ctypes.byref(dims), 1, ctypes.byref(nb))
+        lib.fcr_workspace_size(ctypes.byref(dims), o, 1, ctypes.byref(nb))
         need.append(nb.value)
     nbytes = ctypes.c_size_t(max(need))
     print(f"# workspace {nbytes.value / 2**30:.1f} GiB", flush=True)
@@ -87,11 +87,11 @@ def main(return_state=False):
     for rnd in range(a.rounds + 1):
         for i, lib in enumerate(libs):
             ev[0].record()
-            rc = lib.fcr_forward(ctypes.byref(dims), ctypes.byref(w), p(X), p(u0), p(S), None, p(outs["loss"]),
+            rc = lib.fcr_forward(ctypes.byref(dims), o, ctypes.byref(w), p(X), p(u0), p(S), None, p(outs["loss"]),
                                  p(outs["cost"]), p(outs["command"]), p(outs["error"]), p(outs["pred"]),
                                  p(outs["xhat"]), 1, p(ws), nbytes, st)
             ev[1].record()
-            rc |= lib.fcr_backward(ctypes.byref(dims), p(X), p(S), p(outs["pred"]), p(dl), p(outs["gu0"]),
+            rc |= lib.fcr_backward(ctypes.byref(dims), o, p(X), p(S), p(outs["pred"]), p(dl), p(outs["gu0"]),
                                    p(outs["gwi"]), p(outs["gbi"]), p(outs["gwo"]), p(ws), nbytes, st)
             ev[2].record()
             torch.cuda.synchronize()
@@ -111,11 +111,11 @@ def main(return_state=False):
             evs = [torch.cuda.Event(enable_timing=True) for _ in range(2 * a.sustain + 1)]
             evs[0].record()
             for k in range(a.sustain):
-                lib.fcr_forward(ctypes.byref(dims), ctypes.byref(w), p(X), p(u0), p(S), None, p(outs["loss"]),
+                lib.fcr_forward(ctypes.byref(dims), o, ctypes.byref(w), p(X), p(u0), p(S), None, p(outs["loss"]),
                                 p(outs["cost"]), p(outs["command"]), p(outs["error"]), p(outs["pred"]),
                                 p(outs["xhat"]), 1, p(ws), nbytes, st)
                 evs[2 * k + 1].record()
-                lib.fcr_backward(ctypes.byref(dims), p(X), p(S), p(outs["pred"]), p(dl), p(outs["gu0"]),
+                lib.fcr_backward(ctypes.byref(dims), o, p(X), p(S), p(outs["pred"]), p(dl), p(outs["gu0"]),
                                  p(outs["gwi"]), p(outs["gbi"]), p(outs["gwo"]), p(ws), nbytes, st)
                 evs[2 * k + 2].record()
             torch.cuda.synchronize()

@@ -33,7 +33,7 @@ libs = [bind(p) for p in sys.argv[1:3]]
 sizes = []
 for lib in libs:
     nb = ctypes.c_size_t()
-    assert lib.fcr_workspace_size(ctypes.byref(dims), 1, ctypes.byref(nb)) == 0
+    assert lib.fcr_workspace_size(ctypes.byref(dims), None, 1, ctypes.byref(nb)) == 0
     sizes.append(nb.value)
 print("workspace sizes", sizes)
 f32 = dict(dtype=torch.float32, device=dev)
@@ -45,9 +45,9 @@ for lib in libs:
     o = {k: torch.zeros(s, **f32) for k, s in dict(loss=(), cost=B, command=B, error=B, pred=B * N, xhat=(B, N, 4),
                                                    gu0=(B, 1), gwi=(50, 3), gbi=(50,), gwo=(1, 50)).items()}
     dl = torch.ones(1, **f32)
-    rc = lib.fcr_forward(ctypes.byref(dims), ctypes.byref(w), p(X), p(u0), p(S), None, p(o["loss"]), p(o["cost"]),
+    rc = lib.fcr_forward(ctypes.byref(dims), None, ctypes.byref(w), p(X), p(u0), p(S), None, p(o["loss"]), p(o["cost"]),
                          p(o["command"]), p(o["error"]), p(o["pred"]), p(o["xhat"]), 1, p(ws), ws.numel(), st)
-    rc |= lib.fcr_backward(ctypes.byref(dims), p(X), p(S), p(o["pred"]), p(dl), p(o["gu0"]), p(o["gwi"]), p(o["gbi"]),
+    rc |= lib.fcr_backward(ctypes.byref(dims), None, p(X), p(S), p(o["pred"]), p(dl), p(o["gu0"]), p(o["gwi"]), p(o["gbi"]),
                            p(o["gwo"]), p(ws), ws.numel(), st)
     torch.cuda.synchronize()
     assert rc == 0, lib.fcr_last_error()

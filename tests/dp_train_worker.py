@@ -48,15 +48,41 @@ def global_batches(seed=0):
     return out
 
 
-def train(loader, grad_sync=None, epochs=2):
+class EagerCapturedStep(fca.graphed.CapturedStep):
+    """The captured-step path of train_model (``step=``: _train_model_captured, CapturedStep.skip_empty) with the
+    graph replay replaced by the same step run eagerly, so it runs on the CPU under gloo (the graphs themselves are
+    covered on the GPU by tests/test_graphed.py)."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        for group in self.optimizer.param_groups:   # no graph here: AdamW keeps its host-side step (CPU params)
+            group["capturable"] = False
+
+    def __call__(self, *batch):
+        if batch[0].shape[0] == 0:   # as on the device, where the rollout refuses B = 0 (fcr_forward check_dims)
+            raise RuntimeError("CapturedStep called on an empty shard")
+        out = self._eager(batch)
+        return tuple(t.detach() for t in out)
+
+
+def train(loader, grad_sync=None, epochs=2, captured=False):
     torch.manual_seed(11)
     ctrl = fca.FNNModel(3, 50, 1, 1)
     if grad_sync is not None:
         fca.distributed.broadcast_params(ctrl)
     opt = torch.optim.AdamW(ctrl.parameters(), lr=1e-2)
     sim = surrogate()
-    losses = [fca.NeuralNetwork.train_model(loader, sim, ctrl, fca.MPCLoss(N_HORIZON, ALPHA), opt, "cpu",
-                                            grad_sync=grad_sync)[0]
+    loss_fn = fca.MPCLoss(N_HORIZON, ALPHA)
+    step = None
+    if captured:
+        def body(X, z):
+            loss, f = loss_fn(sim, ctrl, X, ctrl(X), z, "cpu")
+            loss.backward()
+            return (loss.detach(), f["loss"], f["command"], f["error"], f["prediction"])
+        sync = (lambda X, z: grad_sync(ctrl, X.shape[0])) if grad_sync is not None else None
+        step = EagerCapturedStep(ctrl.parameters(), opt, body, sync)
+    losses = [fca.NeuralNetwork.train_model(loader, sim, ctrl, loss_fn, opt, "cpu", grad_sync=grad_sync,
+                                            step=step)[0]
               for _ in range(epochs)]
     return torch.cat([p.detach().reshape(-1) for p in ctrl.parameters()]).numpy(), np.array(losses)
 
@@ -65,6 +91,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ranks", type=int, default=2)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--captured", action="store_true", help="train through the captured-step path (step=...)")
     args = ap.parse_args()
     if "WORLD_SIZE" not in os.environ:
         sys.exit(fca.launch.spawn_ranks(args.ranks, os.path.abspath(__file__), sys.argv[1:], timeout=300))
@@ -75,7 +102,7 @@ def main():
     for X, y, z in global_batches():
         lo, hi = fca.distributed.shard_range(X.shape[0], rank, world)
         shard.append((X[lo:hi], y[lo:hi], z[lo:hi]))
-    params, losses = train(shard, fca.distributed.GradAllReduce())
+    params, losses = train(shard, fca.distributed.GradAllReduce(), captured=args.captured)
     np.savez(os.path.join(args.out, f"rank{rank}.npz"), params=params, losses=losses, world=dist.get_world_size())
     dist.destroy_process_group()
 

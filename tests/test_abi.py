@@ -65,7 +65,7 @@ def test_invalid_dims_rejected_with_message(kw, code):
     lib = fca._native.load()
     out = ctypes.c_size_t(0)
     d = dims(**kw)
-    rc = lib.fcr_workspace_size(ctypes.byref(d), 1, ctypes.byref(out))
+    rc = lib.fcr_workspace_size(ctypes.byref(d), None, 1, ctypes.byref(out))
     assert rc == code
     assert lib.fcr_last_error().decode()
 
@@ -74,9 +74,9 @@ def test_null_pointers_rejected_before_any_device_call():
     lib = fca._native.load()
     d = dims(B=16)
     w = fca._native.FcrWeights()
-    rc = lib.fcr_forward(ctypes.byref(d), ctypes.byref(w), *([None] * 10), 1, None, 0, None)
+    rc = lib.fcr_forward(ctypes.byref(d), None, ctypes.byref(w), *([None] * 10), 1, None, 0, None)
     assert rc == -1 and "NULL" in lib.fcr_last_error().decode()
-    rc = lib.fcr_backward(ctypes.byref(d), *([None] * 8), None, 0, None)
+    rc = lib.fcr_backward(ctypes.byref(d), None, *([None] * 8), None, 0, None)
     assert rc == -1
 
 
@@ -106,15 +106,14 @@ def test_fnn_model_on_cpu_is_the_torch_module():
     assert torch.equal(m(x), ref)
 
 
-def test_small_batch_limit_is_process_wide():
-    """fcr_set_small_batch_limit (the kernel-family choice) is one process-wide setting: torch runs the
-    backward of device tensors on its autograd worker thread, so a setting made by the caller's thread must be
-    seen there too (a thread-local limit changed only the forward)."""
+def test_process_defaults_have_read_only_getters():
+    """fcr_set_small_batch_limit / fcr_set_wide_keep_budget set the process-wide DEFAULTS of the per-call options;
+    the getters read them without changing them (reading by set-and-restore let another thread see 0)."""
     import threading
     n = fca._native
     prev = n.set_small_batch_limit(77)
     try:
-        assert n.small_batch_limit() == 77
+        assert n.small_batch_limit() == 77 and n.small_batch_limit() == 77
         seen = {}
         th = threading.Thread(target=lambda: seen.setdefault("other", n.small_batch_limit()))
         th.start()
@@ -123,7 +122,27 @@ def test_small_batch_limit_is_process_wide():
         assert n.set_small_batch_limit(-5) == 77 and n.small_batch_limit() == 0   # negative clamps to 0 = never
     finally:
         n.set_small_batch_limit(prev)
+    kb = n.wide_keep_budget()
+    assert kb == -1   # the library's policy
+    assert n.set_wide_keep_budget(123) == -1 and n.wide_keep_budget() == 123
+    n.set_wide_keep_budget(kb)
 
 
-def test_last_kernels_query_before_any_call():
-    assert fca._native.last_kernels() == (None, None)
+def test_options_and_workspace_queries_validate_on_the_host():
+    """Per-call options (fcr_options) reach fcr_workspace_size: an H > 52 backward workspace grows by whole kept
+    windows with the call's budget, and fcr_wide_kept_windows reports the count a workspace holds."""
+    n = fca._native
+    d = dims(B=64, N=4, H=64)
+    floor = n.workspace_bytes(d, True, n.make_options(wide_keep_budget=0))
+    one = n.workspace_bytes(d, True, n.make_options(wide_keep_budget=4 * 3 * 10 * 64 * 5 * 64 + 4096))
+    every = n.workspace_bytes(d, True, n.make_options(wide_keep_budget=1 << 40))
+    assert floor < one < every
+    assert [n.kept_windows(d, b) for b in (floor, one, every)] == [0, 1, 4]
+    assert n.kept_windows(dims(B=64), 1 << 30) == 0                 # H <= 52: no kept windows
+    with pytest.raises(ValueError):
+        n.make_options(wide_keep_budget=-7)
+    with pytest.raises(ValueError):
+        n.make_options(small_batch_limit=-1)
+    o = n.make_options()
+    assert (o.small_batch_limit, o.wide_keep_budget, o.kernels) == (n.OPT_INHERIT, n.OPT_INHERIT, 0)
+    assert n.make_options(wide_keep_budget="auto").wide_keep_budget == n.KEEP_AUTO

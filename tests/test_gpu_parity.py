@@ -39,11 +39,13 @@ def modules(params, dev=DEV):
     return sim, ctrl
 
 
-def run(params, X, u0, states, N, alpha, noise=None, dloss=1.0):
+def run(params, X, u0, states, N, alpha, noise=None, dloss=1.0, **loss_kw):
+    """One MPCLoss forward + backward on the GPU; loss_kw: its per-call kernel options (small_batch_limit,
+    wide_keep_budget). out["families"] = the kernel family (forward, backward) the call launched."""
     sim, ctrl = modules(params)
     d = lambda a: torch.as_tensor(np.asarray(a, np.float32), device=DEV)
     u0_t = d(u0).reshape(-1, 1).requires_grad_(True)
-    fn = fca.MPCLoss(prediction_horizon=N, alpha=alpha)
+    fn = fca.MPCLoss(prediction_horizon=N, alpha=alpha, **loss_kw)
     loss, feats = fn(sim, ctrl, d(X), u0_t, d(states), DEV, enable_noise=noise is not None,
                      noise=None if noise is None else d(noise))
     (loss * dloss).backward()
@@ -56,6 +58,8 @@ def run(params, X, u0, states, N, alpha, noise=None, dloss=1.0):
         mod, attr = name.split(".")
         out[k] = getattr(getattr(ctrl, mod), attr).grad.cpu().numpy()
     out["lstm_grad_untouched"] = all(p.grad is None for p in sim.parameters())
+    out["families"] = (fn.last_call.forward, fn.last_call.backward)
+    out["kept_windows"] = fn.last_call.kept_windows
     return out
 
 
@@ -267,24 +271,24 @@ def test_wide_path_hidden_sizes(H, B, N):
 
 
 def test_wide_path_kept_windows_equal_recompute():
-    """H > 52: windows whose cell state the forward keeps (fcr_set_wide_keep_budget) skip the backward's
-    recompute; the kept pre-activations and c are the recompute's, so every output and gradient is the same
-    bit for bit with none, one or all windows kept, and all match the fp64 oracle."""
+    """H > 52: windows whose cell state the forward keeps (MPCLoss(wide_keep_budget=...), fcr_options) skip the
+    backward's recompute; the kept pre-activations and c are the recompute's, so every output and gradient is the
+    same bit for bit with none, one or all windows kept, and all match the fp64 oracle. The budget is the call's
+    own: the process-wide default is left untouched."""
     from tests.golden.make_golden import synth_params
     H, B, N = 64, 200, 4
     params = synth_params(H, 364)
     X, S, _ = _synth(B, N, 464)
     u0 = _u0(params, X)
+    default = fca._native.wide_keep_budget()
     outs = []
-    try:
-        for budget in (0, 1, 1 << 40):   # none; smaller than one window (none); all windows
-            fca._native.set_wide_keep_budget(budget)
-            outs.append(run(params, X, u0, S, N, 20.0))
-        per_window = 4 * 3 * 10 * B * 5 * H   # bytes of one kept window
-        fca._native.set_wide_keep_budget(per_window + 4096)   # exactly one window (the last)
-        outs.append(run(params, X, u0, S, N, 20.0))
-    finally:
-        fca._native.set_wide_keep_budget(-1)
+    per_window = 4 * 3 * 10 * B * 5 * H   # bytes of one kept window
+    # none; smaller than one window (none); all windows; exactly one window (the last)
+    for budget, kept in ((0, 0), (1, 0), (1 << 40, N), (per_window + 4096, 1)):
+        o = run(params, X, u0, S, N, 20.0, wide_keep_budget=budget)
+        assert o["kept_windows"] == kept and o["families"] == ("wide", "wide"), (budget, o["kept_windows"])
+        outs.append(o)
+    assert fca._native.wide_keep_budget() == default
     for o in outs[1:]:
         for k in FEATS + ("xhat",) + tuple(k for k, _ in GRADS):
             assert np.array_equal(o[k], outs[0][k]), k

@@ -7,7 +7,7 @@ case, and agree with each other to ~1e-7 (the same per-tile MFMA chains and poin
 compiler's fma contraction in each instance; the backward's cross-wave partial sums in another fp32 order). The two families share
 the workspace layout, so a forward of one and a backward of the other also pass.
 """
-import contextlib
+import threading
 
 import numpy as np
 import pytest
@@ -21,15 +21,6 @@ from test_gpu_parity import DEV, FEATS, GRADS, TOL, _synth, _u0, modules, run
 pytestmark = pytest.mark.gpu
 native = fca._native
 BIG = 1 << 30
-
-
-@contextlib.contextmanager
-def small_limit(n):
-    prev = native.set_small_batch_limit(n)
-    try:
-        yield
-    finally:
-        native.set_small_batch_limit(prev)
 
 
 FUSED_CASES = [n for n in case_names() if load_case(n)[0]["H"] <= 52]
@@ -47,11 +38,10 @@ def test_small_and_fused_kernels_meet_oracle(name):
     c, params = load_case(name)
     outs = {}
     for lim in (0, BIG):
-        with small_limit(lim):
-            o = run(params, c["X"], c["u0"], c["states"], c["N"], c["alpha"], c["noise"])
+        o = run(params, c["X"], c["u0"], c["states"], c["N"], c["alpha"], c["noise"], small_batch_limit=lim)
         # the small-batch family is built for the 8- and 13-slot tiers (H 17..52); H <= 16 stays fused
         fam = "small" if lim and c["H"] > 16 else "fused"
-        assert native.last_kernels() == (fam, fam), (name, lim, native.last_kernels())   # both passes ran it
+        assert o["families"] == (fam, fam), (name, lim, o["families"])   # both passes ran it
         _check_oracle(o, c, name, fam)
         outs[lim] = o
     for k in FEATS + ("xhat",):
@@ -61,15 +51,17 @@ def test_small_and_fused_kernels_meet_oracle(name):
 
 
 def _run_mixed(params, X, u0, S, N, lim_fwd, lim_bwd):
+    """A forward of one family and a backward of the other: the call's options changed between the passes
+    (RolloutFn carries them from the forward to its backward, so this is the only way to mix them)."""
     sim, ctrl = modules(params)
     d = lambda a: torch.as_tensor(np.asarray(a, np.float32), device=DEV)
     u0_t = d(u0).reshape(-1, 1).requires_grad_(True)
-    with small_limit(lim_fwd):
-        loss, feats = fca.MPCLoss(prediction_horizon=N, alpha=20.0)(sim, ctrl, d(X), u0_t, d(S), DEV)
-    with small_limit(lim_bwd):
-        loss.backward()
+    fn = fca.MPCLoss(prediction_horizon=N, alpha=20.0, small_batch_limit=lim_fwd)
+    loss, feats = fn(sim, ctrl, d(X), u0_t, d(S), DEV)
+    fn.last_call.opts.small_batch_limit = lim_bwd
+    loss.backward()
     torch.cuda.synchronize()
-    out = {"g_u0": u0_t.grad.reshape(-1).cpu().numpy(), "families": native.last_kernels()}
+    out = {"g_u0": u0_t.grad.reshape(-1).cpu().numpy(), "families": (fn.last_call.forward, fn.last_call.backward)}
     for k, name in GRADS[1:]:
         mod, attr = name.split(".")
         out[k] = getattr(getattr(ctrl, mod), attr).grad.cpu().numpy()
@@ -93,8 +85,8 @@ def test_small_kernels_ragged_and_hidden_sizes(H, B, N):
     params = load_case("ref_b15_n10")[1] if H == 50 else synth_params(H, 500 + H)
     X, S, _ = _synth(B, N, 600 + H + B)
     u0 = _u0(params, X)
-    with small_limit(BIG):
-        o = run(params, X, u0, S, N, 20.0)
+    o = run(params, X, u0, S, N, 20.0, small_batch_limit=BIG)
+    assert o["families"] == ("small", "small")
     _, f, tape = R.rollout_forward(params, X, u0, S, N, 20.0)
     g = R.rollout_backward(params, tape)
     for k in FEATS:
@@ -109,19 +101,59 @@ def test_small_kernels_deterministic_and_dloss_linear():
     B, N = 300, 10
     X, S, _ = _synth(B, N, 77)
     u0 = _u0(params, X)
-    with small_limit(BIG):
-        a = run(params, X, u0, S, N, 20.0)
-        b = run(params, X, u0, S, N, 20.0)
-        c2 = run(params, X, u0, S, N, 20.0, dloss=2.0)
+    a = run(params, X, u0, S, N, 20.0, small_batch_limit=BIG)
+    b = run(params, X, u0, S, N, 20.0, small_batch_limit=BIG)
+    c2 = run(params, X, u0, S, N, 20.0, dloss=2.0, small_batch_limit=BIG)
     for k, _ in GRADS:
         assert np.array_equal(a[k], b[k]), k
         assert np.array_equal(2.0 * a[k], c2[k]), k
 
 
 def test_default_limit_routes_the_reference_batch_to_the_small_kernels():
-    prev = native.set_small_batch_limit(123)
-    assert native.set_small_batch_limit(prev) == 123
-    assert prev == 8192   # process-wide default (tests/test_abi.py)
+    assert native.small_batch_limit() == 8192   # the process-wide default (tests/test_abi.py)
     c, params = load_case("ref_b15_n10")
-    run(params, c["X"], c["u0"], c["states"], c["N"], c["alpha"])
-    assert native.last_kernels() == ("small", "small")
+    o = run(params, c["X"], c["u0"], c["states"], c["N"], c["alpha"])   # options inherit the default
+    assert o["families"] == ("small", "small")
+    prev = native.set_small_batch_limit(0)   # a changed process default reaches calls that inherit it ...
+    try:
+        assert run(params, c["X"], c["u0"], c["states"], c["N"], c["alpha"])["families"] == ("fused", "fused")
+        # ... and not a call that sets its own
+        o2 = run(params, c["X"], c["u0"], c["states"], c["N"], c["alpha"], small_batch_limit=BIG)
+        assert o2["families"] == ("small", "small")
+    finally:
+        native.set_small_batch_limit(prev)
+
+
+def test_two_losses_with_different_options_run_concurrently():
+    """Two MPCLoss users in one process — e.g. a training rollout beside a validation rollout — with DIFFERENT
+    kernel options (small-batch kernels for one, fused for the other), each on its own thread and HIP stream at
+    the same time: each gets its own kernel family in both passes (the autograd thread's backward included) and
+    its own workspace, and its results are bit-identical to running it alone. No process state is changed."""
+    c, params = load_case("ref_b37_n25")
+    args = (params, c["X"], c["u0"], c["states"], c["N"], c["alpha"])
+    alone = {lim: run(*args, small_batch_limit=lim) for lim in (0, BIG)}
+    default = native.small_batch_limit()
+    for rep in range(3):
+        res, errs = {}, []
+        barrier = threading.Barrier(2)
+
+        def worker(lim):
+            try:
+                s = torch.cuda.Stream(DEV)
+                with torch.cuda.stream(s):
+                    barrier.wait()
+                    res[lim] = run(*args, small_batch_limit=lim)
+            except Exception as e:   # surfaced below
+                errs.append(e)
+
+        ts = [threading.Thread(target=worker, args=(lim,)) for lim in (0, BIG)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errs, errs
+        for lim, fam in ((0, "fused"), (BIG, "small")):
+            assert res[lim]["families"] == (fam, fam), (rep, lim, res[lim]["families"])
+            for k in FEATS + ("xhat",) + tuple(k for k, _ in GRADS):
+                assert np.array_equal(res[lim][k], alone[lim][k]), (rep, lim, k)
+    assert native.small_batch_limit() == default

@@ -213,19 +213,22 @@ def test_inference_refuses_cpu_tensors():
         fca.simulate_step(sim, torch.zeros(2, 10, 5))
 
 
-@pytest.mark.parametrize("ranks", [2, 8])
-def test_train_model_data_parallel_through_launcher_gloo(tmp_path, ranks):
+@pytest.mark.parametrize("ranks,captured", [(2, False), (8, False), (8, True)])
+def test_train_model_data_parallel_through_launcher_gloo(tmp_path, ranks, captured):
     """The launcher bench.py --gpus N uses (forging_control_amd.launch) starts N gloo ranks that each run the
     real NeuralNetwork.train_model(grad_sync=GradAllReduce()) with the package's MPCLoss (CPU path) on UNEVEN
     shards of the reference's B = 15 batches (2 ranks: 8/7, last batch 4/3; 8 ranks: 2/2/.../1, and the last
     batch of 7 leaves rank 7 an EMPTY shard, which must still join the all-reduce): after two epochs every rank
-    holds bit-identical parameters equal to one process training on the whole batches."""
+    holds bit-identical parameters equal to one process training on the whole batches. captured: the same through
+    train_model's captured-step path (step=..., graph replay stood in by the eager step on the CPU), whose empty
+    shard must join the all-reduce too (CapturedStep.skip_empty)."""
     import subprocess
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__))))
     import dp_train_worker as W
     script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dp_train_worker.py")
-    rc = subprocess.run([sys.executable, script, "--ranks", str(ranks), "--out", str(tmp_path)], timeout=400).returncode
+    rc = subprocess.run([sys.executable, script, "--ranks", str(ranks), "--out", str(tmp_path)] +
+                        (["--captured"] if captured else []), timeout=400).returncode
     assert rc == 0
     res = [np.load(tmp_path / f"rank{r}.npz") for r in range(ranks)]
     assert all(int(r["world"]) == ranks for r in res)
