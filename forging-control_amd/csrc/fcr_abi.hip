@@ -83,12 +83,10 @@ constexpr int kMaxWideH = 2048;   // H > 4*kMaxSlots: the GEMM-per-cell path (fc
 bool is_wide(const fcr_dims *d) { return d->H > 4 * kMaxSlots; }
 int slot_tier(int H) { return H <= 16 ? 4 : (H <= 32 ? 8 : 13); }
 
-// H > 52: the backward's gradient products on the hand-written split-f16 kernel (fcr_wbwd.h) when its k-blocks
-// tile 4H and layer 0's window-row gradient is formed in the cell kernel (rowg_in_cell); rocBLAS otherwise.
-bool wide_hwbwd_ok(int H) {
-    const bool rowg_cell = H % 4 == 0 && 64 % (H / 4) == 0;   // rowg_in_cell (below)
-    return H % 8 == 0 && rowg_cell;
-}
+// H > 52: each backward cell as ONE hand-written kernel (fcr_wbwd.h: the cell's dgates formed in the prologue of the
+// split-f16 [input grad | dh_{t-1}] product) when a K step of 8 units tiles H and [input grad | dh] fits the two
+// column blocks of its row bounds; rocBLAS products + wide_cell_bwd_kernel otherwise.
+bool wide_fused_bwd_ok(int H) { return H % 8 == 0 && H <= kWbMaxH; }
 
 int check_dims(const fcr_dims *d) {
     if (!d) return fail(FCR_EINVAL, "dims is NULL");
@@ -263,8 +261,9 @@ struct WideLayout {
     size_t Act, dH, dC, D[2], rowg, dv, fnn_part, wsc, rng, total;
     // split-f16 gate GEMM operands (fcr_wide.h: forward A per layer, backward A per weight, the cells'
     // operand rows XB [3][10][B][6H] (layer 0 rows 3H + kX16 long), the dgate rows [B][12H])
-    size_t fa[3], bih[3], XB, dGsp, consts, rsc;   // bih: layers >= 1 backward A [12H][2H]
-    size_t bt[3];     // hand-written gradient product (fcr_wbwd.h): W^T split [NO][4H] hi, then lo
+    size_t fa[3], bih[3], XB, dGsp, consts;   // bih: layers >= 1 backward A [12H][2H]
+    size_t bt[3];     // fused backward cell (fcr_wbwd.h): W^T split [NO][4H] hi, then lo (unit-major K)
+    size_t DC2, RMc, RMh, RMd;   // fused: the second dc buffer, the row bounds [2][B], [2][2][B], [2][kL][2][B]
     size_t bx0, E0;   // layer 0's backward A [12H][H + 8] and its product rows [B][H + 8]
     // kept windows (the last `keep` of N): the forward's gate pre-activations and c per cell
     // [keep][3][10][B][4H] / [keep][3][10][B][H], so the backward skips their recompute (wide_keep_fit)
@@ -305,7 +304,7 @@ WideLayout make_wide(const fcr_dims *d, int with_backward, int keep = 0) {
     L.Cs = take(F * kLayers * kL * B * H);
     L.G = take(F * B * 4 * H);
     const size_t F16 = sizeof(_Float16), WW = 4 * H * H;
-    const bool hw = wide_hwbwd_ok((int)H);
+    const bool hw = wide_fused_bwd_ok((int)H);
     for (int l = 0; l < kLayers; ++l) {
         L.fa[l] = take(l == 0 ? F16 * 4 * H * (3 * H + kX16) : F16 * WW * 6);
         if (with_backward && hw) {
@@ -320,10 +319,16 @@ WideLayout make_wide(const fcr_dims *d, int with_backward, int keep = 0) {
     }
     L.XB = take(F16 * kLayers * kL * B * 6 * H);
     if (with_backward) {
-        L.dGsp = take(F16 * B * 12 * H);
+        if (hw) {
+            L.DC2 = take(F * B * H);
+            L.RMc = take(F * 2 * B);
+            L.RMh = take(F * 4 * B);
+            L.RMd = take(F * 4 * kL * B);
+        } else {
+            L.dGsp = take(F16 * B * 12 * H);
+        }
         L.E0 = take(F * B * ((H + 8 + 31) / 32 * 32));
         L.consts = take(F * 4);
-        L.rsc = take(F * (size_t)d->B);   // per-row dgate scales of the hand-written backward product
         L.Act = take(F * kLayers * kL * B * 4 * H);
         L.dH = take(F * B * H);
         L.dC = take(F * B * H);
@@ -447,7 +452,7 @@ int gemm16_bwd(rocblas_handle h, int B, int n, int H, const _Float16 *A, int lda
 struct WideSplit {
     const _Float16 *fa[kLayers], *bih[kLayers], *bt[kLayers];
     _Float16 *XB, *dGsp;
-    float *consts, *rsc;
+    float *consts;
     const _Float16 *bx0;
     float *E0;
 };
@@ -462,7 +467,6 @@ WideSplit wide_split(const WideLayout &L, char *base) {
     w.XB = (_Float16 *)(base + L.XB);
     w.dGsp = L.dGsp ? (_Float16 *)(base + L.dGsp) : nullptr;
     w.consts = L.consts ? (float *)(base + L.consts) : nullptr;
-    w.rsc = (L.rsc && w.bt[0]) ? (float *)(base + L.rsc) : nullptr;   // the hand-written product only
     w.bx0 = L.bx0 ? (const _Float16 *)(base + L.bx0) : nullptr;
     w.E0 = L.E0 ? (float *)(base + L.E0) : nullptr;
     return w;
@@ -479,7 +483,7 @@ int wide_pack_split(const float *const *w_ih, const float *const *w_hh, int H, b
                            (int)(l == 0), wsc, (_Float16 *)sp.fa[l]);
         if ((rc = launch_check("wide_split_fa_kernel"))) return rc;
         if (!backward) continue;
-        if (sp.bt[l]) {   // hand-written gradient product: W^T split, [NO][4H] hi then lo
+        if (sp.bt[l]) {   // fused backward cell: W^T split, [NO][4H] hi then lo, unit-major K
             const int NO = l == 0 ? H : 2 * H;
             const size_t nbt = (size_t)NO * 4 * H;
             _Float16 *hi = (_Float16 *)sp.bt[l];
@@ -552,17 +556,16 @@ constexpr int kRowgT = 4;
 template <bool PRE>
 int launch_cell_bwd(int B, int H, hipStream_t s, const float *act, const float *c, const float *c_prev,
                     const float *dH, const float *din, float *dC, float *dG, _Float16 *dgsp, const float *consts,
-                    int dh_scaled, int ldh, int ldx, const float *wih0 = nullptr, float *rowg = nullptr, int dg3 = 1,
-                    float *rsc = nullptr) {
+                    int dh_scaled, int ldh, int ldx, const float *wih0 = nullptr, float *rowg = nullptr, int dg3 = 1) {
     const int V = cell_vec(H);
     const dim3 grid((unsigned)(((size_t)B * (H / V) + 255) / 256)), blk(256);
-    if ((rowg || rsc) && (V != 4 || 64 % (H / V)))
+    if (rowg && (V != 4 || 64 % (H / V)))
         return fail(FCR_EINVAL, "wide_cell_bwd_kernel: in-kernel row gradient needs 64 %% (H / 4) == 0 (H = %d)", H);
     if (rowg) {   // layer 0: kRowgT trajectories per thread share one load of its W_ih0 rows
         const dim3 g0((unsigned)(((size_t)(B + kRowgT - 1) / kRowgT * (H / V) + 255) / 256));
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4, kRowgT>), g0, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, dg3, wih0, rowg, rsc);
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4, kRowgT>), g0, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, dg3, wih0, rowg);
     } else if (V == 4)
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, dg3, nullptr, nullptr, rsc);
+        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, dg3);
     else if (V == 2)
         hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 2>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, dg3);
     else
@@ -614,36 +617,23 @@ int launch_wgemm_cell(const WgArgs &wa, hipStream_t s) {
     return launch_check("wide_gemm_cell_kernel");
 }
 
-// dX' (row-major [B][ldo], columns [0, NO)) = dGs W on the hand-written split-f16 kernel (fcr_wbwd.h), in the
-// dgates' scaled units like gemm16_bwd; bt = W^T split [NP][4H] hi then lo (NP packed rows; the product uses the
-// first NO <= NP of them), dGs = [hi 4H | lo 4H | (hi 4H)] rows
-int launch_wb(const _Float16 *bt, int NP, int NO, int H, int B, const _Float16 *dGs, float *dX, int ldo, const float *rs,
-              hipStream_t s) {
-    static bool attr_set = false;
-    if (!attr_set) {
-        const hipError_t e = hipFuncSetAttribute((const void *)wide_bwd_gemm_kernel,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kWbLds);
+// One backward cell of the fused path (fcr_wbwd.h): dgates formed in the product's prologue, out = dG [W_ih | W_hh]
+// (columns [0, NO), NO = 0: the dgate part only) in true units
+int launch_fb(const WbArgs &wa, bool l0, hipStream_t s) {
+    static bool attr_set[2] = {false, false};
+    const void *fn = l0 ? (const void *)wide_bwd_fused_kernel<true> : (const void *)wide_bwd_fused_kernel<false>;
+    if (!attr_set[l0]) {
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kWbLds);
         if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(wbwd): %s", hipGetErrorString(e));
-        attr_set = true;
+        attr_set[l0] = true;
     }
-    WbArgs wa{};
-    wa.Ahi = bt;
-    wa.Alo = bt + (size_t)NP * 4 * H;
-    wa.B = dGs;
-    wa.out = dX;
-    wa.lda = 4 * H;
-    wa.ldb = 12 * H;
-    wa.lo_off = 4 * H;
-    wa.rs = rs;
-    wa.ldo = ldo;
-    wa.NB = B;
-    wa.NO = NO;
-    wa.K = 4 * H;
-    if (NO <= 0 || NO > NP || NO % 16 || wa.K % kWbK || B <= 0 || ldo % 4)
-        return fail(FCR_EINVAL, "wide_bwd_gemm_kernel: NO %d K %d B %d ldo %d off its tiling", NO, wa.K, B, ldo);
-    const int nx = (B + kWbN - 1) / kWbN, ny = (NO + kWbM - 1) / kWbM;
-    hipLaunchKernelGGL(wide_bwd_gemm_kernel, dim3((unsigned)(nx * ny)), dim3(kWbThreads), kWbLds, s, wa);
-    return launch_check("wide_bwd_gemm_kernel");
+    if (wa.NO < 0 || wa.NO > 2 * kWbM || wa.NO % 16 || wa.H % 8 || wa.H > kWbMaxH || wa.NB <= 0 || wa.ldo % 4 ||
+        wa.ldh % 2 || wa.ldx % 2 || (l0 && (!wa.wih0 || !wa.rowg)))
+        return fail(FCR_EINVAL, "wide_bwd_fused_kernel: NO %d H %d B %d ldo %d off its tiling", wa.NO, wa.H, wa.NB, wa.ldo);
+    const int nx = (wa.NB + kWbN - 1) / kWbN, ny = wa.NO > 0 ? (wa.NO + kWbM - 1) / kWbM : 1;
+    if (l0) hipLaunchKernelGGL((wide_bwd_fused_kernel<true>), dim3((unsigned)(nx * ny)), dim3(kWbThreads), kWbLds, s, wa);
+    else hipLaunchKernelGGL((wide_bwd_fused_kernel<false>), dim3((unsigned)(nx * ny)), dim3(kWbThreads), kWbLds, s, wa);
+    return launch_check("wide_bwd_fused_kernel");
 }
 
 // One window's cells, forward: 3 layers x 10 steps of [GEMM x_t W_ih^T, GEMM h_{t-1} W_hh^T, cell].
@@ -818,8 +808,14 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
     while (kexp < 60 && (1LL << kexp) < (long long)B * d->N) ++kexp;
     hipLaunchKernelGGL(wide_bscale_kernel, dim3(1), dim3(64), 0, s, dloss, kexp, sp.consts);
     if ((rc = launch_check("wide_bscale_kernel"))) return rc;
+    const bool fused = sp.bt[0] != nullptr;   // wide_fused_bwd_ok: each backward cell one fcr_wbwd.h kernel
+    float *DC[2] = {a.dC, fused ? (float *)(base + L.DC2) : nullptr};
+    float *RMc = fused ? (float *)(base + L.RMc) : nullptr;   // [t & 1][B]      row bound of |dc|
+    float *RMh = fused ? (float *)(base + L.RMh) : nullptr;   // [t & 1][2][B]   of |dh| (per column block)
+    float *RMd = fused ? (float *)(base + L.RMd) : nullptr;   // [l & 1][t][2][B] of |input grad| for the layer below
     for (int j = d->N - 1; j >= 0; --j) {
-        hipLaunchKernelGGL(wide_head_kernel, dim3((unsigned)(((size_t)B * kRoLanes + 255) / 256)), dim3(256), 0, s, a, j);
+        hipLaunchKernelGGL(wide_head_kernel, dim3((unsigned)(((size_t)B * kRoLanes + 255) / 256)), dim3(256), 0, s, a, j,
+                           RMh);   // layer 2's t = 9 reads slot (9 + 1) & 1 = 0
         if ((rc = launch_check("wide_head_kernel"))) return rc;
         if (j >= d->N - L.keep) {   // kept by the forward: no recompute
             a.Act = kept_act(L, base, d, j);
@@ -834,31 +830,69 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
         for (int l = kLayers - 1; l >= 0; --l) {
             if (l < kLayers - 1 && hipMemsetAsync(a.dH, 0, sizeof(float) * cell, s) != hipSuccess)
                 return fail(FCR_EHIP, "hipMemsetAsync failed");
-            if (hipMemsetAsync(a.dC, 0, sizeof(float) * cell, s) != hipSuccess) return fail(FCR_EHIP, "hipMemsetAsync failed");
+            if (hipMemsetAsync(DC[0], 0, sizeof(float) * cell, s) != hipSuccess) return fail(FCR_EHIP, "hipMemsetAsync failed");
+            if (fused && (hipMemsetAsync(RMc, 0, sizeof(float) * B, s) != hipSuccess ||
+                          (l < kLayers - 1 && hipMemsetAsync(RMh, 0, sizeof(float) * 2 * B, s) != hipSuccess)))
+                return fail(FCR_EHIP, "hipMemsetAsync failed");
             for (int t = kL - 1; t >= 0; --t) {
                 const size_t c_off = ((size_t)l * kL + t) * cell;
                 // dh_t below t = 9 comes from cell t+1's combined product: layer 0 columns 0..H-1 of E0, layers
                 // >= 1 columns H..2H-1 of D[l-1] row t+1; the layer above's input gradient from D[l] row t
                 const float *dh_src = t == kL - 1 ? a.dH : l == 0 ? sp.E0 : D[l - 1] + (size_t)(t + 1) * 2 * cell + H;
                 const int ldh = t == kL - 1 ? H : l == 0 ? LE : 2 * H;
+                if (fused) {
+                    const int NP = l == 0 ? H : 2 * H;
+                    WbArgs wa{};
+                    wa.Ahi = sp.bt[l];
+                    wa.Alo = sp.bt[l] + (size_t)NP * 4 * H;
+                    wa.NB = B;
+                    wa.H = H;
+                    wa.pre = a.Act + c_off * 4;
+                    wa.c_prev = t > 0 ? a.Cs + c_off - cell : nullptr;
+                    wa.dh = dh_src;
+                    wa.ldh = ldh;
+                    wa.din = l < kLayers - 1 ? D[l] + (size_t)t * 2 * cell : nullptr;
+                    wa.ldx = 2 * H;
+                    wa.dC = DC[(t + 1) & 1];   // t = 9 reads buffer 0 (zeroed above), t writes buffer t & 1
+                    wa.dC_out = DC[t & 1];
+                    wa.rm_c = RMc + (size_t)((t + 1) & 1) * B;
+                    wa.rm_c_out = t > 0 ? RMc + (size_t)(t & 1) * B : nullptr;
+                    wa.rm_h = RMh + (size_t)((t + 1) & 1) * 2 * B;
+                    wa.rm_h_out = t > 0 ? RMh + (size_t)(t & 1) * 2 * B : nullptr;
+                    wa.rm_d = l < kLayers - 1 ? RMd + ((size_t)((l + 1) & 1) * kL + t) * 2 * B : nullptr;
+                    wa.rm_d_out = l > 0 ? RMd + ((size_t)(l & 1) * kL + t) * 2 * B : nullptr;
+                    if (l > 0) {   // [input gradient | dh_{t-1}] (t = 0: the former only) into D[l-1] row t
+                        wa.out = D[l - 1] + (size_t)t * 2 * cell;
+                        wa.ldo = 2 * H;
+                        wa.NO = t > 0 ? 2 * H : H;
+                        wa.h0 = H;
+                        wa.h1 = t > 0 ? 2 * H : H;
+                        wa.d1 = H;
+                    } else {       // dh_{t-1} into E0 (t = 0: none), and the window-row gradient into rowg row j + t
+                        wa.out = sp.E0;
+                        wa.ldo = LE;
+                        wa.NO = t > 0 ? H : 0;
+                        wa.h0 = 0;
+                        wa.h1 = H;
+                        wa.d1 = 0;
+                        wa.wih0 = wih[0];
+                        wa.rowg = a.rowg + (size_t)(j + t) * B * kIn;
+                    }
+                    if ((rc = launch_fb(wa, l == 0, s))) return rc;
+                    continue;
+                }
                 const bool rg = l == 0 && rowg_in_cell(H);   // layer 0's row gradient from the cell kernel
                 if ((rc = launch_cell_bwd<true>(B, H, s, a.Act + c_off * 4, a.Cs + c_off, t > 0 ? a.Cs + c_off - cell : nullptr,
                                                 dh_src, l < kLayers - 1 ? D[l] + (size_t)t * 2 * cell : nullptr, a.dC,
                                                 nullptr, sp.dGsp, sp.consts,
                                                 l < kLayers - 1 || t < kL - 1,   // (2, 9): the head's dH
                                                 ldh, 2 * H, rg ? wih[0] : nullptr,
-                                                rg ? a.rowg + (size_t)(j + t) * B * kIn : nullptr, sp.bt[0] ? 0 : 1, sp.rsc)))
+                                                rg ? a.rowg + (size_t)(j + t) * B * kIn : nullptr, 1)))
                     return rc;
-                if (l > 0 && sp.bt[l]) {   // [input gradient | dh_{t-1}] (t = 0: the former only), hand-written product
-                    if ((rc = launch_wb(sp.bt[l], 2 * H, t > 0 ? 2 * H : H, H, B, sp.dGsp, D[l - 1] + (size_t)t * 2 * cell, 2 * H,
-                                        sp.rsc, s)))
-                        return rc;
-                } else if (l > 0) {   // [input gradient | dh_{t-1}] (t = 0: the former only) into D[l-1] row t
+                if (l > 0) {   // [input gradient | dh_{t-1}] (t = 0: the former only) into D[l-1] row t
                     if ((rc = gemm16_bwd(h, B, t > 0 ? 2 * H : H, H, sp.bih[l], 2 * H, sp.dGsp, D[l - 1] + (size_t)t * 2 * cell,
                                          2 * H)))
                         return rc;
-                } else if (rg && sp.bt[0]) {   // layer 0, row gradient done: dh_{t-1} only (t = 0: nothing)
-                    if (t > 0 && (rc = launch_wb(sp.bt[0], H, H, H, B, sp.dGsp, sp.E0, LE, sp.rsc, s))) return rc;
                 } else if (rg) {   // layer 0, row gradient done: dh_{t-1} only (t = 0: nothing)
                     if (t > 0 && (rc = gemm16_bwd(h, B, H, H, sp.bx0, H8, sp.dGsp, sp.E0, LE))) return rc;
                 } else {

@@ -1,100 +1,205 @@
-// fcr_wbwd.h — H > 52 (config 5): the backward cell's gradient product [input grad | dh_{t-1}] = dG · [W_ih | W_hh]
-// as ONE hand-written split-f16 MFMA GEMM (in place of rocBLAS gemm16_bwd's Cijk kernels where the shapes allow,
-// fcr_abi.hip wide_hwbwd_ok). Reference: the autograd backward of nn.LSTM inside loss.backward() (Functions.py:325, :655).
+// fcr_wbwd.h — H > 52 (config 5): ONE kernel per backward cell: the cell's gate gradients (the backward of the LSTM
+// cell update, formerly wide_cell_bwd_kernel) formed in the prologue of the gradient product
+// [input grad | dh_{t-1}] = dG · [W_ih | W_hh], so the dgate rows never go to HBM. Reference: the autograd backward of
+// nn.LSTM inside loss.backward() (Functions.py:325, :655).
 //
-// out[b][n] = sum_r dG[b][r] W[r][n] over the 4H gate rows r, fp32-accurate from f16 halves: with dG = dG_hi +
-// dG_lo (the cell kernel's split of dG * scale, wide_cell_bwd_kernel) and W = W_hi + W_lo,
-//   out = W_lo dG_hi + W_hi dG_lo + W_hi dG_hi      (three MFMAs per k-block; the dropped lo·lo is <= 2^-22)
-// Against rocBLAS on the K-concatenated [hi | lo | hi] rows (K = 12H) every hi fragment is read ONCE for its two
-// products, so a workgroup stages 4 halves per (row, k) instead of 6, and the dgate rows need no third copy.
-//
-// Operands (row-major, k contiguous): A = W^T split, [NO][lda] hi and lo (row n = output column: W_ih column n
-// for n < H, W_hh column n - H — wide_split_bt_kernel); B = the dgate rows [B][ldb] hi, lo at +lo_off.
-// MFMA roles: A = W^T (M = output columns), B = dG^T (N = trajectories), D[m][n] = out[b = n][col = m]: a lane's
-// D fragment is 4 consecutive columns of one trajectory row, one 16-B store.
-// Tile: a workgroup owns 256 output columns x 128 trajectories; 8 waves (4 along M x 2 along N), each 64 x 64 =
-// 4 x 4 D tiles; K in steps of 32 (one k-block) through a 3-stage LDS-DMA ring (global_load_lds, 16 B per lane,
-// two steps of prefetch, a bare s_barrier per step) — the staging of fcr_wgemm.h, with hi and lo stages. A stage
-// is 256 + 256 + 128 + 128 rows of 64 B = 48 KB; 3 stages = 144 KB: one workgroup (8 waves, 2 per SIMD) per CU.
-// XCD-aware order: a trajectory block's output-column blocks run on one XCD, so its dgate rows are read from HBM
-// once into that XCD's L2.
+// Product: out[b][n] = sum_r dG[b][r] W[r][n] over the 4H gate rows r, fp32-accurate from f16 halves: with dG = dG_hi
+// + dG_lo (each trajectory row's dgates times its own power of two) and W = W_hi + W_lo,
+//   out = (W_lo dG_hi + W_hi dG_lo + W_hi dG_hi) / scale_b    (three MFMAs per k-block; the dropped lo·lo <= 2^-22)
+// A = W^T split [NP][4H] (row n = output column, W_ih column n for n < H, W_hh column n - H; layer 0: W_hh only) with
+// the K index UNIT-major, r' = 4 unit + gate (wide_split_bt_kernel), so a K step of 32 is 8 whole units: the dgates
+// of one K step need only those units' inputs.
+// Tile: a workgroup owns 256 output columns x 128 trajectories; 8 waves (4 along M x 2 along N), each 64 x 64 = 4 x 4
+// D tiles (lane = trajectory, 4 consecutive columns: one 16-B store). K in steps of 32: A through a 2-stage LDS-DMA
+// ring (W^T is L2-resident); the B tile (the step's dgates, hi | lo) is computed by the workgroup itself, one step
+// ahead of the MFMAs that read it: thread (row r = tid / 4, pair p = tid % 4) loads units 8s + 2p, 8s + 2p + 1 of
+// its trajectory (pre-activations, c_{t-1}, dh, din, dc: 8-B loads, one step ahead in registers), forms
+// the 8 dgates and dc_{t-1} (fcr_wide.h wide_cell_bwd_kernel's algebra, exp2-based activations as fcr_bwd.h), splits
+// them into the 16-B chunk its MFMA lane reads. With two column blocks (NO > 256) both form the same dgates; the
+// first writes dc_{t-1}.
+// Row scale: 2^(13 - e), e the exponent of a bound on the row's |dgates|: |dgate| <= |dc_t| <= |dc| + |dh_rec| +
+// |din| (forget row: x (kL - 1) / 4, fcr_wide.h kWideDgExp). The three maxima come from the kernels that wrote those
+// values (this kernel's epilogue and elementwise part of the previous cell, the head kernel), per row, so no pass
+// over the row precedes the K loop.
 #pragma once
 #include "fcr_common.h"
 #include "fcr_f16.h"
+#include "fcr_wide.h"
 
 namespace fcr {
 
 constexpr int kWbM = 256;                 // output columns per workgroup
 constexpr int kWbN = 128;                 // trajectories per workgroup
-constexpr int kWbK = 32;                  // k per step
+constexpr int kWbK = 32;                  // k per step (8 units x 4 gates)
 constexpr int kWbWM = 4, kWbWN = 2;       // waves along the output columns x along the trajectories
 constexpr int kWbWaves = kWbWM * kWbWN;
 constexpr int kWbTM = kWbM / kWbWM / 16, kWbTN = kWbN / kWbWN / 16;   // D tiles per wave
 constexpr int kWbThreads = 64 * kWbWaves;
 constexpr int kWbStageA = kWbM * kWbK * 2;                // bytes of one split half of A
-constexpr int kWbStageB = kWbN * kWbK * 2;
-constexpr int kWbStage = 2 * kWbStageA + 2 * kWbStageB;   // hi A | lo A | hi B | lo B
-constexpr int kWbStages = 3;
-constexpr int kWbLds = kWbStages * kWbStage;
-constexpr int kWbPieces = kWbStage / 1024 / kWbWaves;     // 1 KB LDS-DMA pieces per wave per stage
+constexpr int kWbStage = 2 * kWbStageA;                   // hi A | lo A
+constexpr int kWbTileB = kWbN * kWbK * 2;                 // one split half of the dgate tile
+constexpr int kWbPieces = kWbStage / 1024 / kWbWaves;     // LDS-DMA pieces per wave per stage
+constexpr int kWbOffB = 2 * kWbStage;                     // [A stage 0 | A stage 1 | B tile 0 hi, lo | B tile 1 ...]
+constexpr int kWbOffDown = kWbOffB + 4 * kWbTileB;
+constexpr int kWbOffW0 = kWbOffDown + kWbN * 4;           // layer 0: W_ih0 as [unit][gate][kIn]
+constexpr int kWbMaxH = 256;                              // NO = 2H <= 2 column blocks (the row bounds' slots)
+constexpr int kWbLds = kWbOffW0 + 4 * kWbMaxH * kIn * 4;
 static_assert(kWbStage % (1024 * kWbWaves) == 0, "DMA pieces");
+static_assert(kWbThreads == 4 * kWbN, "dgate mapping: four threads (two units each) per trajectory row");
 static_assert(kWbLds <= 163840, "LDS");
 
 struct WbArgs {
-    const _Float16 *Ahi, *Alo;   // [NO][lda]
-    const _Float16 *B;           // dgate rows [B][ldb], hi at +0, lo at +lo_off halves
-    float *out;                  // [B][ldo], columns [0, NO)
-    const float *rs;             // [B] per-row factor applied to the output (the dgate rows' own inverse scales), or null
-    int lda, ldb, lo_off, ldo, NB, NO, K;
+    const _Float16 *Ahi, *Alo;   // [NP][4H], unit-major K
+    float *out;                  // [B][ldo], columns [0, NO); NO = 0: no product (layer 0, t = 0)
+    int ldo, NO, NB, H;
+    const float *pre;            // [B][4H] gate pre-activations (i | f | g | o blocks of H) of the cell
+    const float *c_prev;         // [B][H] or null (t = 0)
+    const float *dh;             // [B][ldh] incoming dh of the recurrence (the head's, or the next cell's product)
+    const float *din;            // [B][ldx] the layer above's input gradient at t, or null
+    const float *dC;             // [B][H] carried dc in
+    float *dC_out;               // [B][H] dc_{t-1} out (another buffer: the other column block still reads dC)
+    int ldh, ldx;
+    const float *rm_c, *rm_h, *rm_d;   // row bounds in: max|dc| [B], max|dh| [2][B] (per column block), max|din| [2][B] or null
+    float *rm_c_out, *rm_h_out, *rm_d_out;   // row bounds out (or null): of dc_{t-1}, of the dh / input-grad columns
+    int h0, h1, d1;              // output columns [h0, h1) are dh_{t-1}, [0, d1) the layer below's input gradient
+    const float *wih0;           // layer 0: W_ih0 [4H][kIn] (the window-row gradient), else null
+    float *rowg;                 // layer 0: [B][kIn] window-row gradient row (+=), else null
 };
 
 // byte offset of 16-B chunk c of 64-B LDS row r: the swizzle puts the 8 rows of a fragment read's 8-lane phase
 // on distinct 16-B slots of a 128-B bank line (fcr_wgemm.h wg_off)
 __device__ __forceinline__ uint32_t wb_off(int r, int c) { return (uint32_t)(r * 64 + ((c ^ ((r >> 1) & 3)) << 4)); }
 
-__global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_gemm_kernel(WbArgs a) {
-    static_assert(kWbPieces == 6 || kWbPieces == 12, "vmcnt immediates");
+// one step's inputs of a dgate thread: two consecutive units of one trajectory
+struct WbIn {
+    f32x2 pi, pf, pg, po, cp, dh, dn, dc;
+};
+
+template <bool L0>
+__global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wv % kWbWM, wn = wv / kWbWM;            // column slice, trajectory slice
-    const int ny = (a.NO + kWbM - 1) / kWbM, total = gridDim.x, id = blockIdx.x;
+    const int H = a.H, K = 4 * H, nk = K / kWbK;
+    const bool prod = a.NO > 0;
+    const int ny = prod ? (a.NO + kWbM - 1) / kWbM : 1, total = gridDim.x, id = blockIdx.x;
+    // XCD-aware order: consecutive ids go to different XCDs; each XCD's ids are renumbered contiguously and walk the
+    // column blocks fastest, so a trajectory block's two column blocks read its rows once into that XCD's L2
     const int xcd = id & 7, loc = id >> 3, q8 = total >> 3, rr = total & 7;
     const int wg = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + loc;
-    const int m0 = (wg % ny) * kWbM;                       // first output column
-    const int b0 = (wg / ny) * kWbN;                       // first trajectory
-    const int nk = a.K / kWbK;
+    const int cb = wg % ny;                                 // column block
+    const int m0 = cb * kWbM;                               // first output column
+    const int b0 = (wg / ny) * kWbN;                        // first trajectory
 
-    // DMA piece j of a stage: 16 rows x 64 B of [A hi (16 pieces) | A lo (16) | B hi (8) | B lo (8)]; lane i lands
-    // at +16 i (row i >> 2, slot i & 3) and fetches the global chunk the row's swizzle puts in that slot
+    // ---- this thread's dgate row and unit pair; the row's scale from the producers' bounds ----
+    const int er = tid >> 2, ep = tid & 3;
+    const int eb = b0 + er < a.NB ? b0 + er : a.NB - 1;    // tail rows recompute the last trajectory (not stored)
+    const bool elive = b0 + er < a.NB;
+    float up, down;
+    {
+        float m = a.rm_c[eb] + fmaxf(a.rm_h[eb], a.rm_h[a.NB + eb]);
+        if (a.rm_d) m += fmaxf(a.rm_d[eb], a.rm_d[a.NB + eb]);
+        const int ex = m > 0.0f ? __builtin_amdgcn_frexp_expf(m) : 0;   // every |dgate| < 2^ex (times (kL-1)/4: forget)
+        up = __builtin_amdgcn_ldexpf(1.0f, kWideDgExp - ex);
+        down = __builtin_amdgcn_ldexpf(1.0f, ex - kWideDgExp);
+        if (ep == 0) reinterpret_cast<float *>(lds + kWbOffDown)[er] = down;
+    }
+    float *w0l = reinterpret_cast<float *>(lds + kWbOffW0);
+    if constexpr (L0) {   // W_ih0 [4H][kIn] -> LDS [unit][gate][kIn]
+        for (int i = tid; i < 4 * H * kIn; i += kWbThreads) {
+            const int rw = i / kIn, c = i % kIn, g = rw / H, u = rw % H;
+            w0l[(u * 4 + g) * kIn + c] = a.wih0[i];
+        }
+    }
+
+    // ---- A: LDS-DMA pieces (16 rows x 64 B of [A hi (16 pieces) | A lo (16)]); lane i lands at +16 i ----
     const _Float16 *gsrc[kWbPieces];
     uint32_t ldst[kWbPieces];
 #pragma unroll
-    for (int p = 0; p < kWbPieces; ++p) {
-        const int j = wv + kWbWaves * p;
-        const int part = j < 16 ? 0 : j < 32 ? 1 : j < 40 ? 2 : 3;
-        const int base = part == 0 ? 0 : part == 1 ? 16 : part == 2 ? 32 : 40;
-        const int r = 16 * (j - base) + (lane >> 2);
+    for (int q = 0; q < kWbPieces; ++q) {
+        const int j = wv + kWbWaves * q;
+        const bool lo = j >= 16;
+        const int r = 16 * (lo ? j - 16 : j) + (lane >> 2);
         const int c = (lane & 3) ^ ((r >> 1) & 3);
-        if (part < 2) {
-            int n = m0 + r;
-            if (n >= a.NO) n = a.NO - 1;                   // tail columns recompute the last one (not stored)
-            gsrc[p] = (part == 0 ? a.Ahi : a.Alo) + (size_t)n * a.lda + 8 * c;
-        } else {
-            int b = b0 + r;
-            if (b >= a.NB) b = a.NB - 1;                   // tail rows recompute the last trajectory (not stored)
-            gsrc[p] = a.B + (size_t)b * a.ldb + (part == 3 ? a.lo_off : 0) + 8 * c;
-        }
-        ldst[p] = (uint32_t)j * 1024;
+        int n = m0 + r;
+        if (n >= a.NO) n = a.NO > 0 ? a.NO - 1 : 0;        // tail columns recompute the last one (not stored)
+        gsrc[q] = (lo ? a.Alo : a.Ahi) + (size_t)n * K + 8 * c;
+        ldst[q] = (uint32_t)j * 1024;
     }
     auto dma = [&](int ks, int buf) {
 #pragma unroll
-        for (int p = 0; p < kWbPieces; ++p)
+        for (int q = 0; q < kWbPieces; ++q)
             __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void *)(gsrc[p] + ks * kWbK),
+                (const __attribute__((address_space(1))) void *)(gsrc[q] + ks * kWbK),
                 (__attribute__((address_space(3))) void *)((__attribute__((address_space(3))) char *)lds + buf * kWbStage +
-                                                           ldst[p]),
+                                                           ldst[q]),
                 16, 0, 0);
+    };
+
+    // ---- the dgate part: inputs one step ahead, the tile one step ahead of the MFMAs ----
+    const float *pre = a.pre + (size_t)eb * K;
+    const float *cpr = a.c_prev ? a.c_prev + (size_t)eb * H : nullptr;
+    const float *dhr = a.dh + (size_t)eb * a.ldh;
+    const float *dnr = a.din ? a.din + (size_t)eb * a.ldx : nullptr;
+    const float *dcr = a.dC + (size_t)eb * H;
+    float *dco_r = a.dC_out + (size_t)eb * H;
+    auto load_in = [&](int s) {
+        WbIn x;
+        const int u = 8 * s + 2 * ep;
+        x.pi = *reinterpret_cast<const f32x2 *>(pre + u);
+        x.pf = *reinterpret_cast<const f32x2 *>(pre + H + u);
+        x.pg = *reinterpret_cast<const f32x2 *>(pre + 2 * H + u);
+        x.po = *reinterpret_cast<const f32x2 *>(pre + 3 * H + u);
+        x.cp = cpr ? *reinterpret_cast<const f32x2 *>(cpr + u) : f32x2{0.0f, 0.0f};
+        x.dh = *reinterpret_cast<const f32x2 *>(dhr + u);
+        x.dn = dnr ? *reinterpret_cast<const f32x2 *>(dnr + u) : f32x2{0.0f, 0.0f};
+        x.dc = *reinterpret_cast<const f32x2 *>(dcr + u);
+        return x;
+    };
+    const bool wr_dc = cb == 0 && elive;   // both column blocks form the same dc_{t-1}: the first stores it
+    float mdc = 0.0f;                      // max |dc_{t-1}| of this thread's units
+    float pc[kIn] = {};                    // layer 0: this thread's share of the window-row gradient
+    auto dgates = [&](int s, const WbIn &x, int buf) {
+        float dg[8], sc[8];
+        f32x2 dco;
+        const int u = 8 * s + 2 * ep;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const float i = sigm(x.pi[k]), f = sigm(x.pf[k]), g = tanh_f(x.pg[k]), o = sigm(x.po[k]);
+            const float cp = x.cp[k];
+            const float tc = tanh_f(fmaf(f, cp, i * g));   // c_t rebuilt as the forward formed it (f c_{t-1} + i g)
+            const float dh = x.dh[k] + x.dn[k];
+            const float dct = fmaf(dh * o, 1.0f - tc * tc, x.dc[k]);
+            dg[4 * k + 0] = dct * g * (i - i * i);
+            dg[4 * k + 1] = dct * cp * (f - f * f);
+            dg[4 * k + 2] = dct * i * (1.0f - g * g);
+            dg[4 * k + 3] = dh * tc * (o - o * o);
+            dco[k] = dct * f;
+        }
+        if (wr_dc) *reinterpret_cast<f32x2 *>(dco_r + u) = dco;
+        mdc = fmaxf(mdc, fmaxf(fabsf(dco[0]), fabsf(dco[1])));
+        if constexpr (L0) {   // sum_r dG[b][r] W_ih0[r][c] over this step's 8 gate rows, fp32
+            const f32x4 *w4 = reinterpret_cast<const f32x4 *>(w0l + u * 4 * kIn);   // 40 floats: units u, u + 1
+#pragma unroll
+            for (int q = 0; q < 2 * 4 * kIn / 4; ++q) {
+                const f32x4 wq = w4[q];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int idx = 4 * q + e;   // (unit k, gate g, column c) = idx / 20, idx / 5 % 4, idx % 5
+                    pc[idx % kIn] = fmaf(dg[idx / kIn], wq[e], pc[idx % kIn]);
+                }
+            }
+        }
+        if (prod) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) sc[e] = up;
+            f16x8 h, l;
+            split8p(dg, sc, h, l);
+            char *bt = lds + kWbOffB + buf * 2 * kWbTileB;
+            *reinterpret_cast<f16x8 *>(bt + wb_off(er, ep)) = h;
+            *reinterpret_cast<f16x8 *>(bt + kWbTileB + wb_off(er, ep)) = l;
+        }
     };
 
     f32x4 acc[kWbTM][kWbTN];
@@ -103,64 +208,120 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_gemm_kernel(WbArgs a) 
 #pragma unroll
         for (int j = 0; j < kWbTN; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     const int fr = lane & 15, fq = lane >> 4;
-    // two steps of prefetch: stage ks is waited for with step ks + 1's pieces still in flight (vmcnt counts this
-    // wave's DMA in issue order); a bare s_barrier publishes every wave's pieces (fcr_wgemm.h)
-    dma(0, 0);
-    if (nk > 1) dma(1, 1);
-    int buf = 0;
+
+    if (prod) dma(0, 0);
+    WbIn xc = load_in(0);
+    __syncthreads();   // W_ih0 and the row scales in LDS
+    dgates(0, xc, 0);
+    if (nk > 1) xc = load_in(1);
     for (int ks = 0; ks < nk; ++ks) {
-        if (ks + 1 < nk) {
-            if constexpr (kWbPieces == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int buf = ks & 1;
+        // stage ks's A landed (issued a step ago), tile ks's dgates written by every thread: publish both
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (prod && ks + 1 < nk) dma(ks + 1, buf ^ 1);   // into the stage every wave finished reading at ks - 1
+        WbIn xn;
+        if (ks + 2 < nk) xn = load_in(ks + 2);
+        if (prod) {
+            const char *st = lds + buf * kWbStage;
+            const char *bt = lds + kWbOffB + buf * 2 * kWbTileB;
+            f16x8 ah[kWbTM], al[kWbTM], bh[kWbTN], bl[kWbTN];
+#pragma unroll
+            for (int j = 0; j < kWbTN; ++j) {
+                const int r = 16 * (kWbTN * wn + j) + fr;
+                bh[j] = *reinterpret_cast<const f16x8 *>(bt + wb_off(r, fq));
+                bl[j] = *reinterpret_cast<const f16x8 *>(bt + kWbTileB + wb_off(r, fq));
+            }
+#pragma unroll
+            for (int i = 0; i < kWbTM; ++i) {
+                const int r = 16 * (kWbTM * wm + i) + fr;
+                ah[i] = *reinterpret_cast<const f16x8 *>(st + wb_off(r, fq));
+                al[i] = *reinterpret_cast<const f16x8 *>(st + kWbStageA + wb_off(r, fq));
+            }
+#pragma unroll
+            for (int i = 0; i < kWbTM; ++i)
+#pragma unroll
+                for (int j = 0; j < kWbTN; ++j) acc[i][j] = mma3(ah[i], al[i], bh[j], bl[j], acc[i][j]);
         }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        const char *st = lds + buf * kWbStage;
-        f16x8 ah[kWbTM], al[kWbTM], bh[kWbTN], bl[kWbTN];
-#pragma unroll
-        for (int j = 0; j < kWbTN; ++j) {
-            const int r = 16 * (kWbTN * wn + j) + fr;
-            bh[j] = *reinterpret_cast<const f16x8 *>(st + 2 * kWbStageA + wb_off(r, fq));
-            bl[j] = *reinterpret_cast<const f16x8 *>(st + 2 * kWbStageA + kWbStageB + wb_off(r, fq));
-        }
-#pragma unroll
-        for (int i = 0; i < kWbTM; ++i) {
-            const int r = 16 * (kWbTM * wm + i) + fr;
-            ah[i] = *reinterpret_cast<const f16x8 *>(st + wb_off(r, fq));
-            al[i] = *reinterpret_cast<const f16x8 *>(st + kWbStageA + wb_off(r, fq));
-        }
-        const int nb = buf == 0 ? 2 : buf - 1;            // (ks + 2) % 3: every wave finished reading it at ks - 1
-        if (ks + 2 < nk) dma(ks + 2, nb);
-#pragma unroll
-        for (int i = 0; i < kWbTM; ++i)
-#pragma unroll
-            for (int j = 0; j < kWbTN; ++j) acc[i][j] = mma3(ah[i], al[i], bh[j], bl[j], acc[i][j]);
-        buf = buf == 2 ? 0 : buf + 1;
+        // the next step's dgates beside this step's MFMAs (their tile buffer was read at ks - 1)
+        if (ks + 1 < nk) dgates(ks + 1, xc, buf ^ 1);
+        if (ks + 2 < nk) xc = xn;
     }
-    // ---- epilogue: lane = trajectory b0 + 16 (TN wn + j) + (lane & 15), columns m0 + 16 (TM wm + i) + 4 (lane >> 4) .. +3
+    // ---- per-row results of the dgate part: dc_{t-1} bound, layer 0's window-row gradient ----
+    mdc = fmaxf(mdc, __shfl_xor(mdc, 1));
+    mdc = fmaxf(mdc, __shfl_xor(mdc, 2));
+    if (a.rm_c_out && wr_dc && ep == 0) a.rm_c_out[eb] = mdc;
+    if constexpr (L0) {
+#pragma unroll
+        for (int c = 0; c < kIn; ++c) {
+            pc[c] += __shfl_xor(pc[c], 1);
+            pc[c] += __shfl_xor(pc[c], 2);
+        }
+        if (a.rowg && elive && cb == 0 && ep == 0)
+#pragma unroll
+            for (int c = 0; c < kIn; ++c) a.rowg[(size_t)eb * kIn + c] += pc[c];
+    }
+    if (!prod) return;
+    // ---- epilogue: lane = trajectory b0 + 16 (TN wn + j) + (lane & 15), columns m0 + 16 (TM wm + i) + 4 (lane >> 4)
+    // .. +3, in true units (x the row's down); and the row maxima of the dh and input-gradient columns ----
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const float *ldown = reinterpret_cast<const float *>(lds + kWbOffDown);
+    float *red = reinterpret_cast<float *>(lds);   // [wm][128 rows][2] (the A stages are retired)
 #pragma unroll
     for (int j = 0; j < kWbTN; ++j) {
-        const int b = b0 + 16 * (kWbTN * wn + j) + fr;
-        if (b >= a.NB) continue;
-        float *row = a.out + (size_t)b * a.ldo;
-        const float f = a.rs ? a.rs[b] : 1.0f;
+        const int rl = 16 * (kWbTN * wn + j) + fr, b = b0 + rl;
+        const float f = ldown[rl];
+        float mh = 0.0f, md = 0.0f;
 #pragma unroll
         for (int i = 0; i < kWbTM; ++i) {
             const int col = m0 + 16 * (kWbTM * wm + i) + 4 * fq;
-            if (col < a.NO) *reinterpret_cast<f32x4 *>(row + col) = acc[i][j] * f;
+            const f32x4 v = acc[i][j] * f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float av = fabsf(v[e]);
+                if (col + e >= a.h0 && col + e < a.h1) mh = fmaxf(mh, av);
+                if (col + e < a.d1) md = fmaxf(md, av);
+            }
+            if (b < a.NB && col < a.NO) *reinterpret_cast<f32x4 *>(a.out + (size_t)b * a.ldo + col) = v;
+        }
+        mh = fmaxf(mh, __shfl_xor(mh, 16));
+        mh = fmaxf(mh, __shfl_xor(mh, 32));
+        md = fmaxf(md, __shfl_xor(md, 16));
+        md = fmaxf(md, __shfl_xor(md, 32));
+        if (fq == 0) {
+            red[(wm * kWbN + rl) * 2] = mh;
+            red[(wm * kWbN + rl) * 2 + 1] = md;
+        }
+    }
+    __syncthreads();
+    if (tid < kWbN && b0 + tid < a.NB) {
+        float mh = 0.0f, md = 0.0f;
+#pragma unroll
+        for (int w = 0; w < kWbWM; ++w) {
+            mh = fmaxf(mh, red[(w * kWbN + tid) * 2]);
+            md = fmaxf(md, red[(w * kWbN + tid) * 2 + 1]);
+        }
+        const int b = b0 + tid;
+        if (a.rm_h_out) {
+            a.rm_h_out[(size_t)cb * a.NB + b] = mh;
+            if (ny == 1) a.rm_h_out[(size_t)a.NB + b] = 0.0f;
+        }
+        if (a.rm_d_out) {
+            a.rm_d_out[(size_t)cb * a.NB + b] = md;
+            if (ny == 1) a.rm_d_out[(size_t)a.NB + b] = 0.0f;
         }
     }
 }
 
 // A of the gradient product, transposed and split: dst_hi / dst_lo [NO][4H], row n = output column n of
-// [W_ih | W_hh] (layers >= 1, NO = 2H; `wih` null for layer 0: W_hh only, NO = H), column r = gate row r.
+// [W_ih | W_hh] (layers >= 1, NO = 2H; `wih` null for layer 0: W_hh only, NO = H), column r' = 4 unit + gate
+// (unit-major: a K step of the fused kernel is 8 whole units) holding torch's gate row gate H + unit.
 __global__ void wide_split_bt_kernel(const float *__restrict__ wih, const float *__restrict__ whh, int H, int NO,
                                      _Float16 *dst_hi, _Float16 *dst_lo) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int K = 4 * H;
     if (idx >= (size_t)NO * K) return;
-    const int n = (int)(idx / K), r = (int)(idx % K);
+    const int n = (int)(idx / K), rp = (int)(idx % K);
+    const int r = (rp & 3) * H + (rp >> 2);
     const float v = (wih && n < H) ? wih[(size_t)r * H + n] : whh[(size_t)r * H + (wih ? n - H : n)];
     const _Float16 hi = (_Float16)v;
     dst_hi[idx] = hi;

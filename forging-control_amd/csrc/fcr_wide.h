@@ -254,7 +254,9 @@ __device__ __forceinline__ void wide_head_dxhat(const WideArgs &a, int j, int b,
     d[2] = d2;
     d[3] = d3;
 }
-__global__ void wide_head_kernel(WideArgs a, int j) {
+// rmh (the fused backward, fcr_wbwd.h), or null: the row bound max_u |dH[b][u]| into rmh[b] (rmh[B + b] = 0: the
+// second column block's slot)
+__global__ void wide_head_kernel(WideArgs a, int j, float *rmh) {
     const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int b = (int)(gid / kRoLanes), q = (int)(gid % kRoLanes);
     const bool live = b < a.B;
@@ -262,9 +264,20 @@ __global__ void wide_head_kernel(WideArgs a, int j) {
     if (live && q == 0) wide_head_dxhat(a, j, b, d);
 #pragma unroll
     for (int k = 0; k < kOut; ++k) d[k] = __shfl(d[k], 0, kRoLanes);
-    if (!live) return;
-    for (int u = q; u < a.H; u += kRoLanes)
-        a.dH[(size_t)b * a.H + u] = a.fcw[u] * d[0] + a.fcw[a.H + u] * d[1] + a.fcw[2 * a.H + u] * d[2] + a.fcw[3 * a.H + u] * d[3];
+    float m = 0.0f;
+    if (live)
+        for (int u = q; u < a.H; u += kRoLanes) {
+            const float v = a.fcw[u] * d[0] + a.fcw[a.H + u] * d[1] + a.fcw[2 * a.H + u] * d[2] + a.fcw[3 * a.H + u] * d[3];
+            a.dH[(size_t)b * a.H + u] = v;
+            m = fmaxf(m, fabsf(v));
+        }
+    if (!rmh) return;
+#pragma unroll
+    for (int s = kRoLanes / 2; s > 0; s >>= 1) m = fmaxf(m, __shfl_xor(m, s, kRoLanes));
+    if (live && q == 0) {
+        rmh[b] = m;
+        rmh[a.B + b] = 0.0f;
+    }
 }
 
 // Backward of one cell: from the activations, c_t, c_{t-1}, the incoming dh (carried dH + din from the
@@ -272,13 +285,10 @@ __global__ void wide_head_kernel(WideArgs a, int j) {
 // act: the gate activations (i, f, g, o) kept by the recompute, or with PRE their pre-activations (the
 // split-f16 rollout keeps the GEMM output per cell instead of writing a second 4H-wide array), from which
 // the activations are rebuilt with the forward's arithmetic. dG (fp32) may be null when only dgsp is used.
-// a lane's value moved by a DPP pattern within its 16-lane row (every lane has a source: no bound control)
-template <int CTRL>
-__device__ __forceinline__ float dpp_f32(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
-}
-// the per-row dgate scale's headroom exponent (wide_cell_bwd_kernel rsc): the forget-gate row of a kL-step window
-// reaches (kL - 1) / 4 * 2^kWideDgExp, which must stay a finite f16
+// The per-row dgate scale of the fused backward cell (fcr_wbwd.h) is 2^(kWideDgExp - e), e the exponent of a bound m on
+// the row's |dc_t| (m >= |dc| + |dh|): the i, g, o rows are |dc_t| or |dh| times a local derivative <= 1, so below
+// 2^kWideDgExp scaled; the forget row is dc_t c_{t-1} f (1 - f) with |c_{t-1}| <= t <= kL - 1 (|c_t| <= |c_{t-1}| + 1
+// from c = 0), so it reaches (kL - 1) / 4 * 2^kWideDgExp (18 432 at kL = 10): a finite f16, with that margin only
 constexpr int kWideDgExp = 13;
 static_assert((kL - 1) * (1 << kWideDgExp) / 4 < 65504, "f16 overflow of the forget-gate dgates: lower kWideDgExp");
 // With PRE, c_t is recomputed from the pre-activations and c_{t-1} rather than loaded (round 3d: bit-identical,
@@ -288,15 +298,11 @@ __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restr
                                      const float *__restrict__ c_prev, const float *__restrict__ dH,
                                      const float *__restrict__ din, float *dC, float *dG, _Float16 *dgsp,
                                      const float *__restrict__ consts, int dh_scaled, int ldh, int ldx, int B,
-                                     int H, int dg3, const float *__restrict__ wih0 = nullptr, float *rowg = nullptr,
-                                     float *rsc = nullptr) {
+                                     int H, int dg3, const float *__restrict__ wih0 = nullptr, float *rowg = nullptr) {
     using W = WideVec<V>;
     // with consts (split-f16 rollout) din, and dH unless it is the head's, come from gemm16_bwd in the
     // scaled units of the dgates: back by 1/scale = consts[0], one fp32 product each
-    // rsc (the hand-written product, fcr_wbwd.h): every trajectory row's dgates are split at their OWN power of two
-    // (2^(13-e), e = exponent of a bound on the row's |dgates|; its inverse to rsc[b], which the product applies to its
-    // output row), so the products come back in true units and din / dH need no unscaling
-    const float c0 = (consts && !rsc) ? consts[0] : 1.0f, mh = dh_scaled ? c0 : 1.0f;
+    const float c0 = consts ? consts[0] : 1.0f, mh = dh_scaled ? c0 : 1.0f;
     const int HV = H / V;
     // a thread owns V units of T consecutive trajectories (T > 1 only for layer 0's row gradient: its W_ih0
     // rows, 4 V kIn floats, are loaded once for the T trajectories instead of once per trajectory)
@@ -332,30 +338,6 @@ __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restr
         if (c_prev) cp = W::ld(c_prev + idx);
         if (!PRE) cv = W::ld(c + idx);
         if (din) dn = W::ld(din + b * ldx + u);
-        // rsc: the row's power of two 2^(13-ex) from m = max(|dc| + |dh|) >= |dc_t| (taken from the inputs, so the row
-        // reduction runs beside the gate arithmetic rather than after it; the row's H / V threads are one aligned
-        // segment of a wave, the host checks 64 % (H / V) == 0). The i, g, o rows are |dc_t| or |dh| times a local
-        // derivative <= 1, so below 2^13 scaled; the forget row is dc_t c_{t-1} f (1 - f), and |c_{t-1}| <= t <= kL - 1
-        // (|c_t| <= |c_{t-1}| + 1 from c = 0), so it stays below (kL - 1) / 4 * 2^13 (18 432 at kL = 10): inside f16's
-        // 65 504, with that margin only (kWideDgExp)
-        float rsc_up = 1.0f;
-        if (rsc) {
-            float mx = 0.0f;
-#pragma unroll
-            for (int k = 0; k < V; ++k) mx = fmaxf(mx, fabsf(dhv[k] * mh + dn[k] * c0) + fabsf(dcv[k]));
-            if (HV >= 16) {   // the first four levels on DPP inside 16-lane rows (as the row gradient's sums)
-                mx = fmaxf(mx, dpp_f32<0xB1>(mx));
-                mx = fmaxf(mx, dpp_f32<0x4E>(mx));
-                mx = fmaxf(mx, dpp_f32<0x141>(mx));
-                mx = fmaxf(mx, dpp_f32<0x140>(mx));
-                for (int o = 16; o < HV; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-            } else {
-                for (int o = 1; o < HV; o <<= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-            }
-            const int ex = mx > 0.0f ? __builtin_amdgcn_frexp_expf(mx) : 0;   // every |dgate| < 2^ex
-            rsc_up = __builtin_amdgcn_ldexpf(1.0f, kWideDgExp - ex);
-            if (u == 0) rsc[b] = __builtin_amdgcn_ldexpf(1.0f, ex - kWideDgExp);
-        }
 #pragma unroll
         for (int k = 0; k < V; ++k) {
             const float i = PRE ? sigm(ai[k]) : ai[k], f = PRE ? sigm(af[k]) : af[k], g = PRE ? tanhf(ag[k]) : ag[k],
@@ -376,9 +358,8 @@ __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restr
 #pragma unroll
             for (int k = 0; k < 4; ++k) W::st(d4 + k * H, dg[k]);
         }
-        if (dgsp) {   // split-f16 operand row [hi | lo | hi] of W^T dG, scaled into the f16 range (wide_bscale_kernel);
-            // the hand-written product (fcr_wbwd.h) reads hi and lo once each: no third copy (dg3 = 0)
-            const float sc = rsc ? rsc_up : consts[3];
+        if (dgsp) {   // split-f16 operand row [hi | lo | hi] of W^T dG, scaled into the f16 range (wide_bscale_kernel)
+            const float sc = consts[3];
             _Float16 *o16 = dgsp + b * 12 * H + u;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {

@@ -200,3 +200,24 @@ def kink_margin(params, X, xhat):
     z = cin @ Wi.T + bi
     v = torch.relu(z) @ Wo[0]
     return torch.minimum(con, torch.minimum(z.abs().amin(dim=(1, 2)), (1 - v.abs()).abs().amin(dim=1)))
+
+
+def one_sided_g_u0(params, X, u0, states, N, alpha, rows, B_full, device="cpu", rel=(1e-9, 1e-8, 1e-7, 1e-6, 1e-5)):
+    """The fp64 d loss / d u0 of trajectories ``rows`` of a batch of ``B_full`` trajectories, evaluated at u0 shifted
+    by +-d for d in ``rel`` (absolute shifts of u0, a Hardtanh output in [-1, 1]): the one-sided derivatives on either
+    side of a kink the trajectory passes near. Where an fp32 evaluation lands on the other side of such a kink than
+    fp64 does (kink_margin), its g_u0 is — to fp32 accuracy — one of these values, not the fp64 value at u0: the
+    full-size parity tests accept a kink-band trajectory above 1e-5 only when its g_u0 matches one of them
+    (checker only). Returns {row: [(shift, g), ...]} with g in the full batch's units (the 1/B of the mean)."""
+    t = lambda a: torch.as_tensor(a).to(device=device, dtype=torch.float64)
+    X, u0, states = t(X), t(u0).reshape(-1), t(states)
+    out = {}
+    for r in rows:
+        res = []
+        for d in rel:
+            for s in (d, -d):
+                g = loss_and_grads_chunked(params, X[r:r + 1], (u0[r:r + 1] + s).reshape(1, 1), states[r:r + 1], N,
+                                           alpha, device=device)["g_u0"]
+                res.append((s, float(g[0]) / B_full))
+        out[r] = res
+    return out
