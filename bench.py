@@ -291,9 +291,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--grad-check", choices=("full", "off"), default="full",
                     help="full: grad max-rel-err of the benchmarked batch vs the fp64 torch restatement (after timing)")
-    ap.add_argument("--precision", choices=("fp32", "f16", "f16fwd"), default="fp32",
-                    help="fp32: reference-accurate (default, config 2); f16: gate products in f16 in both passes; "
-                         "f16fwd: f16 forward, fp32-accurate backward (config 3)")
+    ap.add_argument("--precision", choices=("fp32", "f16"), default="fp32",
+                    help="fp32: reference-accurate (default, config 2); f16: gate products in f16 in both passes, fp32 "
+                         "accumulate (config 3)")
     ap.add_argument("--graphed", action="store_true",
                     help="time the step as NeuralNetwork.captured_step replays it (one HIP graph per step; the "
                          "launch-bound small batches, e.g. the reference's B = 15); 1 GPU")
@@ -431,7 +431,7 @@ def main():
         # ceiling of the arithmetic as executed: an fp32-accurate product is three f16 MFMA products
         # (hi.hi + hi.lo + lo.hi, fcr_f16.h), so the fp32-equivalent ceiling is the f16 peak / 3;
         # in the reduced-precision pass one f16 product each
-        f16_pass = args.precision == "f16" or (args.precision == "f16fwd" and dom[0] == "fwd")
+        f16_pass = args.precision == "f16"
         peak = F16_PEAK_TFLOPS if f16_pass else F16_PEAK_TFLOPS / 3
         roof = {"bound": "mfma", "kernel": kernel, "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
                 "frac": achieved / peak, "traffic": traffic,
@@ -448,12 +448,12 @@ def main():
             roof["executed"] = {"instr": "v_mfma_f32_16x16x32_f16", "achieved": ex, "peak": F16_PEAK_TFLOPS,
                                 "unit": "TFLOP/s", "frac": ex / F16_PEAK_TFLOPS,
                                 "def": "MFMA FLOP issued (split products, padding, backward recompute) / time"}
-        prec_label = {"fp32": "fp32", "f16": "f16 fwd+bwd", "f16fwd": "f16 fwd / fp32-accurate bwd"}[args.precision]
+        prec_label = {"fp32": "fp32", "f16": "f16 fwd+bwd"}[args.precision]
         line = {
             "metric": "rollout-steps/s (batch x horizon), fwd+bwd+AdamW step",
             "value": value, "unit": "rollout-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": {"fp32": "f32", "f16": "f16", "f16fwd": "f16fwd/f32bwd"}[args.precision],
+            "dtype": {"fp32": "f32", "f16": "f16"}[args.precision],
             "data": "synthetic (SURVEY §8d distribution); reference-trained LSTM/controller weights",
             "config": {"workload": f"unsupervised-MPC rollout train step, B={B}/GPU, N={N}, H={H}, 3-layer LSTM, "
                                    f"ctrl 3-50-1, {prec_label}" + (", HIP-graph replay" if captured is not None else ""),

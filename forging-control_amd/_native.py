@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(_HERE, "lib", _LIB_NAME)
 
 FCR_OK = 0
 ABI_VERSION = 5
-PRECISION_FP32, PRECISION_F16, PRECISION_F16_FWD = 0, 1, 2
+PRECISION_FP32, PRECISION_F16 = 0, 1
 ERRORS = {-1: "FCR_EINVAL", -2: "FCR_EWORKSPACE", -3: "FCR_EHIP", -4: "FCR_EUNSUPPORTED"}
 
 # Every symbol include/fcr.h declares (tests check the .so exports exactly these).

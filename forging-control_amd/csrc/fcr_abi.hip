@@ -102,10 +102,11 @@ int check_dims(const fcr_dims *d) {
     if (d->H < 1 || d->H > kMaxWideH)
         return fail(FCR_EUNSUPPORTED, "H=%d: built for 1..%d", d->H, kMaxWideH);
     if ((long long)d->B * d->N > (1LL << 31)) return fail(FCR_EINVAL, "B*N too large");
-    if (d->precision != FCR_PRECISION_FP32 && d->precision != FCR_PRECISION_F16 &&
-        d->precision != FCR_PRECISION_F16_FWD)
-        return fail(FCR_EINVAL, "precision=%d: FCR_PRECISION_FP32 (0), FCR_PRECISION_F16 (1) or "
-                    "FCR_PRECISION_F16_FWD (2)", d->precision);
+    if (d->precision == 2)
+        return fail(FCR_EUNSUPPORTED, "precision=2 (f16 forward, fp32-accurate backward) is retired: it ran 1.08x the "
+                    "fp32 step at the f16 mode's accuracy; use FCR_PRECISION_F16 (1) or FCR_PRECISION_FP32 (0)");
+    if (d->precision != FCR_PRECISION_FP32 && d->precision != FCR_PRECISION_F16)
+        return fail(FCR_EINVAL, "precision=%d: FCR_PRECISION_FP32 (0) or FCR_PRECISION_F16 (1)", d->precision);
     if (d->precision != FCR_PRECISION_FP32 && is_wide(d))
         return fail(FCR_EUNSUPPORTED, "reduced precision is built for H <= %d (the fused kernels)", 4 * kMaxSlots);
     return FCR_OK;
@@ -1417,9 +1418,9 @@ int fcr_forward(const fcr_dims *d, fcr_options *opts, const fcr_weights *w, cons
         else rc = with_backward ? launch_sfwd_t<13, true>(fa, L, s) : launch_sfwd_t<13, false>(fa, L, s);
     } else {
         switch (L.HS) {
-            case 4: rc = launch_fwd<4>(fa, L, d->precision != FCR_PRECISION_FP32, s); break;
-            case 8: rc = launch_fwd<8>(fa, L, d->precision != FCR_PRECISION_FP32, s); break;
-            case 13: rc = launch_fwd<13>(fa, L, d->precision != FCR_PRECISION_FP32, s); break;
+            case 4: rc = launch_fwd<4>(fa, L, d->precision == FCR_PRECISION_F16, s); break;
+            case 8: rc = launch_fwd<8>(fa, L, d->precision == FCR_PRECISION_F16, s); break;
+            case 13: rc = launch_fwd<13>(fa, L, d->precision == FCR_PRECISION_F16, s); break;
             default: rc = fail(FCR_EUNSUPPORTED, "H=%d", d->H);
         }
     }

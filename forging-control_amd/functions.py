@@ -131,7 +131,7 @@ class MPCLoss(nn.Module):
         super().__init__()
         self.N = prediction_horizon
         self.alpha = alpha
-        self.precision = precision     # "fp32" (reference-accurate), "f16fwd" (config 3) or "f16" (include/fcr.h)
+        self.precision = precision     # "fp32" (reference-accurate) or "f16" (config 3, include/fcr.h)
         self.small_batch_limit = small_batch_limit
         self.wide_keep_budget = wide_keep_budget
         self.activation = nn.ReLU()

@@ -134,14 +134,13 @@ class RolloutFn(torch.autograd.Function):
         return (None, g_u0, None, None, g_wi, g_bi, g_wo) + (None,) * 12
 
 
-PRECISIONS = {"fp32": _native.PRECISION_FP32, "f16": _native.PRECISION_F16, "f16fwd": _native.PRECISION_F16_FWD}
+PRECISIONS = {"fp32": _native.PRECISION_FP32, "f16": _native.PRECISION_F16}
 
 
 def rollout(X, u0, states, ctrl_params, lstm_params, N, alpha, noise=None, precision="fp32", info=None):
     """Functional entry: ctrl_params = (W_inp, b_inp, W_out), lstm_params = (w_ih[3], w_hh[3], fc_w, fc_b).
-    precision: "fp32" (fp32-accurate, the default), "f16fwd" (config 3: f16 gate products in the forward,
-    fp32-accurate backward, include/fcr.h FCR_PRECISION_F16_FWD) or "f16" (f16 gate products in both passes,
-    FCR_PRECISION_F16). info: a CallInfo with this call's fcr_options (None: every option inherits the process
+    precision: "fp32" (fp32-accurate, the default) or "f16" (config 3: f16 gate products in both passes, fp32
+    accumulate, include/fcr.h FCR_PRECISION_F16; the former "f16fwd" mode is retired). info: a CallInfo with this call's fcr_options (None: every option inherits the process
     default); the kernel families it ran are recorded in it."""
     if precision not in PRECISIONS:
         raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {precision!r}")

@@ -54,7 +54,7 @@ typedef struct fcr_dims {
     int32_t ctrl_in;     /* controller inputs (must be 3)                     */
     int32_t ctrl_hidden; /* controller hidden units (<= 52)                   */
     float alpha;         /* MPCLoss.alpha, command-variation weight            */
-    int32_t precision;   /* FCR_PRECISION_FP32 (0), _F16 (1) or _F16_FWD (2), below */
+    int32_t precision;   /* FCR_PRECISION_FP32 (0) or FCR_PRECISION_F16 (1), below */
 } fcr_dims;
 
 /* Arithmetic of the gate products (fcr_forward/fcr_backward; fcr_lstm_* ignore it and run fp32):
@@ -64,14 +64,11 @@ typedef struct fcr_dims {
  *                        f16 operands (11-bit significand, more than bf16's 8; the backward's per-trajectory
  *                        power-of-two scaling keeps them in range), one MFMA per product, fp32 accumulate;
  *                        H <= 52 only;
- *   FCR_PRECISION_F16_FWD — config 3 as BASELINE words it ("bf16 fwd / fp32 accum"): the forward's gate
- *                        products in f16 (as FCR_PRECISION_F16), the backward fp32-accurate (as FCR_PRECISION_FP32:
- *                        it recomputes each cell's gates from the f16 forward's stored h and c with split products,
- *                        so the gradients are fp32-accurate gradients at the f16 trajectory); H <= 52 only.
+ *   (2, the former FCR_PRECISION_F16_FWD — f16 forward, fp32-accurate backward — is retired in ABI v5 and refused
+ *   with FCR_EUNSUPPORTED: it ran 1.08x the fp32 step at the all-f16 mode's accuracy, DESIGN.md §4 "Config 3".)
  * Both calls of one step must be given the same dims (the same precision value). */
 #define FCR_PRECISION_FP32 0
 #define FCR_PRECISION_F16 1
-#define FCR_PRECISION_F16_FWD 2
 
 /* Weights, torch layouts (row-major, as state_dict holds them). */
 typedef struct fcr_weights {

@@ -59,7 +59,7 @@ def test_workspace_size_scales_with_batch_and_backward():
 
 @pytest.mark.parametrize("kw,code", [
     (dict(B=0), -1), (dict(N=0), -1), (dict(H=4096), -4), (dict(H=0), -4), (dict(layers=2), -4), (dict(ctrl_hidden=80), -4),
-    (dict(precision=3), -1), (dict(precision=1, H=64), -4), (dict(precision=2, H=64), -4),
+    (dict(precision=3), -1), (dict(precision=1, H=64), -4), (dict(precision=2), -4),
 ])
 def test_invalid_dims_rejected_with_message(kw, code):
     lib = fca._native.load()

@@ -145,12 +145,12 @@ def test_config3_full_batch_fp32(ref_params, seed):
 
 
 @pytest.mark.parametrize("seed", [("own", 23), BENCH])
-def test_config3_full_batch_f16fwd(ref_params, seed):
-    """B = 262 144 in config 3's mode (f16 forward, fp32-accurate backward) at the stated tolerances
-    (tests/test_gpu_precision.py)."""
-    from test_gpu_precision import TOL_FEATS, TOL_GRADS_F16FWD_FULL, TOL_GU0_F16FWD, TOL_LOSS
-    _check(*hip_and_oracle(ref_params, 262144, 10, seed, precision="f16fwd"), 262144, TOL_FEATS, TOL_GU0_F16FWD,
-           TOL_GRADS_F16FWD_FULL, TOL_LOSS, kink=False)   # the f16 forward's own error exceeds the kink bar
+def test_config3_full_batch_f16(ref_params, seed):
+    """B = 262 144 in config 3's reduced-precision mode (f16 gate products in both passes, fp32 accumulate) at the
+    stated tolerances (tests/test_gpu_precision.py)."""
+    from test_gpu_precision import TOL_FEATS, TOL_GRADS_F16_FULL, TOL_GU0_F16_FULL, TOL_LOSS
+    _check(*hip_and_oracle(ref_params, 262144, 10, seed, precision="f16"), 262144, TOL_FEATS, TOL_GU0_F16_FULL,
+           TOL_GRADS_F16_FULL, TOL_LOSS, kink=False)   # the f16 forward's own error exceeds the kink bar
 
 
 def _params_of(sim, ctrl):

@@ -65,26 +65,16 @@ def test_f16_mode_refused_on_the_gemm_path():
         run_p(params, c, "f16")
 
 
-# FCR_PRECISION_F16_FWD (config 3 as BASELINE words it: "bf16 fwd / fp32 accum"): the forward is the f16 mode's
-# kernel, the backward the fp32-accurate one run on the f16 forward's stored states. Its gradients are
-# fp32-accurate gradients AT THE f16 TRAJECTORY, so against the fp64 oracle (exact trajectory) they carry the
-# forward's deviation, not the backward's: on the small golden batches that deviation dominates (B = 256:
-# g_W_inp 3.5e-3, g_b_inp 8.0e-3, the same as the f16 mode's), on a full batch it averages out — at B = 262 144 (r2c,
-# tests/test_gpu_fullsize.py) the controller-parameter gradients are within 3.4e-4..6.2e-4; per-trajectory
-# g_u0 8.7e-3 (each trajectory's own f16 deviation, up to 2.6e-3 in x̂, through the rollout's kinks).
-TOL_GRADS_F16FWD = TOL_GRADS         # controller-parameter gradients, golden batches (B <= 256)
-TOL_GRADS_F16FWD_FULL = 2e-3         # the same at B = 262 144
-TOL_GU0_F16FWD = 2e-2                # per-trajectory d loss / d u0
+# Full batch (tests/test_gpu_fullsize.py, B = 262 144): the controller-parameter gradients, sums over 2.6 M terms, average
+# the per-trajectory f16 deviations out (round 2: 2.4e-4 .. 4.2e-4); per-trajectory g_u0 carries each trajectory's own
+# (x̂ up to ~2.6e-3, through the rollout's kinks: ~1e-2).
+TOL_GRADS_F16_FULL = 2e-3            # controller-parameter gradients at B = 262 144
+TOL_GU0_F16_FULL = 2e-2              # per-trajectory d loss / d u0 at B = 262 144
 
 
-@pytest.mark.parametrize("name", [n for n in case_names() if load_case(n)[0]["H"] <= 52])
-def test_f16fwd_mode_within_stated_tolerance(name):
-    c, params = load_case(name)
-    o = run_p(params, c, "f16fwd")
-    h = run_p(params, c, "f16")
-    for k in T.FEATS + ("xhat",):      # the forward IS the f16 mode's kernel
-        assert np.array_equal(o[k], h[k]), k
-    assert abs(o["loss_scalar"] - float(c["loss64"])) <= TOL_LOSS * abs(float(c["loss64"]))
-    for k, _ in T.GRADS:
-        e = relerr(o[k], c[f"{k}_64"])
-        assert e <= (TOL_GU0_F16FWD if k == "g_u0" else TOL_GRADS_F16FWD), (k, e, "f16 mode:", relerr(h[k], c[f"{k}_64"]))
+def test_retired_f16fwd_mode_is_refused():
+    """precision "f16fwd" (f16 forward, fp32-accurate backward) was retired in ABI v5 (1.08x the fp32 step at the f16
+    mode's accuracy): the Python layer refuses the name, the C ABI the value."""
+    c, params = load_case("ref_b15_n10")
+    with pytest.raises(ValueError, match="precision"):
+        run_p(params, c, "f16fwd")
