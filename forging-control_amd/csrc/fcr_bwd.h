@@ -53,23 +53,32 @@ __device__ __forceinline__ void ld_quads(f32x4 (&dst)[Geo<HS>::HQ], __amdgpu_buf
     }
 }
 
+// the first RW words of a record (buf_store_rec's layout) into the first quads of dst
+template <int HS, int RW, int k = 0>
+__device__ __forceinline__ void ld_rec(f32x4 (&dst)[Geo<HS>::HQ], __amdgpu_buffer_rsrc_t r, uint32_t off, int lane) {
+    if constexpr (k < Geo<RW>::HQ) {
+        dst[k] = buf_ldq<quad_n<RW, k>()>(r, quad_voff<RW, k>(lane), off + quad_soff<RW, k>());
+        ld_rec<HS, RW, k + 1>(dst, r, off, lane);
+    }
+}
+
 // quad k alone (a small-batch wave's own slots, fcr_small.h)
 template <int HS, int k>
 __device__ __forceinline__ void ld_quad(f32x4 (&dst)[Geo<HS>::HQ], __amdgpu_buffer_rsrc_t r, uint32_t off, int lane) {
     dst[k] = buf_ldq<quad_n<HS, k>()>(r, quad_voff<HS, k>(lane), off + quad_soff<HS, k>());
 }
 
-template <int HS, bool NX_L0, bool NX_HC, bool NX_DIN>
+template <int HS, bool NX_L0, bool NX_HC, bool NX_DIN, bool LP = false>
 __device__ __forceinline__ void load_xhd(CellIn<HS> &ci, const NextIn &n, int lane) {
-    constexpr int HQ = Geo<HS>::HQ;
+    constexpr int RW = rec_words<HS, LP>();   // h records: hi halves only in the f16 mode
     if (NX_L0) {
         const f32x2 v = buf_ld2(n.rx, lane * 8, n.x);
         ci.x[0][0] = v[0];
         ci.x[0][1] = v[1];
     } else {
-        ld_quads<HS>(ci.x, n.rh, n.x, lane);
+        ld_rec<HS, RW>(ci.x, n.rh, n.x, lane);
     }
-    if (NX_HC) ld_quads<HS>(ci.h, n.rh, n.h, lane);
+    if (NX_HC) ld_rec<HS, RW>(ci.h, n.rh, n.h, lane);
     if (NX_DIN) ld_quads<HS>(ci.d, n.rd, n.d, lane);
 }
 
@@ -181,7 +190,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     auto slot_grad = [&](int r, f32x4 a, float *va, float *vb) {
         f32x4 P;
         f32x2 Q;
-        if (OWN) lstm_point_grad_h<FIRST>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], rec_h<HS>(ci.o, r), P, Q);
+        if (OWN) lstm_point_grad_h<FIRST>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], rec_h<HS, LP>(ci.o, r), P, Q);
         else lstm_point_grad<FIRST>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], P, Q);
         // torch LSTM semantics: dc = dc_carried + dh dh/dc; the carried dc of the cell below is dc f
         const float dcv = fmaf(dh[r], P[0], dc[r]);
@@ -258,7 +267,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
 #pragma unroll
         for (int k = 0; k < Geo<HS>::HQ; ++k) hkeep[k] = ci.h[k];
     }
-    load_xhd<HS, NX_L0, NX_HC, NX_DIN>(ci, nx, lane);   // x, h, din of this cell are consumed
+    load_xhd<HS, NX_L0, NX_HC, NX_DIN, LP>(ci, nx, lane);   // x, h, din of this cell are consumed
     // DG: the block leaves as it is formed (two 16-B stores per lane), and the trajectory's `down`
     auto dg_store = [&](int kbb, f16x8 h, f16x8 l) {
         if constexpr (DG) {
@@ -337,7 +346,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
 #pragma unroll
                 for (int k = 0; k < Geo<HS>::HQ; ++k) ci.o[k] = hkeep[k];
             } else {
-                ld_quads<HS>(ci.o, nx.rh, nx.o, lane);
+                ld_rec<HS, rec_words<HS, LP>()>(ci.o, nx.rh, nx.o, lane);
             }
         }
     }
@@ -462,7 +471,7 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
     CellIn<HS> ci;
     {
         const NextIn f = next_of(N - 1, 2, kL);   // t = kL -> (N-1, 2, 9)
-        load_xhd<HS, false, true, false>(ci, f, lane);
+        load_xhd<HS, false, true, false, LP>(ci, f, lane);
         ld_quads<HS>(ci.c, f.rc, f.c, lane);
     }
 

@@ -268,6 +268,33 @@ __device__ __forceinline__ void buf_store_quads(__amdgpu_buffer_rsrc_t r, uint32
         buf_store_quads<HS, k + 1>(r, off, v, lane);
     }
 }
+// Words of a cell's h record: the fp32-accurate split record holds [hi | lo] (HS words per lane); the f16 mode's
+// (LP) only the hi halves, ceil(HS / 2) words — its consumers never read a lo half (fcr_f16.h split_rec).
+template <int HS, bool LP>
+constexpr int rec_words() { return LP ? (HS + 1) / 2 : HS; }
+// The first RW words of a record array, stored in the compact layout of an RW-word record (a reader loads them
+// with ld_rec<RW>): the cell's space is the HS-word layout's, so offsets are unchanged and only the bytes shrink.
+template <int RW, int HS, int k = 0>
+__device__ __forceinline__ void buf_store_rec(__amdgpu_buffer_rsrc_t r, uint32_t off, const float (&v)[HS], int lane) {
+    static_assert(RW <= HS, "record words");
+    if constexpr (k < Geo<RW>::HQ) {
+        constexpr int n = quad_n<RW, k>();
+        const uint32_t vo = quad_voff<RW, k>(lane), so = off + quad_soff<RW, k>();
+        if constexpr (n == 4) {
+            buf_st4(r, vo, so, f32x4{v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]});
+        } else if constexpr (n == 3) {
+            typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
+            __builtin_amdgcn_raw_buffer_store_b96(u32x3{__builtin_bit_cast(unsigned, v[4 * k]), __builtin_bit_cast(unsigned, v[4 * k + 1]),
+                                                        __builtin_bit_cast(unsigned, v[4 * k + 2])},
+                                                  r, (int)vo, (int)so, 0);
+        } else if constexpr (n == 2) {
+            buf_st2(r, vo, so, f32x2{v[4 * k], v[4 * k + 1]});
+        } else {
+            buf_st1(r, vo, so, v[4 * k]);
+        }
+        buf_store_rec<RW, HS, k + 1>(r, off, v, lane);
+    }
+}
 template <int HS, int k = 0>
 __device__ __forceinline__ void buf_load_quads(float (&v)[HS], __amdgpu_buffer_rsrc_t r, uint32_t off, int lane) {
     if constexpr (k < Geo<HS>::HQ) {

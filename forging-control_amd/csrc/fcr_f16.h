@@ -215,9 +215,21 @@ __device__ __forceinline__ void fwd_operand(int kb, float x0, float x1, const fl
 // 0..HS-1)], hi = f16(h), lo = f16(h - hi), dword d = halves 2d (low) and 2d+1 (high). The B operands are
 // then assembled from record dwords with alignbit / perm (compile-time selects) instead of re-splitting fp32
 // values — the same halves, so the products are bit for bit those of a split at the consumer.
-template <int HS>
+// LP (the f16 mode, whose products take the hi halves only): words d < ceil(HS / 2) = hi halves 2d, 2d + 1 — half the
+// record's bytes; the remaining words are left as they are (never stored nor read).
+template <int HS, bool LP = false>
 __device__ __forceinline__ void split_rec(const float (&h)[HS], float (&r)[HS]) {
     typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    if constexpr (LP) {
+#pragma unroll
+        for (int d = 0; d < (HS + 1) / 2; ++d) {
+            f16x2 v;
+            v[0] = (_Float16)h[2 * d];
+            v[1] = 2 * d + 1 < HS ? (_Float16)h[2 * d + 1 < HS ? 2 * d + 1 : 0] : (_Float16)0.0f;
+            r[d] = __builtin_bit_cast(float, v);
+        }
+        return;
+    }
     float one = 1.0f;
     asm("" : "+v"(one));   // keeps the v_fma_mix form (a constant 1 folds the fma away)
     _Float16 hh[HS], ll[HS];
@@ -365,8 +377,13 @@ __device__ __forceinline__ void lstm_point_grad(f32x4 a, float c_prev, f32x4 &P,
 // hi + lo in ONE v_fma_mix_f32 (f16 sources picked by op_sel; exact in fp32) — the compiler's form of the
 // same sum is two conversions and an add. A VALU-to-VALU dependency: no MFMA operand hazard. s is a
 // compile-time constant once the cell is unrolled: one of the four op_sel forms survives.
-template <int HS>
+template <int HS, bool LP = false>
 __device__ __forceinline__ float rec_h(const f32x4 *rec, int s) {
+    if constexpr (LP) {   // the f16 mode's record: hi only
+        typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+        const int wh = s >> 1;
+        return (float)__builtin_bit_cast(f16x2, rec[wh >> 2][wh & 3])[s & 1];
+    }
     const int wh = s >> 1, wl = (HS + s) >> 1;
     const float a = rec[wh >> 2][wh & 3], b = rec[wl >> 2][wl & 3];
     float r;

@@ -181,6 +181,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
     float xh0 = 0.0f, xh1 = 0.0f, xh2 = 0.0f, xh3 = 0.0f;
 
     float c[HS], hout[HS], hp[HS], xc[HS], xn[HS];   // hp, xc, xn: split records (fcr_f16.h)
+    constexpr int kRW = rec_words<HS, LP>();         // words of an h record (hi halves only in the f16 mode)
     // sequence slabs [wave][j][layer][t][quad][64]: the split record of h of every cell (layers 0, 1: the
     // next phase's input; with STORE also layer 2) and, with STORE, c; plus the window rows [wave][j][t][64]
     const size_t qcell = (size_t)Geo<HS>::QC;    // one cell of a sequence slab, in 16-B units
@@ -235,21 +236,21 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
                 rot_left(w0);
                 rot_left(w1);
                 fwd16_cell<HS, true, true, LP>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
-                split_rec<HS>(hout, hp);
+                split_rec<HS, LP>(hout, hp);
                 if (STORE) {
-                    buf_store_quads<HS>(rh, SEQ_O(0, 0), hp, lane);
+                    buf_store_rec<kRW>(rh, SEQ_O(0, 0), hp, lane);
                     buf_st2(rx, lane * 8, (uint32_t)(j * kL * kWave * 8), f32x2{x0, x1});
                     buf_store_quads<HS>(rc, SEQ_O(0, 0), c, lane);
                 }
                 fwd16_cell<HS, false, true, LP>(lw1, lane, 0.0f, 0.0f, hp, h1, c1, hout, turn);
-                split_rec<HS>(hout, h1);
-                if (STORE || !LP) buf_store_quads<HS>(rh, SEQ_O(1, 0), h1, lane);   // f16 mode: layer 2 is in this phase
+                split_rec<HS, LP>(hout, h1);
+                if (STORE || !LP) buf_store_rec<kRW>(rh, SEQ_O(1, 0), h1, lane);   // f16 mode: layer 2 is in this phase
                 if (STORE) buf_store_quads<HS>(rc, SEQ_O(1, 0), c1, lane);
                 if constexpr (LP) {   // every layer resident: layer 2 joins the phase (its h_t from registers as well)
                     fwd16_cell<HS, false, true, LP>(lwl[2], lane, 0.0f, 0.0f, h1, h2, c2, hout, turn);
-                    split_rec<HS>(hout, h2);
+                    split_rec<HS, LP>(hout, h2);
                     if (STORE) {
-                        buf_store_quads<HS>(rh, SEQ_O(2, 0), h2, lane);
+                        buf_store_rec<kRW>(rh, SEQ_O(2, 0), h2, lane);
                         buf_store_quads<HS>(rc, SEQ_O(2, 0), c2, lane);
                     }
                 }
@@ -259,22 +260,22 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
                 rot_left(w0);
                 rot_left(w1);
                 fwd16_cell<HS, true, false, LP>(lw0, lane, x0, x1, hp, hp, c, hout, turn);
-                split_rec<HS>(hout, hp);
+                split_rec<HS, LP>(hout, hp);
                 if (STORE) {
-                    buf_store_quads<HS>(rh, SEQ_O(0, t), hp, lane);
+                    buf_store_rec<kRW>(rh, SEQ_O(0, t), hp, lane);
                     buf_st2(rx, lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{x0, x1});
                     if (t + 1 < kL) buf_store_quads<HS>(rc, SEQ_O(0, t), c, lane);   // c_9 is never a c_{t-1}
                 }
                 fwd16_cell<HS, false, false, LP>(lw1, lane, 0.0f, 0.0f, hp, h1, c1, hout, turn);
-                split_rec<HS>(hout, h1);
-                if (STORE || !LP) buf_store_quads<HS>(rh, SEQ_O(1, t), h1, lane);
+                split_rec<HS, LP>(hout, h1);
+                if (STORE || !LP) buf_store_rec<kRW>(rh, SEQ_O(1, t), h1, lane);
                 if (STORE && t + 1 < kL) buf_store_quads<HS>(rc, SEQ_O(1, t), c1, lane);
                 if constexpr (LP) {
                     fwd16_cell<HS, false, false, LP>(lwl[2], lane, 0.0f, 0.0f, h1, h2, c2, hout, turn);
                     if (t + 1 < kL) {   // h_9 of layer 2 only feeds the readout (fp32 hout)
-                        split_rec<HS>(hout, h2);
+                        split_rec<HS, LP>(hout, h2);
                         if (STORE) {
-                            buf_store_quads<HS>(rh, SEQ_O(2, t), h2, lane);
+                            buf_store_rec<kRW>(rh, SEQ_O(2, t), h2, lane);
                             buf_store_quads<HS>(rc, SEQ_O(2, t), c2, lane);
                         }
                     }
@@ -293,8 +294,8 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             buf_load_quads<HS>(xc, rh, SEQ_O(l - 1, 0), lane);
             buf_load_quads<HS>(xn, rh, SEQ_O(l - 1, 1), lane);
             fwd16_cell<HS, false, true, LP>(lwc, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
-            split_rec<HS>(hout, hp);
-            if (STORE) buf_store_quads<HS>(rh, SEQ_O(l, 0), hp, lane);
+            split_rec<HS, LP>(hout, hp);
+            if (STORE) buf_store_rec<kRW>(rh, SEQ_O(l, 0), hp, lane);
             if (STORE) buf_store_quads<HS>(rc, SEQ_O(l, 0), c, lane);
 #pragma unroll
             for (int r = 0; r < HS; ++r) xc[r] = xn[r];
@@ -303,8 +304,8 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
                 buf_load_quads<HS>(xn, rh, SEQ_O(l - 1, t + 1 < kL ? t + 1 : t), lane);
                 fwd16_cell<HS, false, false, LP>(lwc, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
                 if (t + 1 < kL) {   // h_9 of layer 2 only feeds the readout (fp32 hout)
-                    split_rec<HS>(hout, hp);
-                    if (STORE) buf_store_quads<HS>(rh, SEQ_O(l, t), hp, lane);
+                    split_rec<HS, LP>(hout, hp);
+                    if (STORE) buf_store_rec<kRW>(rh, SEQ_O(l, t), hp, lane);
                 }
                 if (STORE && t + 1 < kL) buf_store_quads<HS>(rc, SEQ_O(l, t), c, lane);
 #pragma unroll
