@@ -116,8 +116,7 @@ Layout make_layout(const fcr_dims *d, int with_backward) {
     Layout L{};
     L.HS = slot_tier(d->H);
     L.nw = (d->B + kTile - 1) / kTile;
-    constexpr int kPad = kFwdWaves > kBwdWaves ? kFwdWaves : kBwdWaves;
-    L.nw_pad = (L.nw + kPad - 1) / kPad * kPad;  // covers both launch geometries
+    L.nw_pad = (L.nw + kWavePad - 1) / kWavePad * kWavePad;  // covers every launch geometry
     size_t off = 0;
     auto take = [&](size_t bytes) {
         const size_t o = off;
@@ -173,15 +172,16 @@ Packed packed_ptrs(const Layout &L, char *ws) {
 template <int HS, bool STORE, bool LP>
 int launch_fwd_t(const FwdArgs &fa, const Layout &L, hipStream_t s) {
     const int lds = LP ? Geo16<HS>::LDS_FWD_LP : Geo16<HS>::LDS_FWD;
+    // the f16 mode's forward with stored states fits three waves per SIMD (fcr_fwd.h)
+    constexpr int W = (LP && STORE && HS == 13) ? kFwdWavesLP : kFwdWaves;
     static bool attr_set = false;
     if (!attr_set) {
-        const hipError_t e = hipFuncSetAttribute((const void *)fcr_fwd_kernel<HS, STORE, LP>,
+        const hipError_t e = hipFuncSetAttribute((const void *)fcr_fwd_kernel<HS, STORE, LP, W>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(fwd): %s", hipGetErrorString(e));
         attr_set = true;
     }
-    hipLaunchKernelGGL((fcr_fwd_kernel<HS, STORE, LP>), dim3(L.nw_pad / kFwdWaves), dim3(kFwdWaves * kWave),
-                       lds, s, fa);
+    hipLaunchKernelGGL((fcr_fwd_kernel<HS, STORE, LP, W>), dim3(L.nw_pad / W), dim3(W * kWave), lds, s, fa);
     return launch_check("fcr_fwd_kernel");
 }
 
@@ -1078,8 +1078,7 @@ SurLayout make_sur(const fcr_dims *d, int with_backward) {
     SurLayout L{};
     L.HS = slot_tier(d->H);
     L.nw = (d->B + kTile - 1) / kTile;
-    constexpr int kPad = kFwdWaves > kBwdWaves ? kFwdWaves : kBwdWaves;
-    L.nw_pad = (L.nw + kPad - 1) / kPad * kPad;
+    L.nw_pad = (L.nw + kWavePad - 1) / kWavePad * kWavePad;
     const int nkb = sur_nkb(L.nw);
     L.groups = nkb < kSurWgMaxGroups ? nkb : kSurWgMaxGroups;
     size_t off = 0;

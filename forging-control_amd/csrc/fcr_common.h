@@ -23,6 +23,8 @@ constexpr int kCtrlIn = 3;       // [y_dot, z, ref]
 constexpr int kMS = 13;          // controller hidden slots (units 4m+q), hidden <= 52
 constexpr int kFnpStride = 8;    // floats per (m, q) controller record: W0 W1 W2 b wout 0 0 0
 constexpr int kFwdWaves = 8;     // waves per forward workgroup (2 per SIMD)
+constexpr int kFwdWavesLP = 12;  // f16-mode forward with stored states (168 VGPRs): 3 per SIMD
+constexpr int kWavePad = 24;     // workspace wave padding: a multiple of every launch geometry
 constexpr int kBwdWaves = 8;     // waves per backward workgroup (2 per SIMD)
 constexpr float kP1Max = 2.122366f;  // Functions.py:1411 (32e6 / p1 max_abs_)
 constexpr float kP2Max = 1.036233f;  // Functions.py:1411 (32e6 / p2 max_abs_)

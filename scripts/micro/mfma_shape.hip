@@ -34,8 +34,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kSteps = 8;   // MFMA steps per iteration (one dependency round trip per iteration)
 
 // SH: 16 or 32. V / T: plain VALU and transcendentals per MFMA (times 16 to allow fractions: V16 = 16 V).
-template <int SH, int V16, int T16, int ILP>
-__global__ __launch_bounds__(512, 2) void mix_kernel(const _Float16 *__restrict__ src, float *__restrict__ dst, int iters,
+template <int SH, int V16, int T16, int ILP, int WPB = 8>
+__global__ __launch_bounds__(64 * WPB, WPB == 8 ? 2 : 1) void mix_kernel(const _Float16 *__restrict__ src, float *__restrict__ dst, int iters,
                                                      unsigned long long *clk) {
     constexpr int CH = SH == 16 ? 4 : 2;             // independent accumulator chains
     constexpr int NV = (V16 * CH * kSteps) / 16;     // plain VALU per iteration
@@ -102,18 +102,24 @@ __global__ __launch_bounds__(512, 2) void mix_kernel(const _Float16 *__restrict_
     }
 }
 
-template <int SH, int V16, int T16, int ILP = 8>
+// WPB 8: eight waves per workgroup, two per SIMD; WPB 4 with 160 KB of (unused) LDS: one workgroup per CU, one wave per
+// SIMD — what a 32-trajectory cell whose state needs more than 256 registers would run at. PAD16: MFMA work per unit of
+// useful work x 16 (the 32x32 tile covers 8 units: 56 for H = 50 against 52 on 16x16 tiles, 17/16 ~ 1.077 -> the
+// VALU of a variant with padding is its unpadded VALU / 1.077, and its useful FLOP the executed / 1.077).
+template <int SH, int V16, int T16, int ILP = 8, int WPB = 8, int PAD16 = 16>
 void run(const char *tag, const _Float16 *src, float *dst, unsigned long long *clk, int iters, double target_s) {
     const int waves = SH == 16 ? 4096 : 2048;
-    const int blocks = waves / 8;
+    const int blocks = waves / WPB;
+    const int lds = WPB == 8 ? 0 : 160 * 1024;
+    if (lds) CHECK(hipFuncSetAttribute((const void *)mix_kernel<SH, V16, T16, ILP, WPB>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
     // warm-up and sizing
-    hipLaunchKernelGGL((mix_kernel<SH, V16, T16, ILP>), dim3(blocks), dim3(512), 0, 0, src, dst, iters, clk);
+    hipLaunchKernelGGL((mix_kernel<SH, V16, T16, ILP, WPB>), dim3(blocks), dim3(64 * WPB), lds, 0, src, dst, iters, clk);
     CHECK(hipDeviceSynchronize());
     CHECK(hipEventRecord(e0));
-    hipLaunchKernelGGL((mix_kernel<SH, V16, T16, ILP>), dim3(blocks), dim3(512), 0, 0, src, dst, iters, clk);
+    hipLaunchKernelGGL((mix_kernel<SH, V16, T16, ILP, WPB>), dim3(blocks), dim3(64 * WPB), lds, 0, src, dst, iters, clk);
     CHECK(hipEventRecord(e1));
     CHECK(hipEventSynchronize(e1));
     float ms1 = 0.0f;
@@ -122,7 +128,7 @@ void run(const char *tag, const _Float16 *src, float *dst, unsigned long long *c
     if (reps < 3) reps = 3;
     CHECK(hipEventRecord(e0));
     for (int r = 0; r < reps; ++r)
-        hipLaunchKernelGGL((mix_kernel<SH, V16, T16, ILP>), dim3(blocks), dim3(512), 0, 0, src, dst, iters, clk);
+        hipLaunchKernelGGL((mix_kernel<SH, V16, T16, ILP, WPB>), dim3(blocks), dim3(64 * WPB), lds, 0, src, dst, iters, clk);
     CHECK(hipEventRecord(e1));
     CHECK(hipEventSynchronize(e1));
     float ms = 0.0f;
@@ -136,9 +142,10 @@ void run(const char *tag, const _Float16 *src, float *dst, unsigned long long *c
     free(h);
     constexpr int CH = SH == 16 ? 4 : 2;
     const double flop = (double)waves * iters * kSteps * CH * (SH == 16 ? 16.0 * 16 * 32 : 32.0 * 32 * 16) * 2;
-    printf("{\"tag\": \"%s\", \"ilp\": %d, \"shape\": \"%dx%dx%d\", \"valu_per_mfma\": %.3f, \"trans_per_mfma\": %.3f, \"waves\": %d, "
+    const double useful_ms = ms * PAD16 / 16.0;   // time per unit of useful work, padding charged
+    printf("{\"tag\": \"%s\", \"waves_per_simd\": %d, \"pad\": %.3f, \"ms_per_useful\": %.4f, \"ilp\": %d, \"shape\": \"%dx%dx%d\", \"valu_per_mfma\": %.3f, \"trans_per_mfma\": %.3f, \"waves\": %d, "
            "\"ms\": %.4f, \"tflops\": %.1f, \"clock_ghz\": %.3f, \"cycles_per_mfma_per_simd\": %.2f}\n",
-           tag, SH == 16 ? ILP : 2 * ILP, SH, SH, SH == 16 ? 32 : 16, V16 / 16.0, T16 / 16.0, waves, ms, flop / (ms * 1e-3) / 1e12, ghz,
+           tag, WPB == 8 ? 2 : 1, PAD16 / 16.0, useful_ms, SH == 16 ? ILP : 2 * ILP, SH, SH, SH == 16 ? 32 : 16, V16 / 16.0, T16 / 16.0, waves, ms, flop / (ms * 1e-3) / 1e12, ghz,
            ghz * 1e9 * ms * 1e-3 / ((double)waves / 1024 * iters * kSteps * CH));
     fflush(stdout);
 }
@@ -169,6 +176,11 @@ int main(int argc, char **argv) {
     // less independent VALU work per lane (the real cell's chains are short: 64 % issue efficiency at two waves)
     run<16, 39, 7, 4>("bwd_mix_ilp", src, dst, clk, iters, target_s);
     run<32, 78, 14, 4>("bwd_mix_ilp", src, dst, clk, iters, target_s);
+    // the 32-trajectory cell as it would be built: 56 units on 32x32 tiles against 52 (MFMA work x 17/16 per useful
+    // work, its VALU unchanged per useful work: 78 / (17/16) = 73, 14 -> 13), at two and at one wave per SIMD
+    run<32, 73, 13, 8, 8, 17>("bwd_mix_pad", src, dst, clk, iters, target_s);
+    run<32, 73, 13, 8, 4, 17>("bwd_mix_pad_1wave", src, dst, clk, iters, target_s);
+    run<32, 73, 13, 4, 4, 17>("bwd_mix_pad_1wave_ilp", src, dst, clk, iters, target_s);
     // order reversed (DVFS drift check)
     run<32, 78, 14>("bwd_mix_rev", src, dst, clk, iters, target_s);
     run<16, 39, 7>("bwd_mix_rev", src, dst, clk, iters, target_s);
