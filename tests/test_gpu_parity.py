@@ -249,13 +249,17 @@ def test_wide_path_any_incoming_gradient_scale(dloss):
         assert relerr(o[k] / dloss, c[f"{k}_64"]) <= TOL, (k, relerr(o[k] / dloss, c[f"{k}_64"]))
 
 
-@pytest.mark.parametrize("H,B,N", [(54, 300, 3), (57, 77, 2), (96, 520, 4), (64, 129, 2), (128, 300, 3)])
+@pytest.mark.parametrize("H,B,N", [(54, 300, 3), (57, 77, 2), (96, 520, 4), (64, 129, 2), (128, 300, 3), (192, 260, 2),
+                                   (200, 140, 2), (264, 130, 2)])
 def test_wide_path_hidden_sizes(H, B, N):
     """H > 52 at sizes the golden cases do not hit: even H not a multiple of 4 (cell kernels 2 units per
     thread), odd H (1 unit per thread), a multiple of 4 at a few hundred trajectories, and multiples of 64
     (the fused GEMM + cell kernel, fcr_wgemm.h) with a ragged last block of 128 trajectories — the window-row
-    columns inside layer 0's split GEMM and the combined [input gradient | dh] backward products, against
-    the fp64 oracle on seeded synthetic weights (parity unpinned: no reference output at these sizes)."""
+    columns inside layer 0's split GEMM and the combined [input gradient | dh] backward products. The fused
+    backward cell (fcr_wbwd.h, H % 8 == 0 and H <= 256): one column block (H <= 128), two with the dh columns
+    straddling them (H = 192, 200: the row bounds' partial slots), the rocBLAS forward beside it (H = 200); H = 264
+    the rocBLAS backward path. Against the fp64 oracle on seeded synthetic weights (parity unpinned: no reference
+    output at these sizes)."""
     from tests.golden.make_golden import synth_params
     params = synth_params(H, 300 + H)
     X, S, _ = _synth(B, N, 400 + H)
