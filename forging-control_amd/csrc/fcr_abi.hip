@@ -201,7 +201,8 @@ int launch_bwd_t(const BwdArgs &ba, const Layout &L, hipStream_t s) {
         if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(bwd): %s", hipGetErrorString(e));
         attr_set = true;
     }
-    hipLaunchKernelGGL((fcr_bwd_kernel<HS, LP>), dim3(L.nw_pad / kBwdWaves), dim3(kBwdWaves * kWave), lds, s, ba);
+    constexpr int W = LP ? kBwdWavesLP : kBwdWaves;
+    hipLaunchKernelGGL((fcr_bwd_kernel<HS, LP>), dim3(L.nw_pad / W), dim3(W * kWave), lds, s, ba);
     return launch_check("fcr_bwd_kernel");
 }
 

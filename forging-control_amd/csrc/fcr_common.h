@@ -26,6 +26,7 @@ constexpr int kFwdWaves = 8;     // waves per forward workgroup (2 per SIMD)
 constexpr int kFwdWavesLP = 12;  // f16-mode forward with stored states (168 VGPRs): 3 per SIMD
 constexpr int kWavePad = 24;     // workspace wave padding: a multiple of every launch geometry
 constexpr int kBwdWaves = 8;     // waves per backward workgroup (2 per SIMD)
+constexpr int kBwdWavesLP = 12;  // f16-mode backward: 3 per SIMD
 constexpr float kP1Max = 2.122366f;  // Functions.py:1411 (32e6 / p1 max_abs_)
 constexpr float kP2Max = 1.036233f;  // Functions.py:1411 (32e6 / p2 max_abs_)
 

@@ -24,14 +24,38 @@ from bench import load_weights, synth_batch  # noqa: E402
 _n = fca._native
 
 
+class _V4:
+    """An ABI v4 library (round 3: no fcr_options argument) behind the v5 call signatures used below."""
+
+    def __init__(self, lib):
+        self.lib = lib
+
+    def fcr_workspace_size(self, d, o, wb, nb):
+        return self.lib.fcr_workspace_size(d, wb, nb)
+
+    def fcr_forward(self, d, o, *rest):
+        return self.lib.fcr_forward(d, *rest)
+
+    def fcr_backward(self, d, o, *rest):
+        return self.lib.fcr_backward(d, *rest)
+
+    def fcr_last_error(self):
+        return self.lib.fcr_last_error()
+
+
 def bind(path):
     lib = ctypes.CDLL(os.path.abspath(path))
     vp, i32, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    lib.fcr_last_error.restype = ctypes.c_char_p
+    if lib.fcr_abi_version() < 5:   # round-3 builds: the same calls without the options pointer
+        lib.fcr_workspace_size.argtypes = [ctypes.POINTER(_n.FcrDims), i32, ctypes.POINTER(sz)]
+        lib.fcr_forward.argtypes = [ctypes.POINTER(_n.FcrDims), ctypes.POINTER(_n.FcrWeights)] + [vp] * 10 + [i32, vp, sz, vp]
+        lib.fcr_backward.argtypes = [ctypes.POINTER(_n.FcrDims)] + [vp] * 8 + [vp, sz, vp]
+        return _V4(lib)
     po = ctypes.POINTER(_n.FcrOptions)   # ABI v5 (include/fcr.h)
     lib.fcr_workspace_size.argtypes = [ctypes.POINTER(_n.FcrDims), po, i32, ctypes.POINTER(sz)]
     lib.fcr_forward.argtypes = [ctypes.POINTER(_n.FcrDims), po, ctypes.POINTER(_n.FcrWeights)] + [vp] * 10 + [i32, vp, sz, vp]
     lib.fcr_backward.argtypes = [ctypes.POINTER(_n.FcrDims), po] + [vp] * 8 + [vp, sz, vp]
-    lib.fcr_last_error.restype = ctypes.c_char_p
     return lib
 
 
@@ -65,6 +89,12 @@ def main(return_state=False):
         w.w_hh[k] = getattr(sim.lstm, f"weight_hh_l{k}").data_ptr()
     w.fc_w, w.fc_b = sim.fc.weight.data_ptr(), sim.fc.bias.data_ptr()
     libs = [bind(p) for p in a.libs]
+    for lib in libs:   # ABI v4 builds take the keep budget / small-batch limit process-wide
+        if isinstance(lib, _V4) and a.keep_budget is not None:
+            lib.lib.fcr_set_wide_keep_budget.argtypes = [ctypes.c_int64]
+            lib.lib.fcr_set_wide_keep_budget(a.keep_budget)
+        if isinstance(lib, _V4) and a.small_limit is not None:
+            lib.lib.fcr_set_small_batch_limit(a.small_limit)
     need = []
     for lib in libs:
         nb = ctypes.c_size_t()
