@@ -249,16 +249,19 @@ def grad_check(sim, ctrl, X, S, N, dev, precision, B_check=None):
             t32_b = float(e32[~reg].max()) if (~reg).any() else 0.0
             # a band g_u0 above 1e-5 must be the fp64 one-sided derivative of its kink (u0 shifted by +-d): a flip
             flagged = torch.nonzero(~reg & (e > 1e-5)).reshape(-1).tolist()
-            side = T.one_sided_g_u0(params, X, u.detach(), S, N, ALPHA, flagged, B, device=dev)
+            # one fp64 rollout per shift and trajectory: the fp32-accurate mode's few flips only
+            examine = precision == "fp32" and len(flagged) <= 64
+            side = T.one_sided_g_u0(params, X, u.detach(), S, N, ALPHA, flagged, B, device=dev) if examine else {}
             flips = []
-            for i in flagged:
+            for i in (flagged if examine else []):
                 g = float(a[i])
                 best = min(side[i], key=lambda sg: abs(g - sg[1]))
                 flips.append({"trajectory": i, "err_at_u0": float(e[i]), "one_sided_shift": best[0],
                               "err_one_sided": abs(g - best[1]) / float(den)})
             band = {"trajectories": int((~reg).sum()), "max_rel_err": hip_b, "above_1e-5": len(flagged),
                     "torch_fp32_max_rel_err": t32_b, "torch_fp32_above_1e-5": int((e32[~reg] > 1e-5).sum()),
-                    "flips": flips, "flips_explained": all(f["err_one_sided"] <= 1e-5 for f in flips),
+                    "flips": flips, "flips_examined": examine,
+                    "flips_explained": examine and all(f["err_one_sided"] <= 1e-5 for f in flips),
                     "rule": "every band g_u0 above 1e-5 equals an fp64 one-sided derivative at u0 +- d within 1e-5"}
             a, r = a[reg], r[reg]
         err[k] = float((a - r).abs().max() / den)
