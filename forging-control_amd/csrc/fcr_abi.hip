@@ -116,7 +116,8 @@ Layout make_layout(const fcr_dims *d, int with_backward) {
     Layout L{};
     L.HS = slot_tier(d->H);
     L.nw = (d->B + kTile - 1) / kTile;
-    L.nw_pad = (L.nw + kWavePad - 1) / kWavePad * kWavePad;  // covers every launch geometry
+    constexpr int kPad = kFwdWaves > kBwdWaves ? kFwdWaves : kBwdWaves;
+    L.nw_pad = (L.nw + kPad - 1) / kPad * kPad;  // covers both launch geometries
     size_t off = 0;
     auto take = [&](size_t bytes) {
         const size_t o = off;
@@ -172,16 +173,15 @@ Packed packed_ptrs(const Layout &L, char *ws) {
 template <int HS, bool STORE, bool LP>
 int launch_fwd_t(const FwdArgs &fa, const Layout &L, hipStream_t s) {
     const int lds = LP ? Geo16<HS>::LDS_FWD_LP : Geo16<HS>::LDS_FWD;
-    // the f16 mode's forward with stored states fits three waves per SIMD (fcr_fwd.h)
-    constexpr int W = (LP && STORE && HS == 13) ? kFwdWavesLP : kFwdWaves;
     static bool attr_set = false;
     if (!attr_set) {
-        const hipError_t e = hipFuncSetAttribute((const void *)fcr_fwd_kernel<HS, STORE, LP, W>,
+        const hipError_t e = hipFuncSetAttribute((const void *)fcr_fwd_kernel<HS, STORE, LP>,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(fwd): %s", hipGetErrorString(e));
         attr_set = true;
     }
-    hipLaunchKernelGGL((fcr_fwd_kernel<HS, STORE, LP, W>), dim3(L.nw_pad / W), dim3(W * kWave), lds, s, fa);
+    hipLaunchKernelGGL((fcr_fwd_kernel<HS, STORE, LP>), dim3(L.nw_pad / kFwdWaves), dim3(kFwdWaves * kWave),
+                       lds, s, fa);
     return launch_check("fcr_fwd_kernel");
 }
 
@@ -201,8 +201,7 @@ int launch_bwd_t(const BwdArgs &ba, const Layout &L, hipStream_t s) {
         if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(bwd): %s", hipGetErrorString(e));
         attr_set = true;
     }
-    constexpr int W = LP ? kBwdWavesLP : kBwdWaves;
-    hipLaunchKernelGGL((fcr_bwd_kernel<HS, LP>), dim3(L.nw_pad / W), dim3(W * kWave), lds, s, ba);
+    hipLaunchKernelGGL((fcr_bwd_kernel<HS, LP>), dim3(L.nw_pad / kBwdWaves), dim3(kBwdWaves * kWave), lds, s, ba);
     return launch_check("fcr_bwd_kernel");
 }
 
@@ -629,7 +628,7 @@ int launch_fb(const WbArgs &wa, bool l0, hipStream_t s) {
         if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(wbwd): %s", hipGetErrorString(e));
         attr_set[l0] = true;
     }
-    if (wa.NO < 0 || wa.NO > 2 * kWbM || wa.NO % 16 || wa.H % 8 || wa.H > kWbMaxH || wa.NB <= 0 || wa.ldo % 4 ||
+    if (wa.NO < 0 || wa.NO > 2 * kWbM || wa.NO % 4 || wa.H % 8 || wa.H > kWbMaxH || wa.NB <= 0 || wa.ldo % 4 ||
         wa.ldh % 2 || wa.ldx % 2 || (l0 && (!wa.wih0 || !wa.rowg)))
         return fail(FCR_EINVAL, "wide_bwd_fused_kernel: NO %d H %d B %d ldo %d off its tiling", wa.NO, wa.H, wa.NB, wa.ldo);
     const int nx = (wa.NB + kWbN - 1) / kWbN, ny = wa.NO > 0 ? (wa.NO + kWbM - 1) / kWbM : 1;
@@ -1079,7 +1078,8 @@ SurLayout make_sur(const fcr_dims *d, int with_backward) {
     SurLayout L{};
     L.HS = slot_tier(d->H);
     L.nw = (d->B + kTile - 1) / kTile;
-    L.nw_pad = (L.nw + kWavePad - 1) / kWavePad * kWavePad;
+    constexpr int kPad = kFwdWaves > kBwdWaves ? kFwdWaves : kBwdWaves;
+    L.nw_pad = (L.nw + kPad - 1) / kPad * kPad;
     const int nkb = sur_nkb(L.nw);
     L.groups = nkb < kSurWgMaxGroups ? nkb : kSurWgMaxGroups;
     size_t off = 0;

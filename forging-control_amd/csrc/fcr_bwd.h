@@ -96,7 +96,9 @@ constexpr float kInvNegLog2e = 1.0f / kNegLog2e;
 // recomputed forward tiles 2kb+2, 2kb+3 and their gradients, which form block kb+1.
 // OWN: the cell's own h_t record is in ci.o (every cell but the first of a window's layer-2 phase, whose h_9
 // only fed the readout): tanh(c_t) comes from it (lstm_point_grad_h) instead of being re-evaluated.
-// NX_OWN: the next cell's is fetched.
+// NX_OWN: the next cell's is fetched. Not in the f16 mode: its records hold f16(h) only, and tanh(c_t) = h / o from
+// an f16 h loses the local derivative 1 - tanh^2 c near saturation (g_u0 2.8e-2 off the oracle at B = 15 with it):
+// tanh(c_t) is re-evaluated from the fp32 c record.
 #ifndef FCR_STAMP
 #define FCR_STAMP 0   // diagnostic: per-wave s_memtime sums of the cell's sections (ws tail)
 #endif
@@ -118,18 +120,12 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
                                          float &dx4, CellIn<HS> &ci, const NextIn &nx, Stamps &sp,
                                          const DgOut *dgo = nullptr) {
     const unsigned long long t0 = stamp_now();
+    constexpr bool OWNH = OWN && !LP, NX_OWNH = NX_OWN && !LP;   // tanh(c_t) from the h record (fp32 mode)
     // the two waves of a SIMD take turns at the higher issue priority, cell by cell, so neither runs
     // ahead of the other between the phase barriers (oldest-first arbitration otherwise skews them)
-    // (the f16 mode runs three waves per SIMD: each has the higher priority every third cell)
-    if constexpr (LP) {
-        if (sp.t[4] == 2) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-        sp.t[4] = sp.t[4] == 2 ? 0 : sp.t[4] + 1;
-    } else {
-        if (sp.t[4] & 1) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-        sp.t[4] ^= 1;
-    }
+    if (sp.t[4] & 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+    sp.t[4] ^= 1;
     using I = Img<HS, L0>;
     using G = Geo16<HS>;
     constexpr int KB = I::KB, NB = I::NB, KBB = I::KBB;
@@ -197,7 +193,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     auto slot_grad = [&](int r, f32x4 a, float *va, float *vb) {
         f32x4 P;
         f32x2 Q;
-        if (OWN) lstm_point_grad_h<FIRST>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], rec_h<HS, LP>(ci.o, r), P, Q);
+        if (OWNH) lstm_point_grad_h<FIRST>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], rec_h<HS>(ci.o, r), P, Q);
         else lstm_point_grad<FIRST>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], P, Q);
         // torch LSTM semantics: dc = dc_carried + dh dh/dc; the carried dc of the cell below is dc f
         const float dcv = fmaf(dh[r], P[0], dc[r]);
@@ -268,7 +264,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     }
     // OWN_REG: the next cell (t - 1, same phase) owns h_{t-1}, whose record this cell has in ci.h: kept in registers
     // for it instead of re-read from the slab (an L2 miss by then)
-    constexpr bool OWN_REG = NX_OWN && !FIRST;
+    constexpr bool OWN_REG = NX_OWNH && !FIRST;
     f32x4 hkeep[Geo<HS>::HQ];
     if constexpr (OWN_REG) {
 #pragma unroll
@@ -348,12 +344,12 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
             dg_store(kbb + 1, gh[nu], gl[nu]);
         }
         // every slot's own h consumed: the next cell's record comes in (an L2 hit: this cell read it as h_{t-1})
-        if (NX_OWN && kbb + 2 == KBB) {
+        if (NX_OWNH && kbb + 2 == KBB) {
             if constexpr (OWN_REG) {
 #pragma unroll
                 for (int k = 0; k < Geo<HS>::HQ; ++k) ci.o[k] = hkeep[k];
             } else {
-                ld_rec<HS, rec_words<HS, LP>()>(ci.o, nx.rh, nx.o, lane);
+                ld_quads<HS>(ci.o, nx.rh, nx.o, lane);
             }
         }
     }
@@ -397,9 +393,8 @@ struct BwdLds {
     static_assert(I1::HALF % 16 == 0 && I0::HALF % 16 == 0, "images must be whole 16-B chunks");
 };
 
-// W waves per workgroup: kBwdWaves (two per SIMD); the f16 mode kBwdWavesLP (three per SIMD, <= 168 VGPRs)
-template <int HS, bool LP, int W = LP ? kBwdWavesLP : kBwdWaves>
-__global__ __launch_bounds__(W * kWave, W / 4) void fcr_bwd_kernel(BwdArgs a) {
+template <int HS, bool LP>
+__global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kernel(BwdArgs a) {
     using LD = BwdLds<HS, LP>;
     using I1 = Img<HS, false>;
     using I0 = Img<HS, true>;
@@ -418,7 +413,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void fcr_bwd_kernel(BwdArgs a) {
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int q = lane >> 4, sl = lane & 15;
-    const int wave = blockIdx.x * W + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wave = blockIdx.x * kBwdWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int b = wave * kTile + sl;
     const bool valid = b < a.B;
     const int bc = valid ? b : a.B - 1;
@@ -474,7 +469,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void fcr_bwd_kernel(BwdArgs a) {
         n.d = (uint32_t)((nl < 2 ? doff(nj, nl + 1, nt) : 0) * 16);
         return n;
     };
-    Stamps sp = {{0, 0, 0, 0, (unsigned long long)((threadIdx.x >> 8) % (W / 4)), 0, 0, 0}};
+    Stamps sp = {{0, 0, 0, 0, (unsigned long long)((threadIdx.x >> 8) & 1), 0, 0, 0}};
     const unsigned long long tk0 = stamp_now();
     CellIn<HS> ci;
     {
@@ -534,7 +529,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void fcr_bwd_kernel(BwdArgs a) {
         float unused0, unused1;
         const unsigned long long tw1 = stamp_now();
         if (!LP) {
-            lds_fill<I1::BYTES, W>(lw, a.p.img[2]);
+            lds_fill<I1::BYTES, kBwdWaves>(lw, a.p.img[2]);
         }
         if (FCR_STAMP) {
             const unsigned long long tw2 = stamp_now();
@@ -565,7 +560,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void fcr_bwd_kernel(BwdArgs a) {
         // ---- layer 1 ----
         const unsigned long long tw3 = stamp_now();
         if (!LP) {
-            lds_fill<I1::BYTES, W>(lw, a.p.img[1]);
+            lds_fill<I1::BYTES, kBwdWaves>(lw, a.p.img[1]);
         }
         if (FCR_STAMP) sp.t[7] += stamp_now() - tw3;
 #pragma unroll
@@ -583,7 +578,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void fcr_bwd_kernel(BwdArgs a) {
         buf_store_quads<HS>(nb.rd, (uint32_t)((doff(j, 1, 0)) * 16), dxo, lane);
         // ---- layer 0: dx -> window-row gradients ----
         if (!LP) {
-            lds_fill<I0::BYTES, W>(lw, a.p.img[0]);
+            lds_fill<I0::BYTES, kBwdWaves>(lw, a.p.img[0]);
         }
 #pragma unroll
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;

@@ -23,10 +23,7 @@ constexpr int kCtrlIn = 3;       // [y_dot, z, ref]
 constexpr int kMS = 13;          // controller hidden slots (units 4m+q), hidden <= 52
 constexpr int kFnpStride = 8;    // floats per (m, q) controller record: W0 W1 W2 b wout 0 0 0
 constexpr int kFwdWaves = 8;     // waves per forward workgroup (2 per SIMD)
-constexpr int kFwdWavesLP = 12;  // f16-mode forward with stored states (168 VGPRs): 3 per SIMD
-constexpr int kWavePad = 24;     // workspace wave padding: a multiple of every launch geometry
 constexpr int kBwdWaves = 8;     // waves per backward workgroup (2 per SIMD)
-constexpr int kBwdWavesLP = 12;  // f16-mode backward: 3 per SIMD
 constexpr float kP1Max = 2.122366f;  // Functions.py:1411 (32e6 / p1 max_abs_)
 constexpr float kP2Max = 1.036233f;  // Functions.py:1411 (32e6 / p2 max_abs_)
 
@@ -156,11 +153,14 @@ __device__ __forceinline__ f32x4 buf_ldq(__amdgpu_buffer_rsrc_t r, uint32_t voff
     if (n == 4) {
         q = buf_ld4(r, voff, soff);
     } else if (n == 3) {
+        // the whole vector is cast: this compiler's __builtin_bit_cast of an ext_vector ELEMENT (v[1]) reads
+        // element 0 (round 4: the f16 mode's 7-word h records came back as (w4, w4, w4) — DESIGN.md §2)
         typedef unsigned int u32x3 __attribute__((ext_vector_type(3)));
-        const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(r, (int)voff, (int)soff, 0);
-        q[0] = __builtin_bit_cast(float, v[0]);
-        q[1] = __builtin_bit_cast(float, v[1]);
-        q[2] = __builtin_bit_cast(float, v[2]);
+        typedef float f32x3 __attribute__((ext_vector_type(3)));
+        const f32x3 v = __builtin_bit_cast(f32x3, __builtin_amdgcn_raw_buffer_load_b96(r, (int)voff, (int)soff, 0));
+        q[0] = v[0];
+        q[1] = v[1];
+        q[2] = v[2];
     } else if (n == 2) {
         const f32x2 v = buf_ld2(r, voff, soff);
         q[0] = v[0];
