@@ -4,7 +4,7 @@
 # counter group its own run, MI355X_MICROARCH.md). Summaries: profiles/TAG[_CFG]_{kernel_stats.csv,timed_kernels.json,
 # pmc.json} (copied here from gpurun_out/ after the call).
 #   usage: scripts/profile.sh TAG [CONFIG] [gputest]
-#   CONFIG: c2 (default: B 65 536, N 10, H 50, fp32) | c3 (B 262 144, f16) | c3fwd (B 262 144, f16fwd) |
+#   CONFIG: c2 (default: B 65 536, N 10, H 50, fp32) | c3 (B 262 144, f16) |
 #           c3fp32 (B 262 144, fp32) | c5 (H 256, N 25, library keep budget) | c5max (c5, every window kept)
 set -e -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -13,7 +13,6 @@ CFG=${2:-c2}
 case $CFG in
   c2) ARGS=""; SUF="" ;;
   c3) ARGS="--batch 262144 --precision f16"; SUF="_c3f16" ;;
-  c3fwd) ARGS="--batch 262144 --precision f16fwd"; SUF="_c3f16fwd" ;;
   c3fp32) ARGS="--batch 262144"; SUF="_c3fp32" ;;
   c5) ARGS="--hidden 256 --horizon 25"; SUF="_c5" ;;
   c5max) ARGS="--hidden 256 --horizon 25 --wide-keep-budget max"; SUF="_c5" ;;
