@@ -79,7 +79,54 @@ __device__ __forceinline__ void load_xhd(CellIn<HS> &ci, const NextIn &n, int la
         ld_rec<HS, RW>(ci.x, n.rh, n.x, lane);
     }
     if (NX_HC) ld_rec<HS, RW>(ci.h, n.rh, n.h, lane);
-    if (NX_DIN) ld_quads<HS>(ci.d, n.rd, n.d, lane);
+    if (NX_DIN) ld_rec<HS, din_words<HS, LP>()>(ci.d, n.rd, n.d, lane);
+}
+
+// The f16 mode's d record (din_words): v 2^(14-e) as f16 halves, e = the exponent of the trajectory's largest |v| (over
+// its four lanes: every scaled value is below 2^14), and e itself (an integer, exact in f16) in half HS. Relative to
+// the trajectory's largest din the halves keep 2^-12 — the precision of the f16 dgates the products consume.
+template <int HS>
+__device__ __forceinline__ void din_store_lp(__amdgpu_buffer_rsrc_t r, uint32_t off, const float (&v)[HS], int lane) {
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    constexpr int DW = din_words<HS, true>();
+    float m = 0.0f;
+#pragma unroll
+    for (int s = 0; s < HS; ++s) m = fmaxf(m, fabsf(v[s]));
+    m = max_q(m);
+    const int e = max(__builtin_amdgcn_frexp_expf(m), -100);   // m < 2^e; all-zero -> e = 0
+    const float sc = __builtin_amdgcn_ldexpf(1.0f, 14 - e);
+    float w[HS];
+#pragma unroll
+    for (int d = 0; d < DW; ++d) {
+        f16x2 p;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = 2 * d + u;
+            p[u] = i < HS ? (_Float16)__builtin_fmaf(v[i < HS ? i : 0], sc, 0.0f) : i == HS ? (_Float16)(float)e : (_Float16)0.0f;
+        }
+        w[d] = __builtin_bit_cast(float, p);
+    }
+    buf_store_rec<DW>(r, off, w, lane);
+}
+template <int HS, bool LP>
+__device__ __forceinline__ void din_store(__amdgpu_buffer_rsrc_t r, uint32_t off, const float (&v)[HS], int lane) {
+    if constexpr (LP) din_store_lp<HS>(r, off, v, lane);
+    else buf_store_quads<HS>(r, off, v, lane);
+}
+// din of slot r from the f16 mode's d record, given 2^(e-14) (dsc)
+template <int HS>
+__device__ __forceinline__ float din_lp(const f32x4 *d, int r, float dsc) {
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    const int w = r >> 1;
+    const float wv = d[w >> 2][w & 3];   // (a plain element read: bit_cast of a vector element misreads, fcr_common.h)
+    return (float)__builtin_bit_cast(f16x2, wv)[r & 1] * dsc;
+}
+template <int HS>
+__device__ __forceinline__ float din_scale_lp(const f32x4 *d) {
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    constexpr int w = HS >> 1;
+    const float wv = d[w >> 2][w & 3];
+    return __builtin_amdgcn_ldexpf(1.0f, (int)(float)__builtin_bit_cast(f16x2, wv)[HS & 1] - 14);
 }
 
 // inverse exp2 pre-scales of the packed gate rows (fcr_img.h), folded into the dgate scaling
@@ -248,9 +295,10 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     // which only need this cell's (prefetched) inputs, so the previous cell's tail overlaps them ----
     {
         float m = 0.0f;
+        const float dsc = (DIN && LP) ? din_scale_lp<HS>(ci.d) : 0.0f;
 #pragma unroll
         for (int r = 0; r < HS; ++r) {
-            const float din = DIN ? ci.d[r >> 2][r & 3] : ext[r];
+            const float din = DIN ? (LP ? din_lp<HS>(ci.d, r, dsc) : ci.d[r >> 2][r & 3]) : ext[r];
             dh[r] = dh[r] + din;
             m = fmaxf(m, fabsf(dh[r]) + fabsf(dc[r]));
         }
@@ -543,20 +591,20 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         // t = 9: h_9 of layer 2 only fed the readout (no split record), so this cell re-evaluates tanh(c_9)
         bwd_cell<HS, false, false, false, false, true, false, LP, false>(L1.fb, L1.tb, lane, dh_out, dh, dc, dxo, unused0,
                                                                     unused1, ci, next_of(j, 2, kL - 1), sp);
-        buf_store_quads<HS>(nb.rd, (uint32_t)((doff(j, 2, kL - 1)) * 16), dxo, lane);
+        din_store<HS, LP>(nb.rd, (uint32_t)((doff(j, 2, kL - 1)) * 16), dxo, lane);
 #pragma unroll
         for (int r = 0; r < HS; ++r) dab[r] = 0.0f;
         for (int t = kL - 2; t >= 2; --t) {
             bwd_cell<HS, false, false, false, false, true, false, LP>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
                                                                 unused1, ci, next_of(j, 2, t), sp);
-            buf_store_quads<HS>(nb.rd, (uint32_t)((doff(j, 2, t)) * 16), dxo, lane);
+            din_store<HS, LP>(nb.rd, (uint32_t)((doff(j, 2, t)) * 16), dxo, lane);
         }
         bwd_cell<HS, false, false, false, false, false, false, LP>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
                                                              unused1, ci, next_of(j, 2, 1), sp);
-        buf_store_quads<HS>(nb.rd, (uint32_t)((doff(j, 2, 1)) * 16), dxo, lane);
+        din_store<HS, LP>(nb.rd, (uint32_t)((doff(j, 2, 1)) * 16), dxo, lane);
         bwd_cell<HS, false, false, true, false, true, true, LP>(L1.fb, L1.tb, lane, dab, dh, dc, dxo, unused0,
                                                           unused1, ci, next_of(j, 2, 0), sp);
-        buf_store_quads<HS>(nb.rd, (uint32_t)((doff(j, 2, 0)) * 16), dxo, lane);
+        din_store<HS, LP>(nb.rd, (uint32_t)((doff(j, 2, 0)) * 16), dxo, lane);
         // ---- layer 1 ----
         const unsigned long long tw3 = stamp_now();
         if (!LP) {
@@ -568,14 +616,14 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
         for (int t = kL - 1; t >= 2; --t) {
             bwd_cell<HS, false, true, false, false, true, true, LP>(L1b.fb, L1b.tb, lane, dab, dh, dc, dxo, unused0,
                                                               unused1, ci, next_of(j, 1, t), sp);
-            buf_store_quads<HS>(nb.rd, (uint32_t)((doff(j, 1, t)) * 16), dxo, lane);
+            din_store<HS, LP>(nb.rd, (uint32_t)((doff(j, 1, t)) * 16), dxo, lane);
         }
         bwd_cell<HS, false, true, false, false, false, true, LP>(L1b.fb, L1b.tb, lane, dab, dh, dc, dxo, unused0,
                                                            unused1, ci, next_of(j, 1, 1), sp);
-        buf_store_quads<HS>(nb.rd, (uint32_t)((doff(j, 1, 1)) * 16), dxo, lane);
+        din_store<HS, LP>(nb.rd, (uint32_t)((doff(j, 1, 1)) * 16), dxo, lane);
         bwd_cell<HS, false, true, true, true, true, true, LP>(L1b.fb, L1b.tb, lane, dab, dh, dc, dxo, unused0,
                                                         unused1, ci, next_of(j, 1, 0), sp);
-        buf_store_quads<HS>(nb.rd, (uint32_t)((doff(j, 1, 0)) * 16), dxo, lane);
+        din_store<HS, LP>(nb.rd, (uint32_t)((doff(j, 1, 0)) * 16), dxo, lane);
         // ---- layer 0: dx -> window-row gradients ----
         if (!LP) {
             lds_fill<I0::BYTES, kBwdWaves>(lw, a.p.img[0]);

@@ -275,6 +275,11 @@ __device__ __forceinline__ void buf_store_quads(__amdgpu_buffer_rsrc_t r, uint32
 // (LP) only the hi halves, ceil(HS / 2) words — its consumers never read a lo half (fcr_f16.h split_rec).
 template <int HS, bool LP>
 constexpr int rec_words() { return LP ? (HS + 1) / 2 : HS; }
+// Words of a d record (din: the input gradient a layer hands to the one below at the same t): fp32 per slot; the f16
+// mode's holds f16 halves scaled by a per-trajectory power of two whose exponent rides in half HS (fcr_bwd.h
+// din_store_lp / the DIN read in bwd_cell) — half the bytes of the backward's largest slab stream.
+template <int HS, bool LP>
+constexpr int din_words() { return LP ? HS / 2 + 1 : HS; }
 // The first RW words of a record array, stored in the compact layout of an RW-word record (a reader loads them
 // with ld_rec<RW>): the cell's space is the HS-word layout's, so offsets are unchanged and only the bytes shrink.
 template <int RW, int HS, int k = 0>
