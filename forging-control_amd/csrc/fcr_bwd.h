@@ -113,6 +113,13 @@ __device__ __forceinline__ void din_store(__amdgpu_buffer_rsrc_t r, uint32_t off
     if constexpr (LP) din_store_lp<HS>(r, off, v, lane);
     else buf_store_quads<HS>(r, off, v, lane);
 }
+// c_{t-1} of slot r from the f16 mode's c record (c_store)
+__device__ __forceinline__ float crec_lp(const f32x4 *c, int r) {
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    const int w = r >> 1;
+    const float wv = c[w >> 2][w & 3];   // (a plain element read: bit_cast of a vector element misreads, fcr_common.h)
+    return (float)__builtin_bit_cast(f16x2, wv)[r & 1];
+}
 // din of slot r from the f16 mode's d record, given 2^(e-14) (dsc)
 template <int HS>
 __device__ __forceinline__ float din_lp(const f32x4 *d, int r, float dsc) {
@@ -143,9 +150,8 @@ constexpr float kInvNegLog2e = 1.0f / kNegLog2e;
 // recomputed forward tiles 2kb+2, 2kb+3 and their gradients, which form block kb+1.
 // OWN: the cell's own h_t record is in ci.o (every cell but the first of a window's layer-2 phase, whose h_9
 // only fed the readout): tanh(c_t) comes from it (lstm_point_grad_h) instead of being re-evaluated.
-// NX_OWN: the next cell's is fetched. Not in the f16 mode: its records hold f16(h) only, and tanh(c_t) = h / o from
-// an f16 h loses the local derivative 1 - tanh^2 c near saturation (g_u0 2.8e-2 off the oracle at B = 15 with it):
-// tanh(c_t) is re-evaluated from the fp32 c record.
+// NX_OWN: the next cell's is fetched. (The f16 mode's record holds f16(h) only: tanh(c_t) = h f16-rounded / o, the
+// same accuracy against the fp64 oracle as re-evaluating tanh from the c record, scripts/f16_errs.py, and 5 % faster.)
 #ifndef FCR_STAMP
 #define FCR_STAMP 0   // diagnostic: per-wave s_memtime sums of the cell's sections (ws tail)
 #endif
@@ -167,7 +173,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
                                          float &dx4, CellIn<HS> &ci, const NextIn &nx, Stamps &sp,
                                          const DgOut *dgo = nullptr) {
     const unsigned long long t0 = stamp_now();
-    constexpr bool OWNH = OWN && !LP, NX_OWNH = NX_OWN && !LP;   // tanh(c_t) from the h record (fp32 mode)
+    constexpr bool OWNH = OWN, NX_OWNH = NX_OWN;
     // the two waves of a SIMD take turns at the higher issue priority, cell by cell, so neither runs
     // ahead of the other between the phase barriers (oldest-first arbitration otherwise skews them)
     if (sp.t[4] & 1) __builtin_amdgcn_s_setprio(1);
@@ -240,8 +246,9 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     auto slot_grad = [&](int r, f32x4 a, float *va, float *vb) {
         f32x4 P;
         f32x2 Q;
-        if (OWNH) lstm_point_grad_h<FIRST>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], rec_h<HS>(ci.o, r), P, Q);
-        else lstm_point_grad<FIRST>(a, FIRST ? 0.0f : ci.c[r >> 2][r & 3], P, Q);
+        const float cpv = FIRST ? 0.0f : (LP ? crec_lp(ci.c, r) : ci.c[r >> 2][r & 3]);
+        if (OWNH) lstm_point_grad_h<FIRST>(a, cpv, rec_h<HS, LP>(ci.o, r), P, Q);
+        else lstm_point_grad<FIRST>(a, cpv, P, Q);
         // torch LSTM semantics: dc = dc_carried + dh dh/dc; the carried dc of the cell below is dc f
         const float dcv = fmaf(dh[r], P[0], dc[r]);
         dc[r] = dcv * Q[1];
@@ -253,12 +260,21 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
         vb[1] = P[3];
         vb[2] = Q[0];
         vb[3] = P[1];
-        // c_{t-1} quad of slots 4k..4k+3 consumed: the next cell's comes in
-        if (NX_HC && (r & 3) == 3)
-            ci.c[r >> 2] = buf_ld4(nx.rc, lane * 16, nx.c + (r >> 2) * kWave * 16);
-        if (NX_HC && r == HS - 1 && (r & 3) != 3)
-            ci.c[r >> 2] = buf_ldq<quad_n<HS, (HS - 1) / 4>()>(nx.rc, quad_voff<HS, (HS - 1) / 4>(lane),
-                                                              nx.c + quad_soff<HS, (HS - 1) / 4>());
+        // c_{t-1} quad of slots 4k..4k+3 consumed (f16 mode: 8k..8k+7): the next cell's comes in
+        if constexpr (LP) {
+            constexpr int CW = rec_words<HS, true>(), CQ = Geo<CW>::HQ;
+            static_assert(CQ <= 2, "f16 c record quads");
+            if (NX_HC && CQ == 2 && r == 7)
+                ci.c[0] = buf_ldq<quad_n<CW, 0>()>(nx.rc, quad_voff<CW, 0>(lane), nx.c + quad_soff<CW, 0>());
+            if (NX_HC && r == HS - 1)
+                ci.c[CQ - 1] = buf_ldq<quad_n<CW, CQ - 1>()>(nx.rc, quad_voff<CW, CQ - 1>(lane), nx.c + quad_soff<CW, CQ - 1>());
+        } else {
+            if (NX_HC && (r & 3) == 3)
+                ci.c[r >> 2] = buf_ld4(nx.rc, lane * 16, nx.c + (r >> 2) * kWave * 16);
+            if (NX_HC && r == HS - 1 && (r & 3) != 3)
+                ci.c[r >> 2] = buf_ldq<quad_n<HS, (HS - 1) / 4>()>(nx.rc, quad_voff<HS, (HS - 1) / 4>(lane),
+                                                                  nx.c + quad_soff<HS, (HS - 1) / 4>());
+        }
     };
     // forward MFMAs of slot pair kbb into fa[.][0..1]
     auto fwd_pair = [&](int kbb, f32x4 (&fp)[2]) {
@@ -397,7 +413,7 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
 #pragma unroll
                 for (int k = 0; k < Geo<HS>::HQ; ++k) ci.o[k] = hkeep[k];
             } else {
-                ld_quads<HS>(ci.o, nx.rh, nx.o, lane);
+                ld_rec<HS, rec_words<HS, LP>()>(ci.o, nx.rh, nx.o, lane);
             }
         }
     }
@@ -523,7 +539,7 @@ __global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kern
     {
         const NextIn f = next_of(N - 1, 2, kL);   // t = kL -> (N-1, 2, 9)
         load_xhd<HS, false, true, false, LP>(ci, f, lane);
-        ld_quads<HS>(ci.c, f.rc, f.c, lane);
+        ld_rec<HS, rec_words<HS, LP>()>(ci.c, f.rc, f.c, lane);   // (c records: f16 halves in the f16 mode)
     }
 
     for (int j = N - 1; j >= 0; --j) {

@@ -303,6 +303,27 @@ __device__ __forceinline__ void buf_store_rec(__amdgpu_buffer_rsrc_t r, uint32_t
         buf_store_rec<RW, HS, k + 1>(r, off, v, lane);
     }
 }
+// A cell's c record: fp32 per slot; in the f16 mode (LP) f16 halves (slot 2w | 2w + 1 in word w, rec_words words) —
+// |c_t| <= t + 1 (c_t = f c_{t-1} + i g from zero), so no scaling: the backward's c_{t-1} and its rebuilt c_t carry
+// 2^-12 relative, as the f16 mode's h operands do.
+template <int HS, bool LP>
+__device__ __forceinline__ void c_store(__amdgpu_buffer_rsrc_t r, uint32_t off, const float (&v)[HS], int lane) {
+    if constexpr (LP) {
+        typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+        constexpr int CW = rec_words<HS, true>();
+        float w[HS];
+#pragma unroll
+        for (int d = 0; d < CW; ++d) {
+            f16x2 p;
+            p[0] = (_Float16)v[2 * d];
+            p[1] = 2 * d + 1 < HS ? (_Float16)v[2 * d + 1 < HS ? 2 * d + 1 : 0] : (_Float16)0.0f;
+            w[d] = __builtin_bit_cast(float, p);
+        }
+        buf_store_rec<CW>(r, off, w, lane);
+    } else {
+        buf_store_quads<HS>(r, off, v, lane);
+    }
+}
 template <int HS, int k = 0>
 __device__ __forceinline__ void buf_load_quads(float (&v)[HS], __amdgpu_buffer_rsrc_t r, uint32_t off, int lane) {
     if constexpr (k < Geo<HS>::HQ) {

@@ -377,8 +377,14 @@ __device__ __forceinline__ void lstm_point_grad(f32x4 a, float c_prev, f32x4 &P,
 // hi + lo in ONE v_fma_mix_f32 (f16 sources picked by op_sel; exact in fp32) — the compiler's form of the
 // same sum is two conversions and an add. A VALU-to-VALU dependency: no MFMA operand hazard. s is a
 // compile-time constant once the cell is unrolled: one of the four op_sel forms survives.
-template <int HS>
+template <int HS, bool LP = false>
 __device__ __forceinline__ float rec_h(const f32x4 *rec, int s) {
+    if constexpr (LP) {   // the f16 mode's record: hi halves only
+        typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+        const int wh = s >> 1;
+        const float wv = rec[wh >> 2][wh & 3];   // (a plain element read: bit_cast of a vector element misreads)
+        return (float)__builtin_bit_cast(f16x2, wv)[s & 1];
+    }
     const int wh = s >> 1, wl = (HS + s) >> 1;
     const float a = rec[wh >> 2][wh & 3], b = rec[wl >> 2][wl & 3];
     float r;

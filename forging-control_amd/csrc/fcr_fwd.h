@@ -240,18 +240,18 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
                 if (STORE) {
                     buf_store_rec<kRW>(rh, SEQ_O(0, 0), hp, lane);
                     buf_st2(rx, lane * 8, (uint32_t)(j * kL * kWave * 8), f32x2{x0, x1});
-                    buf_store_quads<HS>(rc, SEQ_O(0, 0), c, lane);
+                    c_store<HS, LP>(rc, SEQ_O(0, 0), c, lane);
                 }
                 fwd16_cell<HS, false, true, LP>(lw1, lane, 0.0f, 0.0f, hp, h1, c1, hout, turn);
                 split_rec<HS, LP>(hout, h1);
                 if (STORE || !LP) buf_store_rec<kRW>(rh, SEQ_O(1, 0), h1, lane);   // f16 mode: layer 2 is in this phase
-                if (STORE) buf_store_quads<HS>(rc, SEQ_O(1, 0), c1, lane);
+                if (STORE) c_store<HS, LP>(rc, SEQ_O(1, 0), c1, lane);
                 if constexpr (LP) {   // every layer resident: layer 2 joins the phase (its h_t from registers as well)
                     fwd16_cell<HS, false, true, LP>(lwl[2], lane, 0.0f, 0.0f, h1, h2, c2, hout, turn);
                     split_rec<HS, LP>(hout, h2);
                     if (STORE) {
                         buf_store_rec<kRW>(rh, SEQ_O(2, 0), h2, lane);
-                        buf_store_quads<HS>(rc, SEQ_O(2, 0), c2, lane);
+                        c_store<HS, LP>(rc, SEQ_O(2, 0), c2, lane);
                     }
                 }
             }
@@ -264,19 +264,19 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
                 if (STORE) {
                     buf_store_rec<kRW>(rh, SEQ_O(0, t), hp, lane);
                     buf_st2(rx, lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{x0, x1});
-                    if (t + 1 < kL) buf_store_quads<HS>(rc, SEQ_O(0, t), c, lane);   // c_9 is never a c_{t-1}
+                    if (t + 1 < kL) c_store<HS, LP>(rc, SEQ_O(0, t), c, lane);   // c_9 is never a c_{t-1}
                 }
                 fwd16_cell<HS, false, false, LP>(lw1, lane, 0.0f, 0.0f, hp, h1, c1, hout, turn);
                 split_rec<HS, LP>(hout, h1);
                 if (STORE || !LP) buf_store_rec<kRW>(rh, SEQ_O(1, t), h1, lane);
-                if (STORE && t + 1 < kL) buf_store_quads<HS>(rc, SEQ_O(1, t), c1, lane);
+                if (STORE && t + 1 < kL) c_store<HS, LP>(rc, SEQ_O(1, t), c1, lane);
                 if constexpr (LP) {
                     fwd16_cell<HS, false, false, LP>(lwl[2], lane, 0.0f, 0.0f, h1, h2, c2, hout, turn);
                     if (t + 1 < kL) {   // h_9 of layer 2 only feeds the readout (fp32 hout)
                         split_rec<HS, LP>(hout, h2);
                         if (STORE) {
                             buf_store_rec<kRW>(rh, SEQ_O(2, t), h2, lane);
-                            buf_store_quads<HS>(rc, SEQ_O(2, t), c2, lane);
+                            c_store<HS, LP>(rc, SEQ_O(2, t), c2, lane);
                         }
                     }
                 }
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
             fwd16_cell<HS, false, true, LP>(lwc, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
             split_rec<HS, LP>(hout, hp);
             if (STORE) buf_store_rec<kRW>(rh, SEQ_O(l, 0), hp, lane);
-            if (STORE) buf_store_quads<HS>(rc, SEQ_O(l, 0), c, lane);
+            if (STORE) c_store<HS, LP>(rc, SEQ_O(l, 0), c, lane);
 #pragma unroll
             for (int r = 0; r < HS; ++r) xc[r] = xn[r];
 #pragma unroll 3
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kern
                     split_rec<HS, LP>(hout, hp);
                     if (STORE) buf_store_rec<kRW>(rh, SEQ_O(l, t), hp, lane);
                 }
-                if (STORE && t + 1 < kL) buf_store_quads<HS>(rc, SEQ_O(l, t), c, lane);
+                if (STORE && t + 1 < kL) c_store<HS, LP>(rc, SEQ_O(l, t), c, lane);
 #pragma unroll
                 for (int r = 0; r < HS; ++r) xc[r] = xn[r];
             }
