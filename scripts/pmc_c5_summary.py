@@ -9,7 +9,9 @@ import shutil
 import sys
 
 tag, root = sys.argv[1], sys.argv[2]
-KERNELS = ("wide_gemm_cell_kernel", "wide_bwd_gemm_kernel", "wide_cell_bwd_kernel")
+KERNELS = ("wide_gemm_cell_kernel", "wide_bwd_fused_kernel", "wide_head_kernel", "wide_cell_bwd_kernel")
+INST = ("SQ_INSTS_VALU_MFMA_F16", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_INST_ANY",
+        "SQ_LDS_BANK_CONFLICT", "GRBM_GUI_ACTIVE")
 
 
 def dispatches(kind, counter):
@@ -43,6 +45,11 @@ for kind, cnt in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         if on and "ctrl_grad_kernel" in n:
             on, last = False, tot
     passes[cnt] = last
+for cnt in INST:   # instruction / wait counters of the same kernels (one pass; per launch, summed over the device)
+    for name in KERNELS:
+        vals = [v for n, v in dispatches("inst", cnt) if name in n]
+        if vals:
+            out.setdefault(name, {})[cnt + "_per_launch"] = sum(vals) / len(vals)
 for name, d in out.items():
     if "FETCH_SIZE_KB_per_launch" in d and "WRITE_SIZE_KB_per_launch" in d:
         d["hbm_bytes_corrected"] = (2 * d["FETCH_SIZE_KB_per_launch"] + d["WRITE_SIZE_KB_per_launch"]) * 1024
@@ -50,7 +57,8 @@ if passes.get("FETCH_SIZE") is not None and passes.get("WRITE_SIZE") is not None
     out["bwd_pass"] = {"FETCH_SIZE_KB": passes["FETCH_SIZE"], "WRITE_SIZE_KB": passes["WRITE_SIZE"],
                        "hbm_bytes_corrected": (2 * passes["FETCH_SIZE"] + passes["WRITE_SIZE"]) * 1024}
 out["_note"] = ("rocprofv3 PMC passes of bench.py --hidden 256 --horizon 25 --batch 65536 (config 5), KB; "
-                "hbm_bytes_corrected = 2*FETCH + WRITE (gfx950). bwd_pass = every dispatch of the last profiled "
+                "hbm_bytes_corrected = 2*FETCH + WRITE (gfx950); SQ_* / GRBM_* per launch from one more pass (SQ_WAVE_CYCLES and "
+                "SQ_WAIT_INST_ANY in quad-cycles, MI355X_MICROARCH.md). bwd_pass = every dispatch of the last profiled "
                 "backward pass, wide_bscale_kernel .. ctrl_grad_kernel.")
 stats = glob.glob(f"{root}/trace/**/*kernel_stats.csv", recursive=True)
 if stats:
