@@ -629,7 +629,7 @@ int launch_fb(const WbArgs &wa, bool l0, hipStream_t s) {
         attr_set[l0] = true;
     }
     if (wa.NO < 0 || wa.NO > 2 * kWbM || wa.NO % 4 || wa.H % 8 || wa.H > kWbMaxH || wa.NB <= 0 || wa.ldo % 4 ||
-        wa.ldh % 2 || wa.ldx % 2 || (l0 && (!wa.wih0 || !wa.rowg)))
+        wa.ldh % 4 || wa.ldx % 4 || (l0 && (!wa.wih0 || !wa.rowg)))
         return fail(FCR_EINVAL, "wide_bwd_fused_kernel: NO %d H %d B %d ldo %d off its tiling", wa.NO, wa.H, wa.NB, wa.ldo);
     const int nx = (wa.NB + kWbN - 1) / kWbN, ny = wa.NO > 0 ? (wa.NO + kWbM - 1) / kWbM : 1;
     if (l0) hipLaunchKernelGGL((wide_bwd_fused_kernel<true>), dim3((unsigned)(nx * ny)), dim3(kWbThreads), kWbLds, s, wa);

@@ -9,19 +9,24 @@
 // A = W^T split [NP][4H] (row n = output column, W_ih column n for n < H, W_hh column n - H; layer 0: W_hh only) with
 // the K index UNIT-major, r' = 4 unit + gate (wide_split_bt_kernel), so a K step of 32 is 8 whole units: the dgates
 // of one K step need only those units' inputs.
-// Tile: a workgroup owns 256 output columns x 128 trajectories; 8 waves (4 along M x 2 along N), each 64 x 64 = 4 x 4
-// D tiles (lane = trajectory, 4 consecutive columns: one 16-B store). K in steps of 32: A through a 2-stage LDS-DMA
-// ring (W^T is L2-resident); the B tile (the step's dgates, hi | lo) is computed by the workgroup itself, one step
-// ahead of the MFMAs that read it: thread (row r = tid / 4, pair p = tid % 4) loads units 8s + 2p, 8s + 2p + 1 of
-// its trajectory (pre-activations, c_{t-1}, dh, din, dc: 8-B loads, one step ahead in registers), forms
-// the 8 dgates and dc_{t-1} (fcr_wide.h wide_cell_bwd_kernel's algebra, exp2-based activations as fcr_bwd.h), splits
-// them into the 16-B chunk its MFMA lane reads. With two column blocks (NO > 256) both form the same dgates; the
-// first writes dc_{t-1}.
+// Tile: a workgroup owns 256 output columns x 128 trajectories, and its 8 waves split by ROLE (round 4): waves 0-3
+// produce the B tiles (the step's dgates, hi | lo), waves 4-7 consume them (each 64 columns x all 128 trajectories =
+// 4 x 8 D tiles; lane = trajectory, 4 consecutive columns: one 16-B store). Wave w runs on SIMD w % 4, so every SIMD
+// holds one producer and one consumer: the producer's transcendental chains issue while its partner's MFMAs run
+// (with every wave doing both in turn, the step barrier lined the two waves of a SIMD up on the same phase, and the
+// dgate chains were the critical path: 247 ms of backward against 168 ms with the activations stubbed out). K in
+// steps of 32: A through a 2-stage LDS-DMA ring issued by the consumers (W^T is L2-resident); the B tile of step
+// ks + 1 is formed while the consumers multiply step ks. Producer thread (row r = tid / 2, half p = tid % 2) loads
+// units 8s + 4p .. + 3 of its trajectory (pre-activations, c_{t-1}, dh, din, dc: 16-B loads, one step ahead), forms
+// their 16 dgates and dc_{t-1} (fcr_wide.h wide_cell_bwd_kernel's algebra), splits them into the two 16-B chunks of
+// its row half. With two column blocks (NO > 256) both form the same dgates; the first writes dc_{t-1}.
 // Row scale: 2^(13 - e), e the exponent of a bound on the row's |dgates|: |dgate| <= |dc_t| <= |dc| + |dh_rec| +
 // |din| (forget row: x (kL - 1) / 4, fcr_wide.h kWideDgExp). The three maxima come from the kernels that wrote those
 // values (this kernel's epilogue and elementwise part of the previous cell, the head kernel), per row, so no pass
 // over the row precedes the K loop.
 #pragma once
+#include <type_traits>
+
 #include "fcr_common.h"
 #include "fcr_f16.h"
 #include "fcr_wide.h"
@@ -31,21 +36,22 @@ namespace fcr {
 constexpr int kWbM = 256;                 // output columns per workgroup
 constexpr int kWbN = 128;                 // trajectories per workgroup
 constexpr int kWbK = 32;                  // k per step (8 units x 4 gates)
-constexpr int kWbWM = 4, kWbWN = 2;       // waves along the output columns x along the trajectories
-constexpr int kWbWaves = kWbWM * kWbWN;
-constexpr int kWbTM = kWbM / kWbWM / 16, kWbTN = kWbN / kWbWN / 16;   // D tiles per wave
+constexpr int kWbProd = 4, kWbCons = 4;   // producer (dgate) waves, consumer (MFMA) waves
+constexpr int kWbWaves = kWbProd + kWbCons;
+constexpr int kWbTM = kWbM / kWbCons / 16, kWbTN = kWbN / 16;   // D tiles per consumer wave: 4 x 8
 constexpr int kWbThreads = 64 * kWbWaves;
+constexpr int kWbUnits = 4;               // units per producer thread and K step (two threads per trajectory row)
 constexpr int kWbStageA = kWbM * kWbK * 2;                // bytes of one split half of A
 constexpr int kWbStage = 2 * kWbStageA;                   // hi A | lo A
 constexpr int kWbTileB = kWbN * kWbK * 2;                 // one split half of the dgate tile
-constexpr int kWbPieces = kWbStage / 1024 / kWbWaves;     // LDS-DMA pieces per wave per stage
+constexpr int kWbPieces = kWbStage / 1024 / kWbCons;      // LDS-DMA pieces per consumer wave per stage
 constexpr int kWbOffB = 2 * kWbStage;                     // [A stage 0 | A stage 1 | B tile 0 hi, lo | B tile 1 ...]
 constexpr int kWbOffDown = kWbOffB + 4 * kWbTileB;
 constexpr int kWbOffW0 = kWbOffDown + kWbN * 4;           // layer 0: W_ih0 as [unit][gate][kIn]
 constexpr int kWbMaxH = 256;                              // NO = 2H <= 2 column blocks (the row bounds' slots)
 constexpr int kWbLds = kWbOffW0 + 4 * kWbMaxH * kIn * 4;
-static_assert(kWbStage % (1024 * kWbWaves) == 0, "DMA pieces");
-static_assert(kWbThreads == 4 * kWbN, "dgate mapping: four threads (two units each) per trajectory row");
+static_assert(kWbStage % (1024 * kWbCons) == 0, "DMA pieces");
+static_assert(64 * kWbProd * kWbUnits == 8 * kWbN, "dgate mapping: a step's 8 units of every row over the producers");
 static_assert(kWbLds <= 163840, "LDS");
 
 struct WbArgs {
@@ -70,9 +76,9 @@ struct WbArgs {
 // on distinct 16-B slots of a 128-B bank line (fcr_wgemm.h wg_off)
 __device__ __forceinline__ uint32_t wb_off(int r, int c) { return (uint32_t)(r * 64 + ((c ^ ((r >> 1) & 3)) << 4)); }
 
-// one step's inputs of a dgate thread: two consecutive units of one trajectory
+// one step's inputs of a producer thread: four consecutive units of one trajectory
 struct WbIn {
-    f32x2 pi, pf, pg, po, cp, dh, dn, dc;
+    f32x4 pi, pf, pg, po, cp, dh, dn, dc;
 };
 
 template <bool L0>
@@ -80,7 +86,8 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a)
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wv % kWbWM, wn = wv / kWbWM;            // column slice, trajectory slice
+    const bool producer = wv < kWbProd;                     // wave-uniform role
+    const int cw = wv - kWbProd;                            // consumer: column slice
     const int H = a.H, K = 4 * H, nk = K / kWbK;
     const bool prod = a.NO > 0;
     const int ny = prod ? (a.NO + kWbM - 1) / kWbM : 1, total = gridDim.x, id = blockIdx.x;
@@ -92,18 +99,17 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a)
     const int m0 = cb * kWbM;                               // first output column
     const int b0 = (wg / ny) * kWbN;                        // first trajectory
 
-    // ---- this thread's dgate row and unit pair; the row's scale from the producers' bounds ----
-    const int er = tid >> 2, ep = tid & 3;
+    // ---- producer thread: its dgate row and unit half; the row's scale from the producers' bounds ----
+    const int er = (tid >> 1) & (kWbN - 1), ep = tid & 1;   // (consumers: unused)
     const int eb = b0 + er < a.NB ? b0 + er : a.NB - 1;    // tail rows recompute the last trajectory (not stored)
     const bool elive = b0 + er < a.NB;
-    float up, down;
-    {
+    float up = 0.0f;
+    if (producer) {
         float m = a.rm_c[eb] + fmaxf(a.rm_h[eb], a.rm_h[a.NB + eb]);
         if (a.rm_d) m += fmaxf(a.rm_d[eb], a.rm_d[a.NB + eb]);
         const int ex = m > 0.0f ? __builtin_amdgcn_frexp_expf(m) : 0;   // every |dgate| < 2^ex (times (kL-1)/4: forget)
         up = __builtin_amdgcn_ldexpf(1.0f, kWideDgExp - ex);
-        down = __builtin_amdgcn_ldexpf(1.0f, ex - kWideDgExp);
-        if (ep == 0) reinterpret_cast<float *>(lds + kWbOffDown)[er] = down;
+        if (ep == 0) reinterpret_cast<float *>(lds + kWbOffDown)[er] = __builtin_amdgcn_ldexpf(1.0f, ex - kWideDgExp);
     }
     float *w0l = reinterpret_cast<float *>(lds + kWbOffW0);
     if constexpr (L0) {   // W_ih0 [4H][kIn] -> LDS [unit][gate][kIn]
@@ -113,12 +119,15 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a)
         }
     }
 
-    // ---- A: LDS-DMA pieces (16 rows x 64 B of [A hi (16 pieces) | A lo (16)]); lane i lands at +16 i ----
+    // ---- consumers: A by LDS-DMA pieces (16 rows x 64 B of [A hi (16 pieces) | A lo (16)]; lane i lands at +16 i).
+    // Issued from inline asm: with the intrinsic anywhere in the kernel the compiler's wait insertion drains every
+    // outstanding load (vmcnt(0)) before the use of a prefetched value, the producers' included. The step barrier's
+    // vmcnt(0) retires each consumer's own pieces. M0 carries the wave's LDS base; nothing else in the kernel uses it.
     const _Float16 *gsrc[kWbPieces];
     uint32_t ldst[kWbPieces];
 #pragma unroll
     for (int q = 0; q < kWbPieces; ++q) {
-        const int j = wv + kWbWaves * q;
+        const int j = (producer ? 0 : cw) + kWbCons * q;
         const bool lo = j >= 16;
         const int r = 16 * (lo ? j - 16 : j) + (lane >> 2);
         const int c = (lane & 3) ^ ((r >> 1) & 3);
@@ -129,43 +138,47 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a)
     }
     auto dma = [&](int ks, int buf) {
 #pragma unroll
-        for (int q = 0; q < kWbPieces; ++q)
-            __builtin_amdgcn_global_load_lds(
-                (const __attribute__((address_space(1))) void *)(gsrc[q] + ks * kWbK),
-                (__attribute__((address_space(3))) void *)((__attribute__((address_space(3))) char *)lds + buf * kWbStage +
-                                                           ldst[q]),
-                16, 0, 0);
+        for (int q = 0; q < kWbPieces; ++q) {
+            const uint32_t la = __builtin_amdgcn_readfirstlane(
+                (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)(lds + buf * kWbStage + ldst[q]));
+            const _Float16 *g = gsrc[q] + ks * kWbK;
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+            asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" :: "s"(la), "v"(g) : "memory", "m0");
+#pragma clang diagnostic pop
+        }
     };
 
-    // ---- the dgate part: inputs one step ahead, the tile one step ahead of the MFMAs ----
+    // ---- producers: inputs one step ahead, the tile one step ahead of the MFMAs ----
     const float *pre = a.pre + (size_t)eb * K;
     const float *cpr = a.c_prev ? a.c_prev + (size_t)eb * H : nullptr;
     const float *dhr = a.dh + (size_t)eb * a.ldh;
     const float *dnr = a.din ? a.din + (size_t)eb * a.ldx : nullptr;
     const float *dcr = a.dC + (size_t)eb * H;
     float *dco_r = a.dC_out + (size_t)eb * H;
+    auto ld4 = [](const float *p) { return *reinterpret_cast<const f32x4 *>(p); };
     auto load_in = [&](int s) {
         WbIn x;
-        const int u = 8 * s + 2 * ep;
-        x.pi = *reinterpret_cast<const f32x2 *>(pre + u);
-        x.pf = *reinterpret_cast<const f32x2 *>(pre + H + u);
-        x.pg = *reinterpret_cast<const f32x2 *>(pre + 2 * H + u);
-        x.po = *reinterpret_cast<const f32x2 *>(pre + 3 * H + u);
-        x.cp = cpr ? *reinterpret_cast<const f32x2 *>(cpr + u) : f32x2{0.0f, 0.0f};
-        x.dh = *reinterpret_cast<const f32x2 *>(dhr + u);
-        x.dn = dnr ? *reinterpret_cast<const f32x2 *>(dnr + u) : f32x2{0.0f, 0.0f};
-        x.dc = *reinterpret_cast<const f32x2 *>(dcr + u);
+        const int u = 8 * s + kWbUnits * ep;
+        x.pi = ld4(pre + u);
+        x.pf = ld4(pre + H + u);
+        x.pg = ld4(pre + 2 * H + u);
+        x.po = ld4(pre + 3 * H + u);
+        x.cp = cpr ? ld4(cpr + u) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        x.dh = ld4(dhr + u);
+        x.dn = dnr ? ld4(dnr + u) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        x.dc = ld4(dcr + u);
         return x;
     };
     const bool wr_dc = cb == 0 && elive;   // both column blocks form the same dc_{t-1}: the first stores it
     float mdc = 0.0f;                      // max |dc_{t-1}| of this thread's units
     float pc[kIn] = {};                    // layer 0: this thread's share of the window-row gradient
     auto dgates = [&](int s, const WbIn &x, int buf) {
-        float dg[8], sc[8];
-        f32x2 dco;
-        const int u = 8 * s + 2 * ep;
+        float dg[4 * kWbUnits];
+        f32x4 dco;
+        const int u = 8 * s + kWbUnits * ep;
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < kWbUnits; ++k) {
             const float i = sigm(x.pi[k]), f = sigm(x.pf[k]), g = tanh_f(x.pg[k]), o = sigm(x.po[k]);
             const float cp = x.cp[k];
             const float tc = tanh_f(fmaf(f, cp, i * g));   // c_t rebuilt as the forward formed it (f c_{t-1} + i g)
@@ -177,126 +190,169 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a)
             dg[4 * k + 3] = dh * tc * (o - o * o);
             dco[k] = dct * f;
         }
-        if (wr_dc) *reinterpret_cast<f32x2 *>(dco_r + u) = dco;
-        mdc = fmaxf(mdc, fmaxf(fabsf(dco[0]), fabsf(dco[1])));
-        if constexpr (L0) {   // sum_r dG[b][r] W_ih0[r][c] over this step's 8 gate rows, fp32
-            const f32x4 *w4 = reinterpret_cast<const f32x4 *>(w0l + u * 4 * kIn);   // 40 floats: units u, u + 1
+        if (wr_dc) *reinterpret_cast<f32x4 *>(dco_r + u) = dco;
 #pragma unroll
-            for (int q = 0; q < 2 * 4 * kIn / 4; ++q) {
+        for (int k = 0; k < kWbUnits; ++k) mdc = fmaxf(mdc, fabsf(dco[k]));
+        if constexpr (L0) {   // sum_r dG[b][r] W_ih0[r][c] over this thread's 16 gate rows, fp32
+            const f32x4 *w4 = reinterpret_cast<const f32x4 *>(w0l + u * 4 * kIn);   // 80 floats: units u .. u + 3
+#pragma unroll
+            for (int q = 0; q < kWbUnits * 4 * kIn / 4; ++q) {
                 const f32x4 wq = w4[q];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const int idx = 4 * q + e;   // (unit k, gate g, column c) = idx / 20, idx / 5 % 4, idx % 5
+                    const int idx = 4 * q + e;   // (unit k, gate g, column c): idx / 20, idx / 5 % 4, idx % 5
                     pc[idx % kIn] = fmaf(dg[idx / kIn], wq[e], pc[idx % kIn]);
                 }
             }
         }
         if (prod) {
+            // the split (fcr_f16.h mix_pair): hi = f16(up dg), lo = f16(up dg - hi); units 4 ep .. of the row's 8
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            unsigned hw[8], lw[8];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) sc[e] = up;
-            f16x8 h, l;
-            split8p(dg, sc, h, l);
+            for (int p = 0; p < 8; ++p) mix_pair(dg[2 * p], up, dg[2 * p + 1], up, hw[p], lw[p]);
             char *bt = lds + kWbOffB + buf * 2 * kWbTileB;
-            *reinterpret_cast<f16x8 *>(bt + wb_off(er, ep)) = h;
-            *reinterpret_cast<f16x8 *>(bt + kWbTileB + wb_off(er, ep)) = l;
+            const uint32_t o0 = wb_off(er, 2 * ep), o1 = wb_off(er, 2 * ep + 1);
+            *reinterpret_cast<u32x4 *>(bt + o0) = u32x4{hw[0], hw[1], hw[2], hw[3]};
+            *reinterpret_cast<u32x4 *>(bt + o1) = u32x4{hw[4], hw[5], hw[6], hw[7]};
+            *reinterpret_cast<u32x4 *>(bt + kWbTileB + o0) = u32x4{lw[0], lw[1], lw[2], lw[3]};
+            *reinterpret_cast<u32x4 *>(bt + kWbTileB + o1) = u32x4{lw[4], lw[5], lw[6], lw[7]};
         }
     };
 
-    f32x4 acc[kWbTM][kWbTN];
+    // The two roles run separate loops with the same barriers (one per K step, plus the prologue's and the
+    // epilogue's): a shared loop would keep the consumers' 128 accumulator registers live in the producers too.
+    auto barrier = [] { asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+    const float *ldown = reinterpret_cast<const float *>(lds + kWbOffDown);
+    float *red = reinterpret_cast<float *>(lds);   // epilogue: [cw][128 rows][2] (the A stages are retired)
+    if (producer) {
+        // a producer's barrier waits only for its LDS tile writes: its input loads stay in flight across it, and the
+        // compiler's own wait before their first use (exact counts: no DMA intrinsic in the kernel) is all
+        auto pbarrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+        if constexpr (!L0) {
+            // inputs three steps ahead in rotating register sets (unrolled by three: a copy between sets would wait
+            // for the loads)
+            WbIn x0 = load_in(0), x1, x2;
+            if (nk > 1) x1 = load_in(1);
+            if (nk > 2) x2 = load_in(2);
+            barrier();   // W_ih0 and the row scales in LDS
+            dgates(0, x0, 0);
+            auto pstep = [&](auto full, int ks, const WbIn &xuse, WbIn &xload) {
+                constexpr bool FULL = decltype(full)::value;   // ks + 3 < nk: nothing conditional in the step
+                pbarrier();                                    // tile ks published
+                if (FULL || ks + 3 < nk) xload = load_in(ks + 3);
+                if (FULL || ks + 1 < nk) dgates(ks + 1, xuse, (ks & 1) ^ 1);   // (its buffer was read at ks - 1)
+            };
+            using Full = std::integral_constant<bool, true>;
+            using Tail = std::integral_constant<bool, false>;
+            int ks = 0;
+            for (; ks + 5 < nk; ks += 3) {   // step ks + t: dgates from set (t + 1) % 3, loads into set t
+                pstep(Full{}, ks, x1, x0);
+                pstep(Full{}, ks + 1, x2, x1);
+                pstep(Full{}, ks + 2, x0, x2);
+            }
+            if (ks < nk) pstep(Tail{}, ks, x1, x0);   // the last 1..5 steps, the sets rotating on
+            if (ks + 1 < nk) pstep(Tail{}, ks + 1, x2, x1);
+            if (ks + 2 < nk) pstep(Tail{}, ks + 2, x0, x2);
+            if (ks + 3 < nk) pstep(Tail{}, ks + 3, x1, x0);
+            if (ks + 4 < nk) pstep(Tail{}, ks + 4, x2, x1);
+        } else {
+            // layer 0 (the window-row gradient's W_ih0 reads and accumulators) has registers for one set ahead
+            WbIn xc = load_in(0);
+            barrier();
+            dgates(0, xc, 0);
+            if (nk > 1) xc = load_in(1);
+            for (int ks = 0; ks < nk; ++ks) {
+                pbarrier();
+                WbIn xn;
+                if (ks + 2 < nk) xn = load_in(ks + 2);
+                if (ks + 1 < nk) dgates(ks + 1, xc, (ks & 1) ^ 1);
+                if (ks + 2 < nk) xc = xn;
+            }
+        }
+        // per-row results: dc_{t-1} bound, layer 0's window-row gradient
+        mdc = fmaxf(mdc, __shfl_xor(mdc, 1));
+        if (a.rm_c_out && wr_dc && ep == 0) a.rm_c_out[eb] = mdc;
+        if constexpr (L0) {
 #pragma unroll
-    for (int i = 0; i < kWbTM; ++i)
+            for (int c = 0; c < kIn; ++c) pc[c] += __shfl_xor(pc[c], 1);
+            if (a.rowg && elive && cb == 0 && ep == 0)
 #pragma unroll
-        for (int j = 0; j < kWbTN; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    const int fr = lane & 15, fq = lane >> 4;
-
-    if (prod) dma(0, 0);
-    WbIn xc = load_in(0);
-    __syncthreads();   // W_ih0 and the row scales in LDS
-    dgates(0, xc, 0);
-    if (nk > 1) xc = load_in(1);
-    for (int ks = 0; ks < nk; ++ks) {
-        const int buf = ks & 1;
-        // stage ks's A landed (issued a step ago), tile ks's dgates written by every thread: publish both
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (prod && ks + 1 < nk) dma(ks + 1, buf ^ 1);   // into the stage every wave finished reading at ks - 1
-        WbIn xn;
-        if (ks + 2 < nk) xn = load_in(ks + 2);
-        if (prod) {
+                for (int c = 0; c < kIn; ++c) a.rowg[(size_t)eb * kIn + c] += pc[c];
+        }
+        if (!prod) return;
+        barrier();   // (the consumers' epilogue reuses the A stages)
+        barrier();   // the consumers' row maxima are in `red`
+    } else {
+        f32x4 acc[kWbTM][kWbTN];
+#pragma unroll
+        for (int i = 0; i < kWbTM; ++i)
+#pragma unroll
+            for (int j = 0; j < kWbTN; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        const int fr = lane & 15, fq = lane >> 4;
+        if (prod) dma(0, 0);
+        barrier();
+        for (int ks = 0; ks < nk; ++ks) {
+            const int buf = ks & 1;
+            barrier();   // stage ks's A landed (each consumer waits for its own pieces), tile ks written
+            if (!prod) continue;
+            if (ks + 1 < nk) dma(ks + 1, buf ^ 1);   // into the stage every consumer finished reading at ks - 1
             const char *st = lds + buf * kWbStage;
             const char *bt = lds + kWbOffB + buf * 2 * kWbTileB;
-            f16x8 ah[kWbTM], al[kWbTM], bh[kWbTN], bl[kWbTN];
-#pragma unroll
-            for (int j = 0; j < kWbTN; ++j) {
-                const int r = 16 * (kWbTN * wn + j) + fr;
-                bh[j] = *reinterpret_cast<const f16x8 *>(bt + wb_off(r, fq));
-                bl[j] = *reinterpret_cast<const f16x8 *>(bt + kWbTileB + wb_off(r, fq));
-            }
+            f16x8 ah[kWbTM], al[kWbTM];
 #pragma unroll
             for (int i = 0; i < kWbTM; ++i) {
-                const int r = 16 * (kWbTM * wm + i) + fr;
+                const int r = 16 * (kWbTM * cw + i) + fr;
                 ah[i] = *reinterpret_cast<const f16x8 *>(st + wb_off(r, fq));
                 al[i] = *reinterpret_cast<const f16x8 *>(st + kWbStageA + wb_off(r, fq));
             }
 #pragma unroll
-            for (int i = 0; i < kWbTM; ++i)
+            for (int j = 0; j < kWbTN; ++j) {   // B tile by tile; the A fragments stay in registers across them
+                const int r = 16 * j + fr;
+                const f16x8 bh = *reinterpret_cast<const f16x8 *>(bt + wb_off(r, fq));
+                const f16x8 bl = *reinterpret_cast<const f16x8 *>(bt + kWbTileB + wb_off(r, fq));
 #pragma unroll
-                for (int j = 0; j < kWbTN; ++j) acc[i][j] = mma3(ah[i], al[i], bh[j], bl[j], acc[i][j]);
-        }
-        // the next step's dgates beside this step's MFMAs (their tile buffer was read at ks - 1)
-        if (ks + 1 < nk) dgates(ks + 1, xc, buf ^ 1);
-        if (ks + 2 < nk) xc = xn;
-    }
-    // ---- per-row results of the dgate part: dc_{t-1} bound, layer 0's window-row gradient ----
-    mdc = fmaxf(mdc, __shfl_xor(mdc, 1));
-    mdc = fmaxf(mdc, __shfl_xor(mdc, 2));
-    if (a.rm_c_out && wr_dc && ep == 0) a.rm_c_out[eb] = mdc;
-    if constexpr (L0) {
-#pragma unroll
-        for (int c = 0; c < kIn; ++c) {
-            pc[c] += __shfl_xor(pc[c], 1);
-            pc[c] += __shfl_xor(pc[c], 2);
-        }
-        if (a.rowg && elive && cb == 0 && ep == 0)
-#pragma unroll
-            for (int c = 0; c < kIn; ++c) a.rowg[(size_t)eb * kIn + c] += pc[c];
-    }
-    if (!prod) return;
-    // ---- epilogue: lane = trajectory b0 + 16 (TN wn + j) + (lane & 15), columns m0 + 16 (TM wm + i) + 4 (lane >> 4)
-    // .. +3, in true units (x the row's down); and the row maxima of the dh and input-gradient columns ----
-    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    const float *ldown = reinterpret_cast<const float *>(lds + kWbOffDown);
-    float *red = reinterpret_cast<float *>(lds);   // [wm][128 rows][2] (the A stages are retired)
-#pragma unroll
-    for (int j = 0; j < kWbTN; ++j) {
-        const int rl = 16 * (kWbTN * wn + j) + fr, b = b0 + rl;
-        const float f = ldown[rl];
-        float mh = 0.0f, md = 0.0f;
-#pragma unroll
-        for (int i = 0; i < kWbTM; ++i) {
-            const int col = m0 + 16 * (kWbTM * wm + i) + 4 * fq;
-            const f32x4 v = acc[i][j] * f;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float av = fabsf(v[e]);
-                if (col + e >= a.h0 && col + e < a.h1) mh = fmaxf(mh, av);
-                if (col + e < a.d1) md = fmaxf(md, av);
+                for (int i = 0; i < kWbTM; ++i) acc[i][j] = mma3(ah[i], al[i], bh, bl, acc[i][j]);
             }
-            if (b < a.NB && col < a.NO) *reinterpret_cast<f32x4 *>(a.out + (size_t)b * a.ldo + col) = v;
         }
-        mh = fmaxf(mh, __shfl_xor(mh, 16));
-        mh = fmaxf(mh, __shfl_xor(mh, 32));
-        md = fmaxf(md, __shfl_xor(md, 16));
-        md = fmaxf(md, __shfl_xor(md, 32));
-        if (fq == 0) {
-            red[(wm * kWbN + rl) * 2] = mh;
-            red[(wm * kWbN + rl) * 2 + 1] = md;
+        if (!prod) return;
+        // epilogue: lane = trajectory b0 + 16 j + (lane & 15), columns m0 + 16 (TM cw + i) + 4 (lane >> 4) .. +3, in
+        // true units (x the row's down); and the row maxima of the dh and input-gradient columns
+        barrier();
+#pragma unroll
+        for (int j = 0; j < kWbTN; ++j) {
+            const int rl = 16 * j + fr, b = b0 + rl;
+            const float f = ldown[rl];
+            float mh = 0.0f, md = 0.0f;
+#pragma unroll
+            for (int i = 0; i < kWbTM; ++i) {
+                const int col = m0 + 16 * (kWbTM * cw + i) + 4 * fq;
+                const f32x4 v = acc[i][j] * f;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float av = fabsf(v[e]);
+                    if (col + e >= a.h0 && col + e < a.h1) mh = fmaxf(mh, av);
+                    if (col + e < a.d1) md = fmaxf(md, av);
+                }
+                if (b < a.NB && col < a.NO) *reinterpret_cast<f32x4 *>(a.out + (size_t)b * a.ldo + col) = v;
+            }
+            mh = fmaxf(mh, __shfl_xor(mh, 16));
+            mh = fmaxf(mh, __shfl_xor(mh, 32));
+            md = fmaxf(md, __shfl_xor(md, 16));
+            md = fmaxf(md, __shfl_xor(md, 32));
+            if (fq == 0) {
+                red[(cw * kWbN + rl) * 2] = mh;
+                red[(cw * kWbN + rl) * 2 + 1] = md;
+            }
         }
+        barrier();
+        return;
     }
-    __syncthreads();
+    // the producers (threads 0 .. 127 of them) reduce the consumers' row maxima over the column slices
     if (tid < kWbN && b0 + tid < a.NB) {
         float mh = 0.0f, md = 0.0f;
 #pragma unroll
-        for (int w = 0; w < kWbWM; ++w) {
+        for (int w = 0; w < kWbCons; ++w) {
             mh = fmaxf(mh, red[(w * kWbN + tid) * 2]);
             md = fmaxf(md, red[(w * kWbN + tid) * 2 + 1]);
         }
