@@ -78,3 +78,26 @@ def test_retired_f16fwd_mode_is_refused():
     c, params = load_case("ref_b15_n10")
     with pytest.raises(ValueError, match="precision"):
         run_p(params, c, "f16fwd")
+
+
+def test_f16_mode_nonfinite_incoming_gradient_propagates():
+    """The f16 mode's d records scale each trajectory's din by a power of two taken from its largest value (fcr_bwd.h
+    din_store_lp): an infinite upstream gradient must still come out non-finite, as in the fp32 mode
+    (test_gpu_parity.py test_nonfinite_incoming_gradient_propagates)."""
+    c, params = load_case("ref_b15_n10")
+    o = T.run(params, c["X"], c["u0"], c["states"], c["N"], c["alpha"], c["noise"], dloss=float("inf"), precision="f16")
+    for k, _ in T.GRADS:
+        assert not np.isfinite(o[k]).all(), k
+
+
+@pytest.mark.parametrize("shift", [-60, 40])
+def test_f16_mode_exactly_linear_in_a_power_of_two_dloss(shift):
+    """Every scale inside the f16 mode's backward (the dgates' per-trajectory 2^(13-e), the d records' 2^(14-e)) is
+    a power of two taken from the values themselves, so an incoming gradient 2^shift times larger or smaller moves
+    only exponents: the gradients come out exactly 2^shift times those at dloss = 1."""
+    c, params = load_case("ref_b15_n10")
+    args = (params, c["X"], c["u0"], c["states"], c["N"], c["alpha"], c["noise"])
+    base = T.run(*args, dloss=1.0, precision="f16")
+    scaled = T.run(*args, dloss=float(2.0 ** shift), precision="f16")
+    for k, _ in T.GRADS:
+        assert np.array_equal(scaled[k], (base[k].astype(np.float64) * 2.0 ** shift).astype(np.float32)), k
