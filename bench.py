@@ -423,7 +423,9 @@ def main():
                    "rocBLAS split-f16 gate GEMM + wide_cell_kernel",
             "bwd": ("backward pass: recompute wide_gemm_cell_kernel" if H % 64 == 0 else
                     "backward pass: recompute rocBLAS gate GEMM + wide_cell_kernel")
-                   + " + wide_cell_bwd_kernel + hand-written split-f16 [input grad | dh] product wide_bwd_gemm_kernel"}
+                   + (" + wide_bwd_fused_kernel (dgates on producer waves, split-f16 [input grad | dh] product on"
+                      " consumer waves)" if H % 8 == 0 and H <= 256 else
+                      " + wide_cell_bwd_kernel + rocBLAS split-f16 [input grad | dh] products")}
         kernel = (f"fcr_s{dom[0]}_kernel" if small else f"fcr_{dom[0]}_kernel") if narrow else wide_label[dom[0]]
         achieved = B * N * fl[dom[0]] / (dom[1] * 1e-3) / 1e12
         hbm_roof = HBM_PEAK_GBS * 1e9 / hbm_bytes_per_rollout_step(N)
