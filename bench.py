@@ -366,6 +366,11 @@ def main():
             ev[2].record(stream)
         if sync is not None:
             sync(ctrl, B, B * world, loss)
+            if ev is not None:
+                # after the all-reduce has been joined into the launching stream (RCCL: the collective's stream
+                # is waited on by this one before dist.all_reduce returns; gloo: host-side, so the event also
+                # carries the host round trip): ev[2] -> ev[3] is the step's exchange as the stream sees it
+                ev[3].record(stream)
         opt.step()
         return loss
 
@@ -384,7 +389,7 @@ def main():
 
     # timed region: K steps; HIP events on the launching stream bracket the fused forward and backward of
     # EVERY timed step (the per-kernel times come from the same steps as ms_per_step)
-    marks = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    marks = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -398,6 +403,7 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    dt_local = dt
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -406,12 +412,22 @@ def main():
     value = world * B * N / (dt / args.steps)
     if captured is not None:
         # graph replays carry no events between kernels: time the same kernels in a few eager steps after
-        marks = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(5)]
+        marks = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(5)]
         for k in range(len(marks)):
             step(marks[k])
         torch.cuda.synchronize()
     fwd_ms = [e[0].elapsed_time(e[1]) for e in marks]
     bwd_ms = [e[1].elapsed_time(e[2]) for e in marks]
+    ar_ms = [e[2].elapsed_time(e[3]) for e in marks] if sync is not None else []
+    per_rank = None
+    if world > 1:
+        # every rank's own means and step clock at rank 0: how far the ranks spread, and how much of the step the
+        # all-reduce is (Functions.py:1463 is the shard point; the exchange is the one grad all-reduce, :658)
+        mine = {"rank": rank, "device": str(dev), "fwd_ms": float(np.mean(fwd_ms)), "bwd_ms": float(np.mean(bwd_ms)),
+                "allreduce_ms": float(np.mean(ar_ms)), "allreduce_max_ms": float(np.max(ar_ms)),
+                "step_ms": 1000.0 * dt_local / args.steps}
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
 
     if rank == 0:
         f_ms, b_ms = float(np.mean(fwd_ms)), float(np.mean(bwd_ms))
@@ -474,9 +490,14 @@ def main():
                                         "number)"} if args.share_gpu else {})},
             "roofline": roof,
             "kernels_ms": {"fwd": f_ms, "bwd": b_ms,
+                           **({"allreduce": float(np.mean(ar_ms)), "allreduce_max": float(np.max(ar_ms))}
+                              if ar_ms else {}),
                            "source": ("HIP events on the launching stream, 5 eager steps after the graphed timed region"
                                       if captured is not None else
                                       "HIP events on the launching stream, every timed step")},
+            **({"ranks": {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                          "step_ms_spread": max(r["step_ms"] for r in per_rank) - min(r["step_ms"] for r in per_rank),
+                          "per_rank": per_rank}} if per_rank else {}),
             # the design's own HBM traffic (activation records and hand-off slabs, PMC-measured) against
             # 8 TB/s: how close the dominant kernel runs to the bandwidth its data movement needs
             "hbm_traffic_frac": (traffic / (dom[1] * 1e-3) / (HBM_PEAK_GBS * 1e9)) if traffic else None,

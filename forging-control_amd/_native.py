@@ -23,8 +23,9 @@ EXPORTS = ("fcr_workspace_size", "fcr_wide_kept_windows", "fcr_forward", "fcr_ba
            "fcr_lstm_forward", "fcr_lstm_backward", "fcr_plant_rk4", "fcr_closed_loop_run", "fcr_window_gather",
            "fcr_fnn_workspace_size", "fcr_fnn_forward", "fcr_fnn_backward", "fcr_set_small_batch_limit",
            "fcr_get_small_batch_limit", "fcr_set_wide_keep_budget", "fcr_get_wide_keep_budget", "fcr_last_error",
-           "fcr_abi_version")
+           "fcr_abi_version", "fcr_wide_bwd_cell_workspace", "fcr_wide_bwd_cell")
 OPT_INHERIT, KEEP_AUTO = -2, -1
+INT32_MAX, INT64_MAX = 2**31 - 1, 2**63 - 1
 
 
 class FcrDims(ctypes.Structure):
@@ -44,11 +45,12 @@ class FcrOptions(ctypes.Structure):
 def make_options(small_batch_limit=None, wide_keep_budget=None) -> FcrOptions:
     """Per-call options: None inherits the process-wide default; wide_keep_budget "auto" = the library's policy."""
     keep = OPT_INHERIT if wide_keep_budget is None else KEEP_AUTO if wide_keep_budget == "auto" else int(wide_keep_budget)
-    if wide_keep_budget is not None and keep < KEEP_AUTO:
-        raise ValueError(f"wide_keep_budget must be >= 0 bytes, 'auto' or None, got {wide_keep_budget!r}")
+    if wide_keep_budget is not None and not KEEP_AUTO <= keep <= INT64_MAX:
+        raise ValueError(f"wide_keep_budget must be 0..2**63-1 bytes, 'auto' or None, got {wide_keep_budget!r}")
     small = OPT_INHERIT if small_batch_limit is None else int(small_batch_limit)
-    if small < 0 and small_batch_limit is not None:
-        raise ValueError(f"small_batch_limit must be >= 0 or None, got {small_batch_limit!r}")
+    # the fields are c_int32 / c_int64: a value outside them would wrap silently into INHERIT or 'never'
+    if small_batch_limit is not None and not 0 <= small <= INT32_MAX:
+        raise ValueError(f"small_batch_limit must be 0..2**31-1 or None, got {small_batch_limit!r}")
     return FcrOptions(small, 0, keep)
 
 
@@ -141,6 +143,10 @@ def load() -> ctypes.CDLL:
         lib.fcr_last_error.restype = ctypes.c_char_p
         lib.fcr_abi_version.argtypes = []
         lib.fcr_abi_version.restype = i32
+        lib.fcr_wide_bwd_cell_workspace.argtypes = [i32, i32, i32, ctypes.POINTER(sz)]
+        lib.fcr_wide_bwd_cell_workspace.restype = i32
+        lib.fcr_wide_bwd_cell.argtypes = [i32, i32, i32] + [vp] * 11 + [sz, vp]
+        lib.fcr_wide_bwd_cell.restype = i32
         if lib.fcr_abi_version() != ABI_VERSION:
             raise NativeError(f"libfcr ABI {lib.fcr_abi_version()} != expected {ABI_VERSION}")
         _lib = lib

@@ -47,6 +47,21 @@ int launch_check(const char *what) {
     return FCR_OK;
 }
 
+// hipFuncSetAttribute(max dynamic LDS) once per (kernel instantiation, device): one bit per device in the caller's
+// static mask. The mask is atomic (calls on several threads are allowed, include/fcr.h), two first calls that race
+// both set the attribute (idempotent), and a second device in the process gets its own bit (devices past 63 set
+// it on every call).
+int lds_attr(const void *fn, int bytes, std::atomic<unsigned long long> &done, const char *what) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    const unsigned long long bit = (dev >= 0 && dev < 64) ? 1ull << dev : 0ull;
+    if (bit && (done.load(std::memory_order_acquire) & bit)) return FCR_OK;
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(%s): %s", what, hipGetErrorString(e));
+    done.fetch_or(bit, std::memory_order_release);
+    return FCR_OK;
+}
+
 // window-column scales of the f16 split's range guard (fcr_pack.h) -> wsc[8], from the call's inputs
 int launch_range(const fcr_dims *d, const float *states, const float *u0, const float *noise, const float *fcw,
                  const float *fcb, float *part, float *wsc, hipStream_t s) {
@@ -173,13 +188,8 @@ Packed packed_ptrs(const Layout &L, char *ws) {
 template <int HS, bool STORE, bool LP>
 int launch_fwd_t(const FwdArgs &fa, const Layout &L, hipStream_t s) {
     const int lds = LP ? Geo16<HS>::LDS_FWD_LP : Geo16<HS>::LDS_FWD;
-    static bool attr_set = false;
-    if (!attr_set) {
-        const hipError_t e = hipFuncSetAttribute((const void *)fcr_fwd_kernel<HS, STORE, LP>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(fwd): %s", hipGetErrorString(e));
-        attr_set = true;
-    }
+    static std::atomic<unsigned long long> attr_done{0};
+    if (const int rc = lds_attr((const void *)fcr_fwd_kernel<HS, STORE, LP>, lds, attr_done, "fwd")) return rc;
     hipLaunchKernelGGL((fcr_fwd_kernel<HS, STORE, LP>), dim3(L.nw_pad / kFwdWaves), dim3(kFwdWaves * kWave),
                        lds, s, fa);
     return launch_check("fcr_fwd_kernel");
@@ -194,13 +204,8 @@ int launch_fwd(const FwdArgs &fa, const Layout &L, bool lp, hipStream_t s) {
 template <int HS, bool LP>
 int launch_bwd_t(const BwdArgs &ba, const Layout &L, hipStream_t s) {
     const int lds = BwdLds<HS, LP>::BYTES;
-    static bool attr_set = false;
-    if (!attr_set) {
-        const hipError_t e = hipFuncSetAttribute((const void *)fcr_bwd_kernel<HS, LP>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(bwd): %s", hipGetErrorString(e));
-        attr_set = true;
-    }
+    static std::atomic<unsigned long long> attr_done{0};
+    if (const int rc = lds_attr((const void *)fcr_bwd_kernel<HS, LP>, lds, attr_done, "bwd")) return rc;
     hipLaunchKernelGGL((fcr_bwd_kernel<HS, LP>), dim3(L.nw_pad / kBwdWaves), dim3(kBwdWaves * kWave), lds, s, ba);
     return launch_check("fcr_bwd_kernel");
 }
@@ -229,13 +234,8 @@ void note_kernels(fcr_options *o, int family) {
 template <int HS, bool STORE>
 int launch_sfwd_t(const FwdArgs &fa, const Layout &L, hipStream_t s) {
     constexpr int lds = Small<HS>::LDS_FWD;
-    static bool attr_set = false;
-    if (!attr_set) {
-        const hipError_t e = hipFuncSetAttribute((const void *)fcr_sfwd_kernel<HS, STORE>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(sfwd): %s", hipGetErrorString(e));
-        attr_set = true;
-    }
+    static std::atomic<unsigned long long> attr_done{0};
+    if (const int rc = lds_attr((const void *)fcr_sfwd_kernel<HS, STORE>, lds, attr_done, "sfwd")) return rc;
     hipLaunchKernelGGL((fcr_sfwd_kernel<HS, STORE>), dim3(L.nw), dim3(Small<HS>::NQ * kWave), lds, s, fa);
     return launch_check("fcr_sfwd_kernel");
 }
@@ -243,13 +243,8 @@ int launch_sfwd_t(const FwdArgs &fa, const Layout &L, hipStream_t s) {
 template <int HS>
 int launch_sbwd_t(const BwdArgs &ba, const Layout &L, hipStream_t s) {
     constexpr int lds = Small<HS>::LDS_BWD;
-    static bool attr_set = false;
-    if (!attr_set) {
-        const hipError_t e = hipFuncSetAttribute((const void *)fcr_sbwd_kernel<HS>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(sbwd): %s", hipGetErrorString(e));
-        attr_set = true;
-    }
+    static std::atomic<unsigned long long> attr_done{0};
+    if (const int rc = lds_attr((const void *)fcr_sbwd_kernel<HS>, lds, attr_done, "sbwd")) return rc;
     hipLaunchKernelGGL((fcr_sbwd_kernel<HS>), dim3(L.nw), dim3(Small<HS>::NQ * kWave), lds, s, ba);
     return launch_check("fcr_sbwd_kernel");
 }
@@ -603,13 +598,8 @@ __global__ __launch_bounds__(256) void pack_all_kernel(PackAllArgs p) {
 // H = 256; DESIGN.md "Config 5"); rocBLAS gemm16_fwd + wide_cell_kernel for other H.
 bool wide_fused_ok(int H) { return H % kWgU == 0; }
 int launch_wgemm_cell(const WgArgs &wa, hipStream_t s) {
-    static bool attr_set = false;
-    if (!attr_set) {
-        const hipError_t e = hipFuncSetAttribute((const void *)wide_gemm_cell_kernel,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kWgLds);
-        if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(wgemm): %s", hipGetErrorString(e));
-        attr_set = true;
-    }
+    static std::atomic<unsigned long long> attr_done{0};
+    if (const int rc = lds_attr((const void *)wide_gemm_cell_kernel, kWgLds, attr_done, "wgemm")) return rc;
     if (wa.K <= 0 || wa.K % kWgK || wa.lda % 8 || wa.ldb % 8 || wa.H % kWgU || wa.B <= 0)
         return fail(FCR_EINVAL, "wide_gemm_cell_kernel: K %d lda %d ldb %d H %d B %d off its tiling", wa.K, wa.lda, wa.ldb,
                     wa.H, wa.B);
@@ -621,13 +611,9 @@ int launch_wgemm_cell(const WgArgs &wa, hipStream_t s) {
 // One backward cell of the fused path (fcr_wbwd.h): dgates formed in the product's prologue, out = dG [W_ih | W_hh]
 // (columns [0, NO), NO = 0: the dgate part only) in true units
 int launch_fb(const WbArgs &wa, bool l0, hipStream_t s) {
-    static bool attr_set[2] = {false, false};
+    static std::atomic<unsigned long long> attr_done[2] = {{0}, {0}};
     const void *fn = l0 ? (const void *)wide_bwd_fused_kernel<true> : (const void *)wide_bwd_fused_kernel<false>;
-    if (!attr_set[l0]) {
-        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kWbLds);
-        if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(wbwd): %s", hipGetErrorString(e));
-        attr_set[l0] = true;
-    }
+    if (const int rc = lds_attr(fn, kWbLds, attr_done[l0], "wbwd")) return rc;
     if (wa.NO < 0 || wa.NO > 2 * kWbM || wa.NO % 4 || wa.H % 8 || wa.H > kWbMaxH || wa.NB <= 0 || wa.ldo % 4 ||
         wa.ldh % 4 || wa.ldx % 4 || (l0 && (!wa.wih0 || !wa.rowg)))
         return fail(FCR_EINVAL, "wide_bwd_fused_kernel: NO %d H %d B %d ldo %d off its tiling", wa.NO, wa.H, wa.NB, wa.ldo);
@@ -635,6 +621,95 @@ int launch_fb(const WbArgs &wa, bool l0, hipStream_t s) {
     if (l0) hipLaunchKernelGGL((wide_bwd_fused_kernel<true>), dim3((unsigned)(nx * ny)), dim3(kWbThreads), kWbLds, s, wa);
     else hipLaunchKernelGGL((wide_bwd_fused_kernel<false>), dim3((unsigned)(nx * ny)), dim3(kWbThreads), kWbLds, s, wa);
     return launch_check("wide_bwd_fused_kernel");
+}
+
+// |v| row maxima over the first n columns of B rows of stride ld (one wave per row): the row bounds fcr_wide_bwd_cell
+// hands the fused backward cell, which the rollout gets from the kernels that wrote those rows
+__global__ __launch_bounds__(256) void row_absmax_kernel(const float *__restrict__ v, int n, int ld, int B,
+                                                         float *__restrict__ out) {
+    const int b = blockIdx.x * 4 + (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (b >= B) return;
+    float m = 0.0f;
+    for (int i = lane; i < n; i += 64) m = fmaxf(m, fabsf(v[(size_t)b * ld + i]));
+#pragma unroll
+    for (int o = 32; o; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if (lane == 0) out[b] = m;
+}
+
+// fcr_wide_bwd_cell (test hook): the scratch of one standalone fused backward cell
+struct CellHookLayout {
+    size_t bt, rm, total;
+};
+CellHookLayout cell_hook_layout(int B, int H, int layer0) {
+    CellHookLayout L{};
+    const size_t NP = layer0 ? H : 2 * (size_t)H;
+    L.bt = 0;
+    L.rm = align_up(sizeof(_Float16) * 2 * NP * 4 * H);
+    L.total = L.rm + align_up(sizeof(float) * 5 * (size_t)B);   // rm_c [B], rm_h [2][B], rm_d [2][B]
+    return L;
+}
+int cell_hook_check(int B, int H) {
+    if (B < 1) return fail(FCR_EINVAL, "fcr_wide_bwd_cell: B=%d", B);
+    if (!wide_fused_bwd_ok(H)) return fail(FCR_EUNSUPPORTED, "fcr_wide_bwd_cell: H=%d off the fused cell's tiling", H);
+    return FCR_OK;
+}
+
+// One backward cell of the H > 52 path exactly as wide_backward launches it (launch_fb, fcr_wbwd.h), on caller-given
+// inputs: the standalone form the per-element tests of tests/test_wide_cell.py compare with an fp64 product
+int wide_bwd_cell_hook(int B, int H, int layer0, const float *w_ih, const float *w_hh, const float *pre,
+                       const float *c_prev, const float *dh, const float *din, const float *dc, float *out,
+                       float *dc_out, float *rowg, char *base, hipStream_t s) {
+    const CellHookLayout L = cell_hook_layout(B, H, layer0);
+    const int NP = layer0 ? H : 2 * H;
+    const size_t nbt = (size_t)NP * 4 * H;
+    _Float16 *bt = (_Float16 *)(base + L.bt);
+    hipLaunchKernelGGL(wide_split_bt_kernel, dim3((unsigned)((nbt + 255) / 256)), dim3(256), 0, s,
+                       layer0 ? (const float *)nullptr : w_ih, w_hh, H, NP, bt, bt + nbt);
+    int rc = launch_check("wide_split_bt_kernel");
+    if (rc) return rc;
+    float *rm = (float *)(base + L.rm);
+    float *rm_c = rm, *rm_h = rm + B, *rm_d = rm + 3 * (size_t)B;
+    if (hipMemsetAsync(rm, 0, sizeof(float) * 5 * (size_t)B, s) != hipSuccess) return fail(FCR_EHIP, "hipMemsetAsync failed");
+    const dim3 rg((unsigned)((B + 3) / 4)), rb(256);
+    hipLaunchKernelGGL(row_absmax_kernel, rg, rb, 0, s, dc, H, H, B, rm_c);
+    hipLaunchKernelGGL(row_absmax_kernel, rg, rb, 0, s, dh, H, H, B, rm_h);
+    if (din) hipLaunchKernelGGL(row_absmax_kernel, rg, rb, 0, s, din, H, H, B, rm_d);
+    if ((rc = launch_check("row_absmax_kernel"))) return rc;
+    WbArgs wa{};
+    wa.Ahi = bt;
+    wa.Alo = bt + nbt;
+    wa.NB = B;
+    wa.H = H;
+    wa.pre = pre;
+    wa.c_prev = c_prev;
+    wa.dh = dh;
+    wa.ldh = H;
+    wa.din = din;
+    wa.ldx = H;
+    wa.dC = dc;
+    wa.dC_out = dc_out;
+    wa.rm_c = rm_c;
+    wa.rm_h = rm_h;
+    wa.rm_d = din ? rm_d : nullptr;
+    wa.out = out;
+    if (!layer0) {   // [input gradient | dh_{t-1}] (t = 0, no c_prev: the former only)
+        wa.ldo = 2 * H;
+        wa.NO = c_prev ? 2 * H : H;
+        wa.h0 = H;
+        wa.h1 = c_prev ? 2 * H : H;
+        wa.d1 = H;
+    } else {         // dh_{t-1} (none at t = 0) and the window-row gradient
+        if (hipMemsetAsync(rowg, 0, sizeof(float) * kIn * (size_t)B, s) != hipSuccess)
+            return fail(FCR_EHIP, "hipMemsetAsync failed");
+        wa.ldo = H;
+        wa.NO = c_prev ? H : 0;
+        wa.h0 = 0;
+        wa.h1 = H;
+        wa.d1 = 0;
+        wa.wih0 = w_ih;
+        wa.rowg = rowg;
+    }
+    return launch_fb(wa, layer0 != 0, s);
 }
 
 // One window's cells, forward: 3 layers x 10 steps of [GEMM x_t W_ih^T, GEMM h_{t-1} W_hh^T, cell].
@@ -1142,13 +1217,9 @@ SurArgs sur_args(const fcr_dims *d, const SurLayout &L, char *base) {
 template <int HS>
 int sur_forward_t(const SurArgs &a, const SurLayout &L, bool store, hipStream_t s) {
     constexpr int lds = SurGeo<HS>::LDS_FWD;
-    static bool attr_set[2] = {false, false};
+    static std::atomic<unsigned long long> attr_done[2] = {{0}, {0}};
     const void *fn = store ? (const void *)sur_fwd_kernel<HS, true> : (const void *)sur_fwd_kernel<HS, false>;
-    if (!attr_set[store]) {
-        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(sur_fwd): %s", hipGetErrorString(e));
-        attr_set[store] = true;
-    }
+    if (const int rc = lds_attr(fn, lds, attr_done[store], "sur_fwd")) return rc;
     if (store) hipLaunchKernelGGL((sur_fwd_kernel<HS, true>), dim3(L.nw_pad / kFwdWaves), dim3(kFwdWaves * kWave), lds, s, a);
     else hipLaunchKernelGGL((sur_fwd_kernel<HS, false>), dim3(L.nw_pad / kFwdWaves), dim3(kFwdWaves * kWave), lds, s, a);
     return launch_check("sur_fwd_kernel");
@@ -1157,13 +1228,8 @@ int sur_forward_t(const SurArgs &a, const SurLayout &L, bool store, hipStream_t 
 template <int HS, bool L0>
 int sur_wgrad_t(const SurArgs &a, const SurLayout &L, int l, float *part, float *g_ih, float *g_hh, hipStream_t s) {
     using W = SurWg<HS, L0>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        const hipError_t e = hipFuncSetAttribute((const void *)sur_wgrad_kernel<HS, L0>,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, W::LDS);
-        if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(sur_wgrad): %s", hipGetErrorString(e));
-        attr_set = true;
-    }
+    static std::atomic<unsigned long long> attr_done{0};
+    if (const int rc = lds_attr((const void *)sur_wgrad_kernel<HS, L0>, W::LDS, attr_done, "sur_wgrad")) return rc;
     const int nkb = sur_nkb(L.nw);
     hipLaunchKernelGGL((sur_wgrad_kernel<HS, L0>), dim3(L.groups), dim3(kSurWgThreads), W::LDS, s, a, l, nkb, part);
     int rc = launch_check("sur_wgrad_kernel");
@@ -1183,13 +1249,8 @@ template <int HS>
 int sur_backward_t(const SurArgs &a, const SurLayout &L, float *const *g_w_ih, float *const *g_w_hh, float *part,
                    hipStream_t s) {
     constexpr int lds = SurGeo<HS>::LDS_BWD;
-    static bool attr_set = false;
-    if (!attr_set) {
-        const hipError_t e = hipFuncSetAttribute((const void *)sur_bwd_kernel<HS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 lds);
-        if (e != hipSuccess) return fail(FCR_EHIP, "hipFuncSetAttribute(sur_bwd): %s", hipGetErrorString(e));
-        attr_set = true;
-    }
+    static std::atomic<unsigned long long> attr_done{0};
+    if (const int rc = lds_attr((const void *)sur_bwd_kernel<HS>, lds, attr_done, "sur_bwd")) return rc;
     hipLaunchKernelGGL((sur_bwd_kernel<HS>), dim3(L.nw_pad / kBwdWaves), dim3(kBwdWaves * kWave), lds, s, a);
     int rc = launch_check("sur_bwd_kernel");
     if (rc) return rc;
@@ -1303,6 +1364,27 @@ size_t fcr_debug_stamp_offset(const fcr_dims *d) { return make_layout(d, 1).stam
 size_t fcr_debug_dseq_offset(const fcr_dims *d) { return make_layout(d, 1).dseq; }
 size_t fcr_debug_dxrow_offset(const fcr_dims *d) { return make_layout(d, 1).dxrow; }
 #endif
+
+int fcr_wide_bwd_cell_workspace(int32_t B, int32_t H, int32_t layer0, size_t *bytes) {
+    if (const int rc = cell_hook_check(B, H)) return rc;
+    if (!bytes) return fail(FCR_EINVAL, "bytes is NULL");
+    *bytes = cell_hook_layout(B, H, layer0).total;
+    return FCR_OK;
+}
+
+int fcr_wide_bwd_cell(int32_t B, int32_t H, int32_t layer0, const float *w_ih, const float *w_hh, const float *pre,
+                      const float *c_prev, const float *dh, const float *din, const float *dc, float *out,
+                      float *dc_out, float *rowg, void *ws, size_t ws_bytes, void *stream) {
+    if (const int rc = cell_hook_check(B, H)) return rc;
+    if (!w_hh || !pre || !dh || !dc || !dc_out || !ws || (!layer0 && !w_ih) || (layer0 && (!w_ih || !rowg)) ||
+        ((c_prev || !layer0) && !out))
+        return fail(FCR_EINVAL, "fcr_wide_bwd_cell: a required pointer is NULL");
+    if (((uintptr_t)ws) & 255) return fail(FCR_EINVAL, "fcr_wide_bwd_cell: ws must be 256-byte aligned");
+    const size_t need = cell_hook_layout(B, H, layer0).total;
+    if (ws_bytes < need) return fail(FCR_EWORKSPACE, "fcr_wide_bwd_cell: ws has %zu bytes, needs %zu", ws_bytes, need);
+    return wide_bwd_cell_hook(B, H, layer0, w_ih, w_hh, pre, c_prev, dh, din, dc, out, dc_out, rowg, (char *)ws,
+                              (hipStream_t)stream);
+}
 
 int fcr_workspace_size(const fcr_dims *dims, const fcr_options *opts, int with_backward, size_t *bytes) {
     int rc = check_dims(dims);

@@ -288,7 +288,12 @@ __global__ void wide_head_kernel(WideArgs a, int j, float *rmh) {
 // The per-row dgate scale of the fused backward cell (fcr_wbwd.h) is 2^(kWideDgExp - e), e the exponent of a bound m on
 // the row's |dc_t| (m >= |dc| + |dh|): the i, g, o rows are |dc_t| or |dh| times a local derivative <= 1, so below
 // 2^kWideDgExp scaled; the forget row is dc_t c_{t-1} f (1 - f) with |c_{t-1}| <= t <= kL - 1 (|c_t| <= |c_{t-1}| + 1
-// from c = 0), so it reaches (kL - 1) / 4 * 2^kWideDgExp (18 432 at kL = 10): a finite f16, with that margin only
+// from c = 0), so it reaches (kL - 1) / 4 * 2^kWideDgExp (18 432 at kL = 10): a finite f16, with that margin only.
+// |c_{t-1}| <= t holds because EVERY window's LSTM starts from h = c = 0 (Functions.py:349-350): the rollout never
+// carries a state into a window, and no ABI entry takes an initial c; a path that did would need its own bound here.
+// The bound is formed with fmaxf, which drops a NaN row maximum: the NaN dgates themselves still propagate into the
+// products, so a non-finite gradient stays non-finite (tests/test_gpu_parity.py
+// test_wide_forget_dgates_near_their_f16_margin drives the forget row to 2 of the 9/4 this allows).
 constexpr int kWideDgExp = 13;
 static_assert((kL - 1) * (1 << kWideDgExp) / 4 < 65504, "f16 overflow of the forget-gate dgates: lower kWideDgExp");
 // With PRE, c_t is recomputed from the pre-activations and c_{t-1} rather than loaded (round 3d: bit-identical,

@@ -42,6 +42,7 @@ class CallInfo:
     def __init__(self, opts):
         self.opts = opts
         self.forward = self.backward = None   # "small", "fused" or "wide" once the pass has run
+        self.small_batch_limit = None         # the limit both passes ran with (an inherited one resolved by the forward)
         self.workspace_bytes = 0
         self.kept_windows = 0
 
@@ -63,7 +64,13 @@ class RolloutFn(torch.autograd.Function):
         need_grad = any(ctx.needs_input_grad[i] for i in (1, 4, 5, 6))
         if info is None:
             info = CallInfo(_native.make_options())
-        opts = info.opts
+        # the small-batch limit resolved ONCE, here: an inherited limit is read from the process-wide default now,
+        # and the backward (possibly on the autograd thread, after the caller changed that default) runs with the
+        # same value, so both passes pick their kernel family from one limit
+        small = info.opts.small_batch_limit
+        if small < 0:
+            small = int(lib.fcr_get_small_batch_limit())
+        opts = _native.FcrOptions(small, 0, info.opts.wide_keep_budget)
         try:
             ws = torch.empty(_native.workspace_bytes(dims, need_grad, opts), dtype=torch.uint8, device=dev)
         except torch.cuda.OutOfMemoryError:
@@ -95,6 +102,7 @@ class RolloutFn(torch.autograd.Function):
                                       _ptr(prediction), _ptr(xhat), int(need_grad), _ptr(ws), ws.numel(),
                                       _stream(dev)), "fcr_forward")
         info.forward, info.backward = _native.KERNEL_FAMILIES[opts.kernels], None
+        info.small_batch_limit = small
         ctx.mark_non_differentiable(cost, command, error, prediction, xhat)
         # only loss carries a gradient: without this autograd launches a zero-fill kernel per output
         # before every backward (six per step, ~3 us each at the reference's B = 15)
@@ -103,6 +111,7 @@ class RolloutFn(torch.autograd.Function):
             ctx.ws = ws
             ctx.dims = dims
             ctx.info = info
+            ctx.small_limit = small
             ctx.save_for_backward(Xc, stc, prediction)
             ctx.ctrl_shapes = (W_inp.shape, b_inp.shape, W_out.shape)
         return loss, cost, command, error, prediction, xhat
@@ -124,8 +133,10 @@ class RolloutFn(torch.autograd.Function):
         g_wo = torch.empty(s_wo, **f32)
         dl = g_loss.detach().to(torch.float32).reshape(1).contiguous()
         info = ctx.info
-        # the forward's options (this call's, not process state): the autograd thread sees what the caller set
-        opts = _native.FcrOptions(info.opts.small_batch_limit, 0, info.opts.wide_keep_budget)
+        # the call's options; an inherited small-batch limit is the value the forward resolved (no process state is
+        # read here, so a default changed in between on another thread does not split the passes)
+        small = info.opts.small_batch_limit if info.opts.small_batch_limit >= 0 else ctx.small_limit
+        opts = _native.FcrOptions(small, 0, info.opts.wide_keep_budget)
         _native.check(lib.fcr_backward(ctypes.byref(ctx.dims), ctypes.byref(opts), _ptr(Xc), _ptr(stc),
                                        _ptr(prediction), _ptr(dl), _ptr(g_u0), _ptr(g_wi), _ptr(g_bi), _ptr(g_wo),
                                        _ptr(ctx.ws), ctx.ws.numel(), _stream(dev)), "fcr_backward")

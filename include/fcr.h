@@ -272,6 +272,26 @@ int fcr_get_small_batch_limit(void);
 int64_t fcr_set_wide_keep_budget(int64_t bytes);
 int64_t fcr_get_wide_keep_budget(void);
 
+/*
+ * TEST HOOK (not a reference interface; nothing on the rollout path calls it): ONE backward cell of the H > 52 path,
+ * i.e. the autograd backward of one nn.LSTM cell (Functions.py:325, inside loss.backward() at :655), run by the same
+ * kernel and launcher fcr_backward uses (wide_bwd_fused_kernel), on caller-given inputs, so a test can compare every
+ * output element with an fp64 evaluation. H % 8 == 0 and H <= 256 (the fused cell's tiling). Per trajectory b:
+ *   pre (B,4H)  gate pre-activations, torch order i|f|g|o;  c_prev (B,H) or NULL (t = 0);
+ *   dh (B,H) incoming dh_t of the recurrence;  din (B,H) the layer above's input gradient at t, or NULL;
+ *   dc (B,H) carried dc_t;  ->  dc_out (B,H) = dc_{t-1};
+ *   layer0 == 0: out (B,2H) = dG [W_ih | W_hh] (input gradient | dh_{t-1}; only the first H columns without c_prev),
+ *                w_ih (4H,H), w_hh (4H,H);
+ *   layer0 != 0: out (B,H) = dG W_hh (dh_{t-1}; not written without c_prev), rowg (B,5) = dG W_ih0 (overwritten),
+ *                w_ih = W_ih0 (4H,5), w_hh (4H,H).
+ * dG are the gate gradients of the cell update c = f c_prev + i g, h = o tanh(c) for dh + din and dc. Scratch:
+ * fcr_wide_bwd_cell_workspace bytes, 256-byte aligned.
+ */
+int fcr_wide_bwd_cell_workspace(int32_t B, int32_t H, int32_t layer0, size_t *bytes);
+int fcr_wide_bwd_cell(int32_t B, int32_t H, int32_t layer0, const float *w_ih, const float *w_hh, const float *pre,
+                      const float *c_prev, const float *dh, const float *din, const float *dc, float *out,
+                      float *dc_out, float *rowg, void *ws, size_t ws_bytes, void *stream);
+
 /* Thread-local description of the last error (never NULL). */
 const char *fcr_last_error(void);
 

@@ -342,3 +342,35 @@ def test_unscaled_window_values_stay_finite_like_torch_fp32(H, scale):
         assert np.isfinite(o[k]).all(), k
         e_hip, e_t32 = relerr(o[k], r64[k]), relerr(r32[k], r64[k])
         assert e_hip <= max(5e-5, 4 * e_t32), (k, e_hip, e_t32)
+
+
+def test_wide_forget_dgates_near_their_f16_margin():
+    """H > 52 backward: the per-row dgate scale 2^(13 - e) bounds every scaled dgate by |dc_t| times a local derivative
+    <= 1, except the forget row, dc_t c_{t-1} f (1 - f), which relies on |c_{t-1}| <= t from each window's zero
+    initial state (Functions.py:349-350; fcr_wide.h kWideDgExp). This drives that row toward its margin: input and
+    cell gates saturated (i = g = 1) and the forget gate at 1 for eight steps, so c grows by one per step, then at
+    f = 1/2 (its largest f (1 - f)) in the window's ninth row: c_{t-1} f (1 - f) = 2 where the bound allows 9/4, i.e.
+    scaled forget dgates ~16 k of f16's 65 504. The gradients must still meet the fp64 oracle."""
+    from tests.golden.make_golden import synth_params
+    H, B, N = 64, 48, 2
+    p = synth_params(H, 4242)
+    X, S, _ = _synth(B, N, 4243)
+    wih0 = p["Wih"][0].copy()
+    wih0[0:H, 3] += 30.0            # input gate <- column 3 (z)
+    wih0[2 * H:3 * H, 3] += 30.0    # cell gate  <- column 3
+    wih0[H:2 * H, 0] += 30.0        # forget gate <- column 0 (y_dot)
+    p["Wih"][0] = wih0.astype(np.float32).astype(np.float64)
+    S[:, :, 3] = 1.0
+    S[:, :8, 0] = 1.0               # f = 1 over rows 0..7
+    S[:, 8:, 0] = 0.0               # f ~ 1/2 from row 8 (the other weights add O(0.1) to the pre-activation)
+    u0 = _u0(p, X)
+    o = run(p, X, u0, S, N, 20.0)
+    assert o["families"] == ("wide", "wide")
+    _, f, tape = R.rollout_forward(p, X, u0, S, N, 20.0)
+    g = R.rollout_backward(p, tape)
+    assert np.all(np.isfinite(o["xhat"]))
+    for k in FEATS + ("xhat",):
+        assert relerr(o[k], f[k]) <= TOL, (k, relerr(o[k], f[k]))
+    for k, _ in GRADS:
+        assert np.all(np.isfinite(o[k])), k
+        assert relerr(o[k], g[k]) <= TOL, (k, relerr(o[k], g[k]))

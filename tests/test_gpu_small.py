@@ -157,3 +157,59 @@ def test_two_losses_with_different_options_run_concurrently():
             for k in FEATS + ("xhat",) + tuple(k for k, _ in GRADS):
                 assert np.array_equal(res[lim][k], alone[lim][k]), (rep, lim, k)
     assert native.small_batch_limit() == default
+
+
+def test_inherited_limit_is_resolved_once_by_the_forward():
+    """A call that inherits the process-wide small-batch limit runs BOTH passes with the value its forward read,
+    even when the default changes before the backward (which torch may run on its autograd thread): the two
+    passes never split across kernel families through process state."""
+    c, params = load_case("ref_b15_n10")
+    sim, ctrl = modules(params)
+    d = lambda a: torch.as_tensor(np.asarray(a, np.float32), device=DEV)
+    u0_t = d(c["u0"]).reshape(-1, 1).requires_grad_(True)
+    fn = fca.MPCLoss(prediction_horizon=int(c["N"]), alpha=float(c["alpha"]))   # inherits the default (8192)
+    loss, _ = fn(sim, ctrl, d(c["X"]), u0_t, d(c["states"]), DEV)
+    prev = native.set_small_batch_limit(0)   # "never" from here on, before the backward
+    try:
+        loss.backward()
+        torch.cuda.synchronize()
+    finally:
+        native.set_small_batch_limit(prev)
+    assert (fn.last_call.forward, fn.last_call.backward) == ("small", "small")
+    assert fn.last_call.small_batch_limit == prev
+    assert relerr(u0_t.grad.reshape(-1).cpu().numpy(), c["g_u0_64"]) <= TOL
+
+
+def test_two_wide_losses_with_different_keep_budgets_run_concurrently():
+    """The H > 52 path under the same concurrency as above: two MPCLoss calls at H = 64 on two
+    threads and streams, one keeping every window (its backward skips the recompute) and one keeping none (its
+    backward recomputes every window), at once; each is bit-identical to running it alone."""
+    c, params = load_case("h64_b24_n3")
+    args = (params, c["X"], c["u0"], c["states"], c["N"], c["alpha"])
+    budgets = (0, 1 << 40)
+    alone = {kb: run(*args, wide_keep_budget=kb) for kb in budgets}
+    assert alone[0]["kept_windows"] == 0 and alone[1 << 40]["kept_windows"] == int(c["N"])
+    for rep in range(3):
+        res, errs = {}, []
+        barrier = threading.Barrier(2)
+
+        def worker(kb):
+            try:
+                s = torch.cuda.Stream(DEV)
+                with torch.cuda.stream(s):
+                    barrier.wait()
+                    res[kb] = run(*args, wide_keep_budget=kb)
+            except Exception as e:   # surfaced below
+                errs.append(e)
+
+        ts = [threading.Thread(target=worker, args=(kb,)) for kb in budgets]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errs, errs
+        for kb in budgets:
+            assert res[kb]["families"] == ("wide", "wide"), (rep, kb, res[kb]["families"])
+            assert res[kb]["kept_windows"] == alone[kb]["kept_windows"]
+            for k in FEATS + ("xhat",) + tuple(k for k, _ in GRADS):
+                assert np.array_equal(res[kb][k], alone[kb][k]), (rep, kb, k)
