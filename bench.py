@@ -434,14 +434,10 @@ def main():
         fl = flops_per_rollout_step(H)
         dom = ("bwd", b_ms) if b_ms >= f_ms else ("fwd", f_ms)
         narrow = H <= 52
-        wide_label = {   # H > 52 (fcr_wide.h / fcr_wgemm.h); the fused cell kernel needs H % 64 == 0
-            "fwd": "wide_gemm_cell_kernel (hand-written split-f16 GEMM + cell update)" if H % 64 == 0 else
-                   "rocBLAS split-f16 gate GEMM + wide_cell_kernel",
-            "bwd": ("backward pass: recompute wide_gemm_cell_kernel" if H % 64 == 0 else
-                    "backward pass: recompute rocBLAS gate GEMM + wide_cell_kernel")
-                   + (" + wide_bwd_fused_kernel (dgates on producer waves, split-f16 [input grad | dh] product on"
-                      " consumer waves)" if H % 8 == 0 and H <= 256 else
-                      " + wide_cell_bwd_kernel + rocBLAS split-f16 [input grad | dh] products")}
+        wide_label = {   # H > 52 (fcr_wgemm.h / fcr_wbwd.h; H padded to whole 64-unit blocks)
+            "fwd": "wide_cell_fwd_kernel (hand-written split-f16 GEMM + cell update)",
+            "bwd": "backward pass: recompute wide_cell_fwd_kernel (windows not kept) + wide_bwd_fused_kernel (dgates on "
+                   "producer waves, split-f16 [input grad | dh] product on consumer waves)"}
         kernel = (f"fcr_s{dom[0]}_kernel" if small else f"fcr_{dom[0]}_kernel") if narrow else wide_label[dom[0]]
         achieved = B * N * fl[dom[0]] / (dom[1] * 1e-3) / 1e12
         hbm_roof = HBM_PEAK_GBS * 1e9 / hbm_bytes_per_rollout_step(N)

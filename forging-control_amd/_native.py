@@ -11,7 +11,9 @@ import threading
 
 _LIB_NAME = "libfcr.so"
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", _LIB_NAME)
+# FCR_LIB: another build of the same ABI (A/B timing, scripts/inject_stale_lo.sh's fault-injected build); the
+# in-tree library otherwise
+LIB_PATH = os.environ.get("FCR_LIB") or os.path.join(_HERE, "lib", _LIB_NAME)
 
 FCR_OK = 0
 ABI_VERSION = 5

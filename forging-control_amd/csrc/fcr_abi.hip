@@ -98,11 +98,6 @@ constexpr int kMaxWideH = 2048;   // H > 4*kMaxSlots: the GEMM-per-cell path (fc
 bool is_wide(const fcr_dims *d) { return d->H > 4 * kMaxSlots; }
 int slot_tier(int H) { return H <= 16 ? 4 : (H <= 32 ? 8 : 13); }
 
-// H > 52: each backward cell as ONE hand-written kernel (fcr_wbwd.h: the cell's dgates formed in the prologue of the
-// split-f16 [input grad | dh_{t-1}] product) when a K step of 8 units tiles H and [input grad | dh] fits the two
-// column blocks of its row bounds; rocBLAS products + wide_cell_bwd_kernel otherwise.
-bool wide_fused_bwd_ok(int H) { return H % 8 == 0 && H <= kWbMaxH; }
-
 int check_dims(const fcr_dims *d) {
     if (!d) return fail(FCR_EINVAL, "dims is NULL");
     if (d->B < 1) return fail(FCR_EINVAL, "B=%d must be >= 1", d->B);
@@ -250,22 +245,27 @@ int launch_sbwd_t(const BwdArgs &ba, const Layout &L, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// H > 52: GEMM-per-cell path (fcr_wide.h)
+// H > 52: the batch-wide path (fcr_wide.h, fcr_wgemm.h, fcr_wbwd.h)
 // ---------------------------------------------------------------------------------------------
+// Every kernel of the rollout's wide path runs at Hp = H padded to whole 64-unit blocks of the forward cell kernel
+// (fcr_wgemm.h): the padding units have zero weights in and out, so their gates stay i = f = o = 1/2, g = 0, c = h = 0
+// and every product they enter gains exact zeros (the H <= 52 tiers pad the same way, slot_tier). The split weights,
+// the readout's fc.W and the window-row gradient's W_ih0 are packed padded per call; the caller's tensors keep H.
+int wide_hp(int H) { return (H + kWgU - 1) / kWgU * kWgU; }
+// column blocks of the fused backward cell's [input gradient | dh_{t-1}] product (fcr_wbwd.h): the row-bound slots
+int wide_nslots(int Hp) { return (2 * Hp + kWbM - 1) / kWbM; }
+int wide_dslots(int Hp) { return (Hp + kWbM - 1) / kWbM; }   // the blocks holding the input-gradient columns [0, Hp)
+
 struct WideLayout {
-    size_t wih[3], whh[3], fcw, fcb, cwi, cbi, cwo, fcp, fcbo, fnp, xhat, tot, cmd, err, X0, Hs, Cs, G;
-    size_t Act, dH, dC, D[2], rowg, dv, fnn_part, wsc, rng, total;
-    // split-f16 gate GEMM operands (fcr_wide.h: forward A per layer, backward A per weight, the cells'
-    // operand rows XB [3][10][B][6H] (layer 0 rows 3H + kX16 long), the dgate rows [B][12H])
-    size_t fa[3], bih[3], XB, dGsp, consts;   // bih: layers >= 1 backward A [12H][2H]
-    size_t bt[3];     // fused backward cell (fcr_wbwd.h): W^T split [NO][4H] hi, then lo (unit-major K)
-    size_t DC2, RMc, RMh, RMd;   // fused: the second dc buffer, the row bounds [2][B], [2][2][B], [2][kL][2][B]
-    size_t bx0, E0;   // layer 0's backward A [12H][H + 8] and its product rows [B][H + 8]
+    int Hp, ns, keep, ctrl_blocks;
+    size_t fcw, fcb, cwi, cbi, cwo, fcp, fcbo, fnp, wsc, rng, xhat, tot, cmd, err, Hs, Cs, WR, HR, total;
+    size_t fw[3];   // forward split weights per layer: [2][4Hp][K] (W_hi, W_lo; K = kx + Hp, wide_split_fw_kernel)
+    size_t bt[3];   // backward product A per layer: [2][NO][4Hp] (hi, lo; NO = Hp for layer 0, else 2Hp)
+    size_t w0p;     // W_ih0 packed [Hp][4][kIn] (the fused layer-0 cell's window-row gradient)
+    size_t Act, dH, dC, DC2, D[2], E0, RMc, RMh, RMd, rowg, dv, fnn_part;
     // kept windows (the last `keep` of N): the forward's gate pre-activations and c per cell
-    // [keep][3][10][B][4H] / [keep][3][10][B][H], so the backward skips their recompute (wide_keep_fit)
+    // [keep][3][10][B][4Hp] / [keep][3][10][B][Hp], so the backward skips their recompute (wide_keep_fit)
     size_t KA, KC;
-    int keep;
-    int ctrl_blocks;
 };
 
 WideLayout make_wide(const fcr_dims *d, int with_backward, int keep = 0) {
@@ -276,12 +276,11 @@ WideLayout make_wide(const fcr_dims *d, int with_backward, int keep = 0) {
         off += align_up(bytes);
         return o;
     };
-    const size_t B = d->B, N = d->N, H = d->H, F = sizeof(float);
-    for (int l = 0; l < kLayers; ++l) {
-        L.wih[l] = take(F * 4 * H * (l == 0 ? kIn : H));
-        L.whh[l] = take(F * 4 * H * H);
-    }
-    L.fcw = take(F * kOut * H);
+    const size_t B = d->B, N = d->N, F = sizeof(float), F16 = sizeof(_Float16);
+    const size_t Hp = (size_t)wide_hp(d->H);
+    L.Hp = (int)Hp;
+    L.ns = wide_nslots((int)Hp);
+    L.fcw = take(F * kOut * Hp);
     L.fcb = take(F * kOut);
     L.cwi = take(F * d->ctrl_hidden * kCtrlIn);
     L.cbi = take(F * d->ctrl_hidden);
@@ -295,49 +294,35 @@ WideLayout make_wide(const fcr_dims *d, int with_backward, int keep = 0) {
     L.tot = take(F * B);
     L.cmd = take(F * B);
     L.err = take(F * B);
-    L.X0 = take(F * kL * B * kIn);
-    L.Hs = take(F * kLayers * kL * B * H);
-    L.Cs = take(F * kLayers * kL * B * H);
-    L.G = take(F * B * 4 * H);
-    const size_t F16 = sizeof(_Float16), WW = 4 * H * H;
-    const bool hw = wide_fused_bwd_ok((int)H);
+    L.Hs = take(F * B * Hp);                               // fp32 h of the readout's cell (2, 9)
+    L.Cs = take(F * kLayers * kL * B * Hp);                // c of every cell of the current window
+    L.WR = take(F16 * kL * B * 2 * kWgRecX0);              // layer 0's window records
+    L.HR = take(F16 * 2 * kL * B * 2 * Hp);                // h records of two layers (layer l in slot l & 1)
     for (int l = 0; l < kLayers; ++l) {
-        L.fa[l] = take(l == 0 ? F16 * 4 * H * (3 * H + kX16) : F16 * WW * 6);
-        if (with_backward && hw) {
-            L.bt[l] = take(F16 * 2 * (l == 0 ? H : 2 * H) * 4 * H);
-        } else if (with_backward) {
-            if (l > 0) {
-                L.bih[l] = take(F16 * 6 * WW);   // [12H][2H]: W_ih | W_hh per split row (wide_split_bcat_kernel)
-            } else {
-                L.bx0 = take(F16 * 12 * H * (H + 8));
-            }
-        }
+        const size_t K = (l == 0 ? kWgRecX0 : Hp) + Hp;
+        L.fw[l] = take(F16 * 2 * 4 * Hp * K);
+        if (with_backward) L.bt[l] = take(F16 * 2 * (l == 0 ? Hp : 2 * Hp) * 4 * Hp);
     }
-    L.XB = take(F16 * kLayers * kL * B * 6 * H);
     if (with_backward) {
-        if (hw) {
-            L.DC2 = take(F * B * H);
-            L.RMc = take(F * 2 * B);
-            L.RMh = take(F * 4 * B);
-            L.RMd = take(F * 4 * kL * B);
-        } else {
-            L.dGsp = take(F16 * B * 12 * H);
-        }
-        L.E0 = take(F * B * ((H + 8 + 31) / 32 * 32));
-        L.consts = take(F * 4);
-        L.Act = take(F * kLayers * kL * B * 4 * H);
-        L.dH = take(F * B * H);
-        L.dC = take(F * B * H);
-        L.D[0] = take(F * kL * B * 2 * H);   // per t: [input gradient of the layer above | its dh_{t-1}]
-        L.D[1] = take(F * kL * B * 2 * H);
+        L.w0p = take(F * Hp * 4 * kIn);
+        L.Act = take(F * kLayers * kL * B * 4 * Hp);
+        L.dH = take(F * B * Hp);
+        L.dC = take(F * B * Hp);
+        L.DC2 = take(F * B * Hp);
+        L.D[0] = take(F * kL * B * 2 * Hp);   // per t: [input gradient of the layer above | its dh_{t-1}]
+        L.D[1] = take(F * kL * B * 2 * Hp);
+        L.E0 = take(F * B * Hp);              // layer 0's dh_{t-1}
+        L.RMc = take(F * 2 * B);              // [t & 1][B]            row bound of |dc|
+        L.RMh = take(F * 2 * L.ns * B);       // [t & 1][slot][B]      of |dh|, per column block of its writer
+        L.RMd = take(F * 2 * kL * L.ns * B);  // [l & 1][t][slot][B]   of |input gradient| for the layer below
         L.rowg = take(F * (N + kL - 1) * B * kIn);
         L.dv = take(F * B * N);
         L.ctrl_blocks = (int)(((long long)B * N + kCtrlItems - 1) / kCtrlItems);
         L.fnn_part = take(F * (size_t)L.ctrl_blocks * d->ctrl_hidden * 5);
         if (keep > 0) {
             L.keep = keep;
-            L.KA = take(F * (size_t)keep * kLayers * kL * B * 4 * H);
-            L.KC = take(F * (size_t)keep * kLayers * kL * B * H);
+            L.KA = take(F * (size_t)keep * kLayers * kL * B * 4 * Hp);
+            L.KC = take(F * (size_t)keep * kLayers * kL * B * Hp);
         }
     }
     L.total = off;
@@ -353,10 +338,10 @@ int wide_keep_fit(const fcr_dims *d, size_t ws_bytes) {
 }
 // a kept window's slabs (window j of the last L.keep)
 float *kept_act(const WideLayout &L, char *base, const fcr_dims *d, int j) {
-    return (float *)(base + L.KA) + (size_t)(j - (d->N - L.keep)) * kLayers * kL * d->B * 4 * d->H;
+    return (float *)(base + L.KA) + (size_t)(j - (d->N - L.keep)) * kLayers * kL * d->B * 4 * L.Hp;
 }
 float *kept_c(const WideLayout &L, char *base, const fcr_dims *d, int j) {
-    return (float *)(base + L.KC) + (size_t)(j - (d->N - L.keep)) * kLayers * kL * d->B * d->H;
+    return (float *)(base + L.KC) + (size_t)(j - (d->N - L.keep)) * kLayers * kL * d->B * L.Hp;
 }
 // fcr_set_wide_keep_budget: bytes of kept windows fcr_workspace_size may add; < 0 = the default policy
 // (wide_default_cap). The process-wide default of fcr_options.wide_keep_budget.
@@ -397,7 +382,7 @@ rocblas_handle blas_on(hipStream_t s) {
     if (!h) {
         if (rocblas_create_handle(&h) != rocblas_status_success) return nullptr;
         // no split-K solutions that sum through atomics: every GEMM here is run-to-run deterministic
-        // (the surrogate's and the wide path's gradients, and graph replays, repeat bit for bit)
+        // (the surrogate's gradients and graph replays repeat bit for bit)
         rocblas_set_atomics_mode(h, rocblas_atomics_not_allowed);
     }
     rocblas_set_stream(h, s);
@@ -419,94 +404,41 @@ int gemm_gw(rocblas_handle h, int B, int H4, int K, const float *W, const float 
     return st == rocblas_status_success ? FCR_OK : fail(FCR_EHIP, "rocblas_sgemm (backward) failed: %d", (int)st);
 }
 
-// G (row-major B x 4H) (+)= XB A^T on split-f16 operands, fp32 accumulate: A row-major [4H][lda] (the
-// forward A of fcr_wide.h), XB row-major [B][ldb]; K = the concatenated split length (3H per input part).
-int gemm16_fwd(rocblas_handle h, int B, int H4, int K, const _Float16 *A, int lda, const _Float16 *XB, int ldb,
-               float beta, float *G) {
-    const float one = 1.0f;
-    const rocblas_status st = rocblas_gemm_ex(h, rocblas_operation_transpose, rocblas_operation_none, H4, B, K, &one, A,
-                                              rocblas_datatype_f16_r, lda, XB, rocblas_datatype_f16_r, ldb, &beta, G,
-                                              rocblas_datatype_f32_r, H4, G, rocblas_datatype_f32_r, H4,
-                                              rocblas_datatype_f32_r, rocblas_gemm_algo_standard, 0, 0);
-    return st == rocblas_status_success ? FCR_OK : fail(FCR_EHIP, "rocblas_gemm_ex (forward, f16 split) failed: %d", (int)st);
-}
-// dX' (row-major B x n) = dGs A on split-f16 operands: A row-major [12H][lda] = [W_hi ; W_hi ; W_lo], dGs row-major
-// [B][12H] = [hi | lo | hi] of dG * scale. dX' stays in the scaled units: its consumer (wide_cell_bwd_kernel)
-// multiplies by 1/scale = consts[0] on load — the same single fp32 product a device-pointer alpha would apply,
-// without the per-call alpha/beta copies rocBLAS launches in device pointer mode.
-// n output columns of A (row-major [12H][lda]) into dX rows of stride ldc.
-int gemm16_bwd(rocblas_handle h, int B, int n, int H, const _Float16 *A, int lda, const _Float16 *dGs, float *dX, int ldc) {
-    const float one = 1.0f, zero = 0.0f;
-    const rocblas_status st = rocblas_gemm_ex(h, rocblas_operation_none, rocblas_operation_none, n, B, 12 * H, &one, A,
-                                              rocblas_datatype_f16_r, lda, dGs, rocblas_datatype_f16_r, 12 * H, &zero,
-                                              dX, rocblas_datatype_f32_r, ldc, dX, rocblas_datatype_f32_r, ldc,
-                                              rocblas_datatype_f32_r, rocblas_gemm_algo_standard, 0, 0);
-    return st == rocblas_status_success ? FCR_OK : fail(FCR_EHIP, "rocblas_gemm_ex (backward, f16 split) failed: %d", (int)st);
-}
-
-// Device pointers of the split-f16 operands (rollout only; the surrogate's training step stays fp32)
-struct WideSplit {
-    const _Float16 *fa[kLayers], *bih[kLayers], *bt[kLayers];
-    _Float16 *XB, *dGsp;
-    float *consts;
-    const _Float16 *bx0;
-    float *E0;
-};
-
-WideSplit wide_split(const WideLayout &L, char *base) {
-    WideSplit w{};
-    for (int l = 0; l < kLayers; ++l) {
-        w.fa[l] = (const _Float16 *)(base + L.fa[l]);
-        w.bih[l] = L.bih[l] ? (const _Float16 *)(base + L.bih[l]) : nullptr;
-        w.bt[l] = L.bt[l] ? (const _Float16 *)(base + L.bt[l]) : nullptr;
-    }
-    w.XB = (_Float16 *)(base + L.XB);
-    w.dGsp = L.dGsp ? (_Float16 *)(base + L.dGsp) : nullptr;
-    w.consts = L.consts ? (float *)(base + L.consts) : nullptr;
-    w.bx0 = L.bx0 ? (const _Float16 *)(base + L.bx0) : nullptr;
-    w.E0 = L.E0 ? (float *)(base + L.E0) : nullptr;
-    return w;
-}
-
-// Pack the split-f16 GEMM operands of the current weights (fcr_wide.h layouts)
-int wide_pack_split(const float *const *w_ih, const float *const *w_hh, int H, bool backward, const WideSplit &sp,
-                    const float *wsc, hipStream_t s) {
-    const size_t WW = (size_t)4 * H * H;
+// The rollout's per-call packs of the current weights: forward split weights per layer, the backward product's A
+// and W_ih0 (with_backward), the readout's fc.W, all at the padded Hp
+int wide_pack(const fcr_weights *w, int H, const WideLayout &L, bool backward, char *base, const float *wsc,
+              hipStream_t s) {
+    const int Hp = L.Hp;
     int rc;
+    auto grid = [](size_t n) { return dim3((unsigned)((n + 255) / 256)); };
     for (int l = 0; l < kLayers; ++l) {
-        const size_t n = l == 0 ? (size_t)4 * H * (3 * H + kX16) : WW * 6;
-        hipLaunchKernelGGL(wide_split_fa_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w_ih[l], w_hh[l], H,
-                           (int)(l == 0), wsc, (_Float16 *)sp.fa[l]);
-        if ((rc = launch_check("wide_split_fa_kernel"))) return rc;
+        const size_t K = (l == 0 ? kWgRecX0 : Hp) + Hp, n = (size_t)4 * Hp * K;
+        _Float16 *fw = (_Float16 *)(base + L.fw[l]);
+        hipLaunchKernelGGL(wide_split_fw_kernel, grid(n), dim3(256), 0, s, w->w_ih[l], w->w_hh[l], H, Hp, (int)(l == 0),
+                           wsc, fw, fw + n);
+        if ((rc = launch_check("wide_split_fw_kernel"))) return rc;
         if (!backward) continue;
-        if (sp.bt[l]) {   // fused backward cell: W^T split, [NO][4H] hi then lo, unit-major K
-            const int NO = l == 0 ? H : 2 * H;
-            const size_t nbt = (size_t)NO * 4 * H;
-            _Float16 *hi = (_Float16 *)sp.bt[l];
-            hipLaunchKernelGGL(wide_split_bt_kernel, dim3((unsigned)((nbt + 255) / 256)), dim3(256), 0, s,
-                               l == 0 ? (const float *)nullptr : w_ih[l], w_hh[l], H, NO, hi, hi + nbt);
-            if ((rc = launch_check("wide_split_bt_kernel"))) return rc;
-            continue;
-        }
-        if (l == 0) {
-            const size_t nb0 = (size_t)12 * H * (H + 8);
-            hipLaunchKernelGGL(wide_split_bx0_kernel, dim3((unsigned)((nb0 + 255) / 256)), dim3(256), 0, s, w_ih[0], w_hh[0],
-                               H, wsc, (_Float16 *)sp.bx0);
-            if ((rc = launch_check("wide_split_bx0_kernel"))) return rc;
-            continue;
-        }
-        hipLaunchKernelGGL(wide_split_bcat_kernel, dim3((unsigned)((6 * WW + 255) / 256)), dim3(256), 0, s, w_ih[l],
-                           w_hh[l], H, (_Float16 *)sp.bih[l]);
-        if ((rc = launch_check("wide_split_bcat_kernel"))) return rc;
+        const int NO = l == 0 ? Hp : 2 * Hp;
+        const size_t nbt = (size_t)NO * 4 * Hp;
+        _Float16 *bt = (_Float16 *)(base + L.bt[l]);
+        hipLaunchKernelGGL(wide_split_bt_kernel, grid(nbt), dim3(256), 0, s, l == 0 ? (const float *)nullptr : w->w_ih[l],
+                           w->w_hh[l], H, Hp, NO, bt, bt + nbt);
+        if ((rc = launch_check("wide_split_bt_kernel"))) return rc;
     }
-    return FCR_OK;
+    if (backward) {
+        hipLaunchKernelGGL(wide_pack_w0_kernel, grid((size_t)4 * Hp * kIn), dim3(256), 0, s, w->w_ih[0], H, Hp,
+                           (float *)(base + L.w0p));
+        if ((rc = launch_check("wide_pack_w0_kernel"))) return rc;
+    }
+    hipLaunchKernelGGL(wide_pad_fc_kernel, grid((size_t)kOut * Hp), dim3(256), 0, s, w->fc_w, H, Hp, (float *)(base + L.fcw));
+    return launch_check("wide_pad_fc_kernel");
 }
 
 WideArgs wide_args(const fcr_dims *d, const WideLayout &L, char *base) {
     WideArgs a{};
     a.B = d->B;
     a.N = d->N;
-    a.H = d->H;
+    a.H = L.Hp;   // every wide kernel runs at the padded size
     a.CH = d->ctrl_hidden;
     a.alpha = d->alpha;
     a.fcw = (const float *)(base + L.fcw);
@@ -518,58 +450,42 @@ WideArgs wide_args(const fcr_dims *d, const WideLayout &L, char *base) {
     a.tot = (float *)(base + L.tot);
     a.cmd = (float *)(base + L.cmd);
     a.err = (float *)(base + L.err);
-    a.X0 = (float *)(base + L.X0);
     a.Hs = (float *)(base + L.Hs);
     a.Cs = (float *)(base + L.Cs);
-    a.G = (float *)(base + L.G);
     a.Act = L.Act ? (float *)(base + L.Act) : nullptr;
     a.dH = L.dH ? (float *)(base + L.dH) : nullptr;
     a.dC = L.dC ? (float *)(base + L.dC) : nullptr;
     a.rowg = L.rowg ? (float *)(base + L.rowg) : nullptr;
     a.dv = L.dv ? (float *)(base + L.dv) : nullptr;
     a.wsc = (const float *)(base + L.wsc);
+    a.wr = (_Float16 *)(base + L.WR);
     return a;
 }
 
 // The cell kernels' vector width (fcr_wide.h): 16-B accesses when H % 4 == 0, 8-B when H is even.
 int cell_vec(int H) { return H % 4 == 0 ? 4 : (H % 2 == 0 ? 2 : 1); }
 
+// the surrogate's fp32 cell update (fcr_wide.h wide_cell_kernel)
 int launch_cell(int B, int H, hipStream_t s, const float *G, const float *c_prev, float *c_out, float *h_out,
-                float *act, _Float16 *xb_h, int sh, _Float16 *xb_x, int sx) {
+                float *act) {
     const int V = cell_vec(H);
     const dim3 grid((unsigned)(((size_t)B * (H / V) + 255) / 256)), blk(256);
-    if (V == 4)
-        hipLaunchKernelGGL(wide_cell_kernel<4>, grid, blk, 0, s, G, c_prev, c_out, h_out, act, xb_h, sh, xb_x, sx, B, H);
-    else if (V == 2)
-        hipLaunchKernelGGL(wide_cell_kernel<2>, grid, blk, 0, s, G, c_prev, c_out, h_out, act, xb_h, sh, xb_x, sx, B, H);
-    else
-        hipLaunchKernelGGL(wide_cell_kernel<1>, grid, blk, 0, s, G, c_prev, c_out, h_out, act, xb_h, sh, xb_x, sx, B, H);
+    if (V == 4) hipLaunchKernelGGL(wide_cell_kernel<4>, grid, blk, 0, s, G, c_prev, c_out, h_out, act, B, H);
+    else if (V == 2) hipLaunchKernelGGL(wide_cell_kernel<2>, grid, blk, 0, s, G, c_prev, c_out, h_out, act, B, H);
+    else hipLaunchKernelGGL(wide_cell_kernel<1>, grid, blk, 0, s, G, c_prev, c_out, h_out, act, B, H);
     return launch_check("wide_cell_kernel");
 }
 
-// trajectories per thread of layer 0's backward cell kernel (1, 4 and 8 measured within 2 ms at config 5, round 2f)
-constexpr int kRowgT = 4;
-template <bool PRE>
-int launch_cell_bwd(int B, int H, hipStream_t s, const float *act, const float *c, const float *c_prev,
-                    const float *dH, const float *din, float *dC, float *dG, _Float16 *dgsp, const float *consts,
-                    int dh_scaled, int ldh, int ldx, const float *wih0 = nullptr, float *rowg = nullptr, int dg3 = 1) {
+// the surrogate's fp32 backward cell (fcr_wide.h wide_cell_bwd_kernel)
+int launch_cell_bwd(int B, int H, hipStream_t s, const float *act, const float *c, const float *c_prev, const float *dH,
+                    const float *din, float *dC, float *dG) {
     const int V = cell_vec(H);
     const dim3 grid((unsigned)(((size_t)B * (H / V) + 255) / 256)), blk(256);
-    if (rowg && (V != 4 || 64 % (H / V)))
-        return fail(FCR_EINVAL, "wide_cell_bwd_kernel: in-kernel row gradient needs 64 %% (H / 4) == 0 (H = %d)", H);
-    if (rowg) {   // layer 0: kRowgT trajectories per thread share one load of its W_ih0 rows
-        const dim3 g0((unsigned)(((size_t)(B + kRowgT - 1) / kRowgT * (H / V) + 255) / 256));
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4, kRowgT>), g0, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, dg3, wih0, rowg);
-    } else if (V == 4)
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, dg3);
-    else if (V == 2)
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 2>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, dg3);
-    else
-        hipLaunchKernelGGL((wide_cell_bwd_kernel<PRE, 1>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, dgsp, consts, dh_scaled, ldh, ldx, B, H, dg3);
+    if (V == 4) hipLaunchKernelGGL((wide_cell_bwd_kernel<4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, B, H);
+    else if (V == 2) hipLaunchKernelGGL((wide_cell_bwd_kernel<2>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, B, H);
+    else hipLaunchKernelGGL((wide_cell_bwd_kernel<1>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, B, H);
     return launch_check("wide_cell_bwd_kernel");
 }
-// the in-kernel layer-0 row gradient applies when a trajectory's cell threads (H / 4) tile a wave
-inline bool rowg_in_cell(int H) { return cell_vec(H) == 4 && 64 % (H / 4) == 0; }
 
 // The per-call weight packs (pack_fwd16_item, pack_img_item, pack_misc_item) as jobs of one launch:
 // block ranges in job order, 256 threads each, the same items the separate kernels ran
@@ -593,33 +509,36 @@ __global__ __launch_bounds__(256) void pack_all_kernel(PackAllArgs p) {
     else pack_misc_item(p.a, idx);
 }
 
-// The split path's forward cells (every layer, H % 64 == 0): the cell's GEMM and update as one hand-written
-// kernel (fcr_wgemm.h): 262 us per cell against ~300 us for rocBLAS's GEMM + wide_cell_kernel (B = 65 536,
-// H = 256; DESIGN.md "Config 5"); rocBLAS gemm16_fwd + wide_cell_kernel for other H.
-bool wide_fused_ok(int H) { return H % kWgU == 0; }
+// One forward cell of the wide path: the cell's split-f16 GEMM and update as one hand-written kernel (fcr_wgemm.h)
 int launch_wgemm_cell(const WgArgs &wa, hipStream_t s) {
     static std::atomic<unsigned long long> attr_done{0};
-    if (const int rc = lds_attr((const void *)wide_gemm_cell_kernel, kWgLds, attr_done, "wgemm")) return rc;
-    if (wa.K <= 0 || wa.K % kWgK || wa.lda % 8 || wa.ldb % 8 || wa.H % kWgU || wa.B <= 0)
-        return fail(FCR_EINVAL, "wide_gemm_cell_kernel: K %d lda %d ldb %d H %d B %d off its tiling", wa.K, wa.lda, wa.ldb,
-                    wa.H, wa.B);
+    if (const int rc = lds_attr((const void *)wide_cell_fwd_kernel, kWgLds, attr_done, "wgemm")) return rc;
+    if (wa.H % kWgU || wa.kx % kWgK || wa.K != wa.kx + wa.H || wa.B <= 0 || !wa.W || !wa.xr || !wa.c_out || !wa.h_rec)
+        return fail(FCR_EINVAL, "wide_cell_fwd_kernel: K %d kx %d H %d B %d off its tiling", wa.K, wa.kx, wa.H, wa.B);
     const int nx = (wa.B + kWgN - 1) / kWgN, ny = wa.H / kWgU;
-    hipLaunchKernelGGL(wide_gemm_cell_kernel, dim3((unsigned)(nx * ny)), dim3(kWgThreads), kWgLds, s, wa);
-    return launch_check("wide_gemm_cell_kernel");
+    hipLaunchKernelGGL(wide_cell_fwd_kernel, dim3((unsigned)(nx * ny)), dim3(kWgThreads), kWgLds, s, wa);
+    return launch_check("wide_cell_fwd_kernel");
 }
 
 // One backward cell of the fused path (fcr_wbwd.h): dgates formed in the product's prologue, out = dG [W_ih | W_hh]
 // (columns [0, NO), NO = 0: the dgate part only) in true units
 int launch_fb(const WbArgs &wa, bool l0, hipStream_t s) {
-    static std::atomic<unsigned long long> attr_done[2] = {{0}, {0}};
-    const void *fn = l0 ? (const void *)wide_bwd_fused_kernel<true> : (const void *)wide_bwd_fused_kernel<false>;
-    if (const int rc = lds_attr(fn, kWbLds, attr_done[l0], "wbwd")) return rc;
-    if (wa.NO < 0 || wa.NO > 2 * kWbM || wa.NO % 4 || wa.H % 8 || wa.H > kWbMaxH || wa.NB <= 0 || wa.ldo % 4 ||
-        wa.ldh % 4 || wa.ldx % 4 || (l0 && (!wa.wih0 || !wa.rowg)))
+    static std::atomic<unsigned long long> attr_done[3] = {{0}, {0}, {0}};
+    const bool w0g = l0 && wa.H > kWbW0LdsUnits;
+    const int kind = l0 ? (w0g ? 2 : 1) : 0;
+    const void *fn = kind == 0 ? (const void *)wide_bwd_fused_kernel<false>
+                     : kind == 1 ? (const void *)wide_bwd_fused_kernel<true, false>
+                                 : (const void *)wide_bwd_fused_kernel<true, true>;
+    if (const int rc = lds_attr(fn, kWbLds, attr_done[kind], "wbwd")) return rc;
+    if (wa.NO < 0 || wa.NO > 2 * wa.H || wa.NO % 4 || wa.H % 8 || wa.NB <= 0 || wa.ldo % 4 || wa.ldh % 4 ||
+        wa.ldx % 4 || wa.nrh < 1 || (wa.rm_d && wa.nrd < 1) || (l0 && (!wa.wih0 || !wa.rowg)))
         return fail(FCR_EINVAL, "wide_bwd_fused_kernel: NO %d H %d B %d ldo %d off its tiling", wa.NO, wa.H, wa.NB, wa.ldo);
     const int nx = (wa.NB + kWbN - 1) / kWbN, ny = wa.NO > 0 ? (wa.NO + kWbM - 1) / kWbM : 1;
-    if (l0) hipLaunchKernelGGL((wide_bwd_fused_kernel<true>), dim3((unsigned)(nx * ny)), dim3(kWbThreads), kWbLds, s, wa);
-    else hipLaunchKernelGGL((wide_bwd_fused_kernel<false>), dim3((unsigned)(nx * ny)), dim3(kWbThreads), kWbLds, s, wa);
+    const int lds = wb_lds_bytes(l0, wa.H);
+    if (kind == 0) hipLaunchKernelGGL((wide_bwd_fused_kernel<false>), dim3((unsigned)(nx * ny)), dim3(kWbThreads), lds, s, wa);
+    else if (kind == 1)
+        hipLaunchKernelGGL((wide_bwd_fused_kernel<true, false>), dim3((unsigned)(nx * ny)), dim3(kWbThreads), lds, s, wa);
+    else hipLaunchKernelGGL((wide_bwd_fused_kernel<true, true>), dim3((unsigned)(nx * ny)), dim3(kWbThreads), lds, s, wa);
     return launch_check("wide_bwd_fused_kernel");
 }
 
@@ -638,19 +557,21 @@ __global__ __launch_bounds__(256) void row_absmax_kernel(const float *__restrict
 
 // fcr_wide_bwd_cell (test hook): the scratch of one standalone fused backward cell
 struct CellHookLayout {
-    size_t bt, rm, total;
+    size_t bt, w0, rm, total;
 };
 CellHookLayout cell_hook_layout(int B, int H, int layer0) {
     CellHookLayout L{};
     const size_t NP = layer0 ? H : 2 * (size_t)H;
     L.bt = 0;
-    L.rm = align_up(sizeof(_Float16) * 2 * NP * 4 * H);
-    L.total = L.rm + align_up(sizeof(float) * 5 * (size_t)B);   // rm_c [B], rm_h [2][B], rm_d [2][B]
+    L.w0 = align_up(sizeof(_Float16) * 2 * NP * 4 * H);
+    L.rm = L.w0 + align_up(sizeof(float) * 4 * H * kIn);
+    L.total = L.rm + align_up(sizeof(float) * 3 * (size_t)B);   // rm_c [B], rm_h [1][B], rm_d [1][B]
     return L;
 }
 int cell_hook_check(int B, int H) {
     if (B < 1) return fail(FCR_EINVAL, "fcr_wide_bwd_cell: B=%d", B);
-    if (!wide_fused_bwd_ok(H)) return fail(FCR_EUNSUPPORTED, "fcr_wide_bwd_cell: H=%d off the fused cell's tiling", H);
+    if (H < 8 || H % 8 || H > kMaxWideH)
+        return fail(FCR_EUNSUPPORTED, "fcr_wide_bwd_cell: H=%d off the fused cell's tiling (a multiple of 8)", H);
     return FCR_OK;
 }
 
@@ -664,12 +585,17 @@ int wide_bwd_cell_hook(int B, int H, int layer0, const float *w_ih, const float 
     const size_t nbt = (size_t)NP * 4 * H;
     _Float16 *bt = (_Float16 *)(base + L.bt);
     hipLaunchKernelGGL(wide_split_bt_kernel, dim3((unsigned)((nbt + 255) / 256)), dim3(256), 0, s,
-                       layer0 ? (const float *)nullptr : w_ih, w_hh, H, NP, bt, bt + nbt);
+                       layer0 ? (const float *)nullptr : w_ih, w_hh, H, H, NP, bt, bt + nbt);
     int rc = launch_check("wide_split_bt_kernel");
     if (rc) return rc;
+    float *w0 = (float *)(base + L.w0);
+    if (layer0) {
+        hipLaunchKernelGGL(wide_pack_w0_kernel, dim3((unsigned)((4 * H * kIn + 255) / 256)), dim3(256), 0, s, w_ih, H, H,
+                           w0);
+        if ((rc = launch_check("wide_pack_w0_kernel"))) return rc;
+    }
     float *rm = (float *)(base + L.rm);
-    float *rm_c = rm, *rm_h = rm + B, *rm_d = rm + 3 * (size_t)B;
-    if (hipMemsetAsync(rm, 0, sizeof(float) * 5 * (size_t)B, s) != hipSuccess) return fail(FCR_EHIP, "hipMemsetAsync failed");
+    float *rm_c = rm, *rm_h = rm + B, *rm_d = rm + 2 * (size_t)B;
     const dim3 rg((unsigned)((B + 3) / 4)), rb(256);
     hipLaunchKernelGGL(row_absmax_kernel, rg, rb, 0, s, dc, H, H, B, rm_c);
     hipLaunchKernelGGL(row_absmax_kernel, rg, rb, 0, s, dh, H, H, B, rm_h);
@@ -691,6 +617,8 @@ int wide_bwd_cell_hook(int B, int H, int layer0, const float *w_ih, const float 
     wa.rm_c = rm_c;
     wa.rm_h = rm_h;
     wa.rm_d = din ? rm_d : nullptr;
+    wa.nrh = 1;
+    wa.nrd = 1;
     wa.out = out;
     if (!layer0) {   // [input gradient | dh_{t-1}] (t = 0, no c_prev: the former only)
         wa.ldo = 2 * H;
@@ -706,76 +634,38 @@ int wide_bwd_cell_hook(int B, int H, int layer0, const float *w_ih, const float 
         wa.h0 = 0;
         wa.h1 = H;
         wa.d1 = 0;
-        wa.wih0 = w_ih;
+        wa.wih0 = w0;
         wa.rowg = rowg;
     }
     return launch_fb(wa, layer0 != 0, s);
 }
 
-// One window's cells, forward: 3 layers x 10 steps of [GEMM x_t W_ih^T, GEMM h_{t-1} W_hh^T, cell].
-// sp != nullptr (the rollout): the H-wide products as ONE K-concatenated split-f16 GEMM per cell (gemm16_fwd) — ~3x the fp32
-// GEMM rate at equal accuracy; sp == nullptr (the surrogate's training step): fp32 rocBLAS throughout.
-int wide_cells(rocblas_handle h, const WideArgs &a, const float *const *w_ih, const float *const *w_hh, bool keep_act,
-               const WideSplit *sp, hipStream_t s) {
-    const int B = a.B, H = a.H;
-    const size_t cell = (size_t)B * H;
-    // operand rows of cell (l, t): layer >= 1 [x part 3H | h part 3H], layer 0 [h part 3H]
-    auto ldx = [&](int l) { return l == 0 ? xb0_ld(H) : 6 * H; };
-    auto xb = [&](int l, int t) { return sp->XB + ((size_t)l * kL + t) * B * 6 * H; };
+// One window's 30 cells, forward (the rollout, and the backward's recompute of a window that was not kept): layer by
+// layer, t = 0..9, each cell one wide_cell_fwd_kernel launch. keep_act: the cells' gate pre-activations into `Act`
+// (the backward rebuilds i, f, g, o from them).
+int wide_cells(const WideArgs &a, const WideLayout &L, char *base, bool keep_act, hipStream_t s) {
+    const int B = a.B, Hp = L.Hp;
+    const size_t cell = (size_t)B * Hp;
+    _Float16 *HR = (_Float16 *)(base + L.HR);
+    auto rec = [&](int l, int t) { return HR + ((size_t)(l & 1) * kL + t) * B * 2 * Hp; };   // h record of cell (l, t)
     int rc;
     for (int l = 0; l < kLayers; ++l) {
-        const float *wih = w_ih[l], *whh = w_hh[l];
+        const size_t K = (l == 0 ? kWgRecX0 : Hp) + Hp;
         for (int t = 0; t < kL; ++t) {
-            const float *x = l == 0 ? a.X0 + (size_t)t * B * kIn : a.Hs + ((size_t)(l - 1) * kL + t) * cell;
-            // split path with keep_act (the backward's recompute): the gate pre-activations stay per cell in
-            // the Act slab (wide_cell_bwd_kernel<true> rebuilds the activations) instead of a second array
-            float *G = (sp && keep_act) ? a.Act + ((size_t)l * kL + t) * cell * 4 : a.G;
-            if (sp && wide_fused_ok(H)) {   // GEMM + cell update in one kernel
-                // layer 0: [h part 3H | window-row part kX16], t = 0 without the h part
-                const int k0 = (l == 0 && t == 0) ? 3 * H : 0;
-                WgArgs wa{};
-                wa.A = sp->fa[l] + k0;
-                wa.XB = xb(l, t) + k0;
-                wa.lda = l == 0 ? 3 * H + kX16 : 6 * H;
-                wa.ldb = ldx(l);
-                wa.K = l == 0 ? 3 * H + kX16 - k0 : t > 0 ? 6 * H : 3 * H;
-                wa.B = B;
-                wa.H = H;
-                wa.c_prev = t > 0 ? a.Cs + ((size_t)l * kL + t - 1) * cell : nullptr;
-                wa.c_out = a.Cs + ((size_t)l * kL + t) * cell;
-                wa.h_out = (l == kLayers - 1 && t == kL - 1) ? a.Hs + ((size_t)l * kL + t) * cell : nullptr;
-                wa.preact = keep_act ? G : nullptr;
-                wa.xb_h = t + 1 < kL ? xb(l, t + 1) + (l == 0 ? 0 : 3 * H) : nullptr;
-                wa.sh = ldx(l);
-                wa.xb_x = l + 1 < kLayers ? xb(l + 1, t) : nullptr;
-                wa.sx = ldx(l + 1 < kLayers ? l + 1 : l);
-                if ((rc = launch_wgemm_cell(wa, s))) return rc;
-                continue;
-            }
-            if (sp) {
-                if (l == 0) {   // [h part | window-row part] (wide_window_kernel writes the latter); t = 0: no h
-                    const int k0 = t > 0 ? 0 : 3 * H;
-                    if ((rc = gemm16_fwd(h, B, 4 * H, 3 * H + kX16 - k0, sp->fa[0] + k0, 3 * H + kX16, xb(0, t) + k0, ldx(0),
-                                         0.0f, G)))
-                        return rc;
-                } else if ((rc = gemm16_fwd(h, B, 4 * H, t > 0 ? 6 * H : 3 * H, sp->fa[l], 6 * H, xb(l, t), 6 * H, 0.0f,
-                                            G))) {
-                    return rc;
-                }
-            } else {
-                if ((rc = gemm_xwt(h, B, 4 * H, l == 0 ? kIn : H, wih, x, 0.0f, a.G))) return rc;
-                if (t > 0 && (rc = gemm_xwt(h, B, 4 * H, H, whh, a.Hs + ((size_t)l * kL + t - 1) * cell, 1.0f, a.G)))
-                    return rc;
-            }
-            _Float16 *xh = (sp && t + 1 < kL) ? xb(l, t + 1) + (l == 0 ? 0 : 3 * H) : nullptr;   // next cell's h part
-            _Float16 *xx = (sp && l + 1 < kLayers) ? xb(l + 1, t) : nullptr;                       // layer above's x part
-            // the split path reads h only through the operand rows; fp32 h is kept for the readout (2, 9)
-            float *hout = (!sp || (l == kLayers - 1 && t == kL - 1)) ? a.Hs + ((size_t)l * kL + t) * cell : nullptr;
-            if ((rc = launch_cell(B, H, s, G, t > 0 ? (const float *)(a.Cs + ((size_t)l * kL + t - 1) * cell) : nullptr,
-                                  a.Cs + ((size_t)l * kL + t) * cell, hout,
-                                  (keep_act && !sp) ? a.Act + ((size_t)l * kL + t) * cell * 4 : nullptr, xh, ldx(l), xx,
-                                  ldx(l + 1 < kLayers ? l + 1 : l))))
-                return rc;
+            WgArgs wa{};
+            wa.W = (const _Float16 *)(base + L.fw[l]);
+            wa.K = (int)K;
+            wa.kx = l == 0 ? kWgRecX0 : Hp;
+            wa.xr = l == 0 ? a.wr + (size_t)t * B * 2 * kWgRecX0 : rec(l - 1, t);
+            wa.hr = t > 0 ? rec(l, t - 1) : nullptr;
+            wa.B = B;
+            wa.H = Hp;
+            wa.c_prev = t > 0 ? a.Cs + ((size_t)l * kL + t - 1) * cell : nullptr;
+            wa.c_out = a.Cs + ((size_t)l * kL + t) * cell;
+            wa.h_out = (l == kLayers - 1 && t == kL - 1) ? a.Hs : nullptr;
+            wa.preact = keep_act ? a.Act + ((size_t)l * kL + t) * cell * 4 : nullptr;
+            wa.h_rec = rec(l, t);
+            if ((rc = launch_wgemm_cell(wa, s))) return rc;
         }
     }
     return FCR_OK;
@@ -785,24 +675,20 @@ int wide_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const 
                  const float *noise, float *loss, float *cost, float *command, float *error, float *prediction,
                  float *xhat, int with_backward, char *base, size_t ws_bytes, hipStream_t s) {
     const WideLayout L = make_wide(d, with_backward, with_backward ? wide_keep_fit(d, ws_bytes) : 0);
-    const size_t H = d->H, F = sizeof(float);
+    const size_t F = sizeof(float);
     int rc;
     // private copies of every parameter the backward needs (fcr_backward takes no weights)
     auto cp = [&](size_t off, const float *src, size_t n) {
         return hipMemcpyAsync(base + off, src, n * F, hipMemcpyDeviceToDevice, s);
     };
-    for (int l = 0; l < kLayers; ++l) {
-        if (cp(L.wih[l], w->w_ih[l], 4 * H * (l == 0 ? kIn : H)) || cp(L.whh[l], w->w_hh[l], 4 * H * H))
-            return fail(FCR_EHIP, "hipMemcpyAsync (weights) failed");
-    }
-    if (cp(L.fcw, w->fc_w, kOut * H) || cp(L.fcb, w->fc_b, kOut) || cp(L.cwi, w->ctrl_w_inp, d->ctrl_hidden * kCtrlIn) ||
+    if (cp(L.fcb, w->fc_b, kOut) || cp(L.cwi, w->ctrl_w_inp, d->ctrl_hidden * kCtrlIn) ||
         cp(L.cbi, w->ctrl_b_inp, d->ctrl_hidden) || cp(L.cwo, w->ctrl_w_out, d->ctrl_hidden))
         return fail(FCR_EHIP, "hipMemcpyAsync (parameters) failed");
     PackArgs pa{};   // controller records for ctrl_grad_kernel (the fc part is unused on this path)
     pa.H = kMaxSlots * 4;
     pa.HS = kMaxSlots;
     pa.CH = d->ctrl_hidden;
-    pa.fcw = (const float *)(base + L.fcw);   // read only for units < 52 <= H: in bounds
+    pa.fcw = w->fc_w;   // read only for units < 52 < H: in bounds
     pa.fcb = w->fc_b;
     pa.cwi = w->ctrl_w_inp;
     pa.cbi = w->ctrl_b_inp;
@@ -812,26 +698,15 @@ int wide_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const 
     pa.fnp = (float *)(base + L.fnp);
     hipLaunchKernelGGL(pack_misc_kernel, dim3(2), dim3(256), 0, s, pa);
     if ((rc = launch_check("pack_misc_kernel"))) return rc;
-
-    const WideSplit sp = wide_split(L, base);
     if ((rc = launch_range(d, states, u0, noise, w->fc_w, w->fc_b, (float *)(base + L.rng), (float *)(base + L.wsc), s)))
         return rc;
-    if ((rc = wide_pack_split(w->w_ih, w->w_hh, (int)H, with_backward != 0, sp, (const float *)(base + L.wsc), s)))
-        return rc;
-    rocblas_handle h = blas_on(s);
-    if (!h) return fail(FCR_EHIP, "rocblas_create_handle failed");
+    if ((rc = wide_pack(w, d->H, L, with_backward != 0, base, (const float *)(base + L.wsc), s))) return rc;
     WideArgs a = wide_args(d, L, base);
-    a.xb0 = sp.XB;
     a.X = X;
     a.u0 = u0;
     a.states = states;
     a.noise = noise;
     a.pred = prediction;
-    const float *wih[kLayers], *whh[kLayers];
-    for (int l = 0; l < kLayers; ++l) {
-        wih[l] = (const float *)(base + L.wih[l]);
-        whh[l] = (const float *)(base + L.whh[l]);
-    }
     const int nb = (d->B + 255) / 256;
     for (int j = 0; j < d->N; ++j) {
         hipLaunchKernelGGL(wide_window_kernel<true>, dim3(nb), dim3(256), 0, s, a, j);
@@ -840,12 +715,12 @@ int wide_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const 
             WideArgs ak = a;
             ak.Act = kept_act(L, base, d, j);
             ak.Cs = kept_c(L, base, d, j);
-            if ((rc = wide_cells(h, ak, wih, whh, true, &sp, s))) return rc;
-        } else if ((rc = wide_cells(h, a, wih, whh, false, &sp, s))) {
+            if ((rc = wide_cells(ak, L, base, true, s))) return rc;
+        } else if ((rc = wide_cells(a, L, base, false, s))) {
             return rc;
         }
         hipLaunchKernelGGL(wide_readout_kernel, dim3((unsigned)(((size_t)d->B * kRoLanes + 255) / 256)), dim3(256), 0, s, a, j,
-                           (const float *)(a.Hs + ((size_t)2 * kL + kL - 1) * d->B * H));
+                           (const float *)a.Hs);
         if ((rc = launch_check("wide_readout_kernel"))) return rc;
     }
     hipLaunchKernelGGL(wide_finish_kernel, dim3(nb), dim3(256), 0, s, a, cost, command, error, xhat);
@@ -858,40 +733,26 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
                   const float *dloss, float *g_u0, float *g_w_inp, float *g_b_inp, float *g_w_out, char *base,
                   size_t ws_bytes, hipStream_t s) {
     const WideLayout L = make_wide(d, 1, wide_keep_fit(d, ws_bytes));
-    const int B = d->B, H = d->H, H8 = H + 8;
-    const int LE = (H8 + 31) / 32 * 32;   // E0 rows padded to whole 128-B lines
-    const size_t cell = (size_t)B * H;
+    const int B = d->B, Hp = L.Hp, ns = L.ns, nd = wide_dslots(Hp);
+    const size_t cell = (size_t)B * Hp;
     const int nb = (B + 255) / 256;
     int rc;
-    rocblas_handle h = blas_on(s);
-    if (!h) return fail(FCR_EHIP, "rocblas_create_handle failed");
     WideArgs a = wide_args(d, L, base);
     a.X = X;
     a.states = states;
     a.pred = (float *)prediction;
     a.dloss = dloss;
     float *D[2] = {(float *)(base + L.D[0]), (float *)(base + L.D[1])};
-    const float *wih[kLayers], *whh[kLayers];
-    for (int l = 0; l < kLayers; ++l) {
-        wih[l] = (const float *)(base + L.wih[l]);
-        whh[l] = (const float *)(base + L.whh[l]);
-    }
+    float *E0 = (float *)(base + L.E0);
     if (hipMemsetAsync(a.rowg, 0, sizeof(float) * (size_t)(d->N + kL - 1) * B * kIn, s) != hipSuccess)
         return fail(FCR_EHIP, "hipMemsetAsync failed");
-    const WideSplit sp = wide_split(L, base);
-    a.xb0 = sp.XB;
-    int kexp = 0;   // 2^kexp ~ B N: the dgates' scale into the f16 range (wide_bscale_kernel)
-    while (kexp < 60 && (1LL << kexp) < (long long)B * d->N) ++kexp;
-    hipLaunchKernelGGL(wide_bscale_kernel, dim3(1), dim3(64), 0, s, dloss, kexp, sp.consts);
-    if ((rc = launch_check("wide_bscale_kernel"))) return rc;
-    const bool fused = sp.bt[0] != nullptr;   // wide_fused_bwd_ok: each backward cell one fcr_wbwd.h kernel
-    float *DC[2] = {a.dC, fused ? (float *)(base + L.DC2) : nullptr};
-    float *RMc = fused ? (float *)(base + L.RMc) : nullptr;   // [t & 1][B]      row bound of |dc|
-    float *RMh = fused ? (float *)(base + L.RMh) : nullptr;   // [t & 1][2][B]   of |dh| (per column block)
-    float *RMd = fused ? (float *)(base + L.RMd) : nullptr;   // [l & 1][t][2][B] of |input grad| for the layer below
+    float *DC[2] = {a.dC, (float *)(base + L.DC2)};
+    float *RMc = (float *)(base + L.RMc);
+    float *RMh = (float *)(base + L.RMh);
+    float *RMd = (float *)(base + L.RMd);
     for (int j = d->N - 1; j >= 0; --j) {
         hipLaunchKernelGGL(wide_head_kernel, dim3((unsigned)(((size_t)B * kRoLanes + 255) / 256)), dim3(256), 0, s, a, j,
-                           RMh);   // layer 2's t = 9 reads slot (9 + 1) & 1 = 0
+                           RMh);   // slot 0 of parity (9 + 1) & 1 = 0: layer 2's t = 9 reads it
         if ((rc = launch_check("wide_head_kernel"))) return rc;
         if (j >= d->N - L.keep) {   // kept by the forward: no recompute
             a.Act = kept_act(L, base, d, j);
@@ -901,86 +762,61 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
             a.Cs = (float *)(base + L.Cs);
             hipLaunchKernelGGL(wide_window_kernel<false>, dim3(nb), dim3(256), 0, s, a, j);
             if ((rc = launch_check("wide_window_kernel"))) return rc;
-            if ((rc = wide_cells(h, a, wih, whh, true, &sp, s))) return rc;   // checkpoint: recompute the window
+            if ((rc = wide_cells(a, L, base, true, s))) return rc;   // checkpoint: recompute the window
         }
         for (int l = kLayers - 1; l >= 0; --l) {
             if (l < kLayers - 1 && hipMemsetAsync(a.dH, 0, sizeof(float) * cell, s) != hipSuccess)
                 return fail(FCR_EHIP, "hipMemsetAsync failed");
-            if (hipMemsetAsync(DC[0], 0, sizeof(float) * cell, s) != hipSuccess) return fail(FCR_EHIP, "hipMemsetAsync failed");
-            if (fused && (hipMemsetAsync(RMc, 0, sizeof(float) * B, s) != hipSuccess ||
-                          (l < kLayers - 1 && hipMemsetAsync(RMh, 0, sizeof(float) * 2 * B, s) != hipSuccess)))
+            if (hipMemsetAsync(DC[0], 0, sizeof(float) * cell, s) != hipSuccess ||
+                hipMemsetAsync(RMc, 0, sizeof(float) * B, s) != hipSuccess ||
+                (l < kLayers - 1 && hipMemsetAsync(RMh, 0, sizeof(float) * B, s) != hipSuccess))
                 return fail(FCR_EHIP, "hipMemsetAsync failed");
             for (int t = kL - 1; t >= 0; --t) {
                 const size_t c_off = ((size_t)l * kL + t) * cell;
-                // dh_t below t = 9 comes from cell t+1's combined product: layer 0 columns 0..H-1 of E0, layers
-                // >= 1 columns H..2H-1 of D[l-1] row t+1; the layer above's input gradient from D[l] row t
-                const float *dh_src = t == kL - 1 ? a.dH : l == 0 ? sp.E0 : D[l - 1] + (size_t)(t + 1) * 2 * cell + H;
-                const int ldh = t == kL - 1 ? H : l == 0 ? LE : 2 * H;
-                if (fused) {
-                    const int NP = l == 0 ? H : 2 * H;
-                    WbArgs wa{};
-                    wa.Ahi = sp.bt[l];
-                    wa.Alo = sp.bt[l] + (size_t)NP * 4 * H;
-                    wa.NB = B;
-                    wa.H = H;
-                    wa.pre = a.Act + c_off * 4;
-                    wa.c_prev = t > 0 ? a.Cs + c_off - cell : nullptr;
-                    wa.dh = dh_src;
-                    wa.ldh = ldh;
-                    wa.din = l < kLayers - 1 ? D[l] + (size_t)t * 2 * cell : nullptr;
-                    wa.ldx = 2 * H;
-                    wa.dC = DC[(t + 1) & 1];   // t = 9 reads buffer 0 (zeroed above), t writes buffer t & 1
-                    wa.dC_out = DC[t & 1];
-                    wa.rm_c = RMc + (size_t)((t + 1) & 1) * B;
-                    wa.rm_c_out = t > 0 ? RMc + (size_t)(t & 1) * B : nullptr;
-                    wa.rm_h = RMh + (size_t)((t + 1) & 1) * 2 * B;
-                    wa.rm_h_out = t > 0 ? RMh + (size_t)(t & 1) * 2 * B : nullptr;
-                    wa.rm_d = l < kLayers - 1 ? RMd + ((size_t)((l + 1) & 1) * kL + t) * 2 * B : nullptr;
-                    wa.rm_d_out = l > 0 ? RMd + ((size_t)(l & 1) * kL + t) * 2 * B : nullptr;
-                    if (l > 0) {   // [input gradient | dh_{t-1}] (t = 0: the former only) into D[l-1] row t
-                        wa.out = D[l - 1] + (size_t)t * 2 * cell;
-                        wa.ldo = 2 * H;
-                        wa.NO = t > 0 ? 2 * H : H;
-                        wa.h0 = H;
-                        wa.h1 = t > 0 ? 2 * H : H;
-                        wa.d1 = H;
-                    } else {       // dh_{t-1} into E0 (t = 0: none), and the window-row gradient into rowg row j + t
-                        wa.out = sp.E0;
-                        wa.ldo = LE;
-                        wa.NO = t > 0 ? H : 0;
-                        wa.h0 = 0;
-                        wa.h1 = H;
-                        wa.d1 = 0;
-                        wa.wih0 = wih[0];
-                        wa.rowg = a.rowg + (size_t)(j + t) * B * kIn;
-                    }
-                    if ((rc = launch_fb(wa, l == 0, s))) return rc;
-                    continue;
-                }
-                const bool rg = l == 0 && rowg_in_cell(H);   // layer 0's row gradient from the cell kernel
-                if ((rc = launch_cell_bwd<true>(B, H, s, a.Act + c_off * 4, a.Cs + c_off, t > 0 ? a.Cs + c_off - cell : nullptr,
-                                                dh_src, l < kLayers - 1 ? D[l] + (size_t)t * 2 * cell : nullptr, a.dC,
-                                                nullptr, sp.dGsp, sp.consts,
-                                                l < kLayers - 1 || t < kL - 1,   // (2, 9): the head's dH
-                                                ldh, 2 * H, rg ? wih[0] : nullptr,
-                                                rg ? a.rowg + (size_t)(j + t) * B * kIn : nullptr, 1)))
-                    return rc;
+                // dh_t below t = 9 comes from cell t+1's product: layer 0 columns 0..Hp-1 of E0, layers >= 1 columns
+                // Hp..2Hp-1 of D[l-1] row t+1; the layer above's input gradient from D[l] row t
+                const float *dh_src = t == kL - 1 ? a.dH : l == 0 ? E0 : D[l - 1] + (size_t)(t + 1) * 2 * cell + Hp;
+                WbArgs wa{};
+                wa.Ahi = (const _Float16 *)(base + L.bt[l]);
+                wa.Alo = wa.Ahi + (size_t)(l == 0 ? Hp : 2 * Hp) * 4 * Hp;
+                wa.NB = B;
+                wa.H = Hp;
+                wa.pre = a.Act + c_off * 4;
+                wa.c_prev = t > 0 ? a.Cs + c_off - cell : nullptr;
+                wa.dh = dh_src;
+                wa.ldh = t == kL - 1 || l == 0 ? Hp : 2 * Hp;
+                wa.din = l < kLayers - 1 ? D[l] + (size_t)t * 2 * cell : nullptr;
+                wa.ldx = 2 * Hp;
+                wa.dC = DC[(t + 1) & 1];   // t = 9 reads buffer 0 (zeroed above), t writes buffer t & 1
+                wa.dC_out = DC[t & 1];
+                wa.rm_c = RMc + (size_t)((t + 1) & 1) * B;
+                wa.rm_c_out = t > 0 ? RMc + (size_t)(t & 1) * B : nullptr;
+                // dh's bound: the head's one slot at t = 9 (zeroed for layers below 2, whose dh_9 is 0), else the
+                // column blocks of cell t + 1's product
+                wa.rm_h = RMh + (size_t)((t + 1) & 1) * ns * B;
+                wa.nrh = t == kL - 1 ? 1 : (l > 0 ? ns : nd);
+                wa.rm_h_out = t > 0 ? RMh + (size_t)(t & 1) * ns * B : nullptr;
+                wa.rm_d = l < kLayers - 1 ? RMd + ((size_t)((l + 1) & 1) * kL + t) * ns * B : nullptr;
+                wa.nrd = nd;
+                wa.rm_d_out = l > 0 ? RMd + ((size_t)(l & 1) * kL + t) * ns * B : nullptr;
                 if (l > 0) {   // [input gradient | dh_{t-1}] (t = 0: the former only) into D[l-1] row t
-                    if ((rc = gemm16_bwd(h, B, t > 0 ? 2 * H : H, H, sp.bih[l], 2 * H, sp.dGsp, D[l - 1] + (size_t)t * 2 * cell,
-                                         2 * H)))
-                        return rc;
-                } else if (rg) {   // layer 0, row gradient done: dh_{t-1} only (t = 0: nothing)
-                    if (t > 0 && (rc = gemm16_bwd(h, B, H, H, sp.bx0, H8, sp.dGsp, sp.E0, LE))) return rc;
-                } else {
-                    // layer 0: [dh_{t-1} | window-row gradient] in one product (t = 0: the latter only), then the
-                    // row gradient into rowg row j + t
-                    const int c0 = t > 0 ? 0 : H;
-                    if ((rc = gemm16_bwd(h, B, H8 - c0, H, sp.bx0 + c0, H8, sp.dGsp, sp.E0 + c0, LE))) return rc;
-                    hipLaunchKernelGGL(wide_rowg_kernel, dim3((unsigned)(((size_t)B * kIn + 255) / 256)), dim3(256), 0, s,
-                                       (const float *)(sp.E0 + H), LE, (const float *)sp.consts, a.wsc,
-                                       a.rowg + (size_t)(j + t) * B * kIn, B);
-                    if ((rc = launch_check("wide_rowg_kernel"))) return rc;
+                    wa.out = D[l - 1] + (size_t)t * 2 * cell;
+                    wa.ldo = 2 * Hp;
+                    wa.NO = t > 0 ? 2 * Hp : Hp;
+                    wa.h0 = Hp;
+                    wa.h1 = t > 0 ? 2 * Hp : Hp;
+                    wa.d1 = Hp;
+                } else {       // dh_{t-1} into E0 (t = 0: none), and the window-row gradient into rowg row j + t
+                    wa.out = E0;
+                    wa.ldo = Hp;
+                    wa.NO = t > 0 ? Hp : 0;
+                    wa.h0 = 0;
+                    wa.h1 = Hp;
+                    wa.d1 = 0;
+                    wa.wih0 = (const float *)(base + L.w0p);
+                    wa.rowg = a.rowg + (size_t)(j + t) * B * kIn;
                 }
+                if ((rc = launch_fb(wa, l == 0, s))) return rc;
             }
         }
     }
@@ -1109,6 +945,29 @@ int gemm_wgrad(rocblas_handle h, long long n, int R, int K, const float *dG, con
         }
     }
     return st == rocblas_status_success ? FCR_OK : fail(FCR_EHIP, "rocblas_sgemm (weight gradient) failed: %d", (int)st);
+}
+
+// The surrogate's cells over one window batch at H > 52, fp32 (Model_NN/Functions.py:520-569 trains in fp32): per
+// cell the two gate GEMMs x_t W_ih^T + h_{t-1} W_hh^T on rocBLAS and the cell update; keep_act: the activations
+// i, f, g, o of every cell for the backward
+int sur_wide_cells(rocblas_handle h, const WideArgs &a, const float *const *w_ih, const float *const *w_hh, bool keep_act,
+                   hipStream_t s) {
+    const int B = a.B, H = a.H;
+    const size_t cell = (size_t)B * H;
+    int rc;
+    for (int l = 0; l < kLayers; ++l) {
+        for (int t = 0; t < kL; ++t) {
+            const float *x = l == 0 ? a.X0 + (size_t)t * B * kIn : a.Hs + ((size_t)(l - 1) * kL + t) * cell;
+            if ((rc = gemm_xwt(h, B, 4 * H, l == 0 ? kIn : H, w_ih[l], x, 0.0f, a.G))) return rc;
+            if (t > 0 && (rc = gemm_xwt(h, B, 4 * H, H, w_hh[l], a.Hs + ((size_t)l * kL + t - 1) * cell, 1.0f, a.G)))
+                return rc;
+            if ((rc = launch_cell(B, H, s, a.G, t > 0 ? (const float *)(a.Cs + ((size_t)l * kL + t - 1) * cell) : nullptr,
+                                  a.Cs + ((size_t)l * kL + t) * cell, a.Hs + ((size_t)l * kL + t) * cell,
+                                  keep_act ? a.Act + ((size_t)l * kL + t) * cell * 4 : nullptr)))
+                return rc;
+        }
+    }
+    return FCR_OK;
 }
 
 int lstm_weights_ok(const fcr_weights *w) {
@@ -1611,7 +1470,7 @@ int fcr_lstm_forward(const fcr_dims *d, const fcr_weights *w, const float *x, fl
     rocblas_handle h = blas_on(s);
     if (!h) return fail(FCR_EHIP, "rocblas_create_handle failed");
     const WideArgs a = lstm_args(d, L, base);
-    if ((rc = wide_cells(h, a, w->w_ih, w->w_hh, with_backward != 0, nullptr, s))) return rc;
+    if ((rc = sur_wide_cells(h, a, w->w_ih, w->w_hh, with_backward != 0, s))) return rc;
     hipLaunchKernelGGL(surrogate::readout_kernel, dim3((B + 255) / 256), dim3(256), 0, s,
                        (const float *)(a.Hs + ((size_t)(kLayers - 1) * kL + kL - 1) * B * H), w->fc_w, w->fc_b, y, B, H);
     return launch_check("readout_kernel");
@@ -1662,9 +1521,8 @@ int fcr_lstm_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, 
         for (int t = kL - 1; t >= 0; --t) {
             const size_t c_off = ((size_t)l * kL + t) * cell;
             float *dG = dGs + (size_t)t * gcell;
-            if ((rc = launch_cell_bwd<false>(B, H, s, a.Act + c_off * 4, a.Cs + c_off, t > 0 ? a.Cs + c_off - cell : nullptr,
-                                             a.dH, l < kLayers - 1 ? D[l] + (size_t)t * cell : nullptr, a.dC, dG, nullptr,
-                                             nullptr, 0, H, H)))
+            if ((rc = launch_cell_bwd(B, H, s, a.Act + c_off * 4, a.Cs + c_off, t > 0 ? a.Cs + c_off - cell : nullptr,
+                                      a.dH, l < kLayers - 1 ? D[l] + (size_t)t * cell : nullptr, a.dC, dG)))
                 return rc;
             if (l > 0) {
                 if ((rc = gemm_gw(h, B, 4 * H, H, w->w_ih[l], dG, 0.0f, D[l - 1] + (size_t)t * cell))) return rc;

@@ -48,11 +48,15 @@ constexpr int kWbPieces = kWbStage / 1024 / kWbCons;      // LDS-DMA pieces per 
 constexpr int kWbOffB = 2 * kWbStage;                     // [A stage 0 | A stage 1 | B tile 0 hi, lo | B tile 1 ...]
 constexpr int kWbOffDown = kWbOffB + 4 * kWbTileB;
 constexpr int kWbOffW0 = kWbOffDown + kWbN * 4;           // layer 0: W_ih0 as [unit][gate][kIn]
-constexpr int kWbMaxH = 256;                              // NO = 2H <= 2 column blocks (the row bounds' slots)
-constexpr int kWbLds = kWbOffW0 + 4 * kWbMaxH * kIn * 4;
+constexpr int kWbW0LdsUnits = 768;                        // layer 0 with H above: W_ih0 read from global memory
+constexpr int kWbLds = kWbOffW0 + 4 * kWbW0LdsUnits * kIn * 4;
 static_assert(kWbStage % (1024 * kWbCons) == 0, "DMA pieces");
 static_assert(64 * kWbProd * kWbUnits == 8 * kWbN, "dgate mapping: a step's 8 units of every row over the producers");
 static_assert(kWbLds <= 163840, "LDS");
+// LDS bytes of one launch: the W_ih0 block only for layer 0 with H <= kWbW0LdsUnits
+__host__ __device__ constexpr int wb_lds_bytes(bool l0, int H) {
+    return kWbOffW0 + (l0 && H <= kWbW0LdsUnits ? 4 * H * kIn * 4 : 0);
+}
 
 struct WbArgs {
     const _Float16 *Ahi, *Alo;   // [NP][4H], unit-major K
@@ -65,10 +69,13 @@ struct WbArgs {
     const float *dC;             // [B][H] carried dc in
     float *dC_out;               // [B][H] dc_{t-1} out (another buffer: the other column block still reads dC)
     int ldh, ldx;
-    const float *rm_c, *rm_h, *rm_d;   // row bounds in: max|dc| [B], max|dh| [2][B] (per column block), max|din| [2][B] or null
-    float *rm_c_out, *rm_h_out, *rm_d_out;   // row bounds out (or null): of dc_{t-1}, of the dh / input-grad columns
+    const float *rm_c, *rm_h, *rm_d;   // row bounds in: max|dc| [B], max|dh| [nrh][B] (per column block of their
+                                       // writer), max|din| [nrd][B] or null
+    int nrh, nrd;
+    float *rm_c_out, *rm_h_out, *rm_d_out;   // row bounds out (or null): of dc_{t-1}, of the dh / input-grad columns,
+                                             // [column block][B] (every block writes its slot, 0 where it has none)
     int h0, h1, d1;              // output columns [h0, h1) are dh_{t-1}, [0, d1) the layer below's input gradient
-    const float *wih0;           // layer 0: W_ih0 [4H][kIn] (the window-row gradient), else null
+    const float *wih0;           // layer 0: W_ih0 packed [unit][gate][kIn] (the window-row gradient), else null
     float *rowg;                 // layer 0: [B][kIn] window-row gradient row (+=), else null
 };
 
@@ -81,7 +88,9 @@ struct WbIn {
     f32x4 pi, pf, pg, po, cp, dh, dn, dc;
 };
 
-template <bool L0>
+// W0G: layer 0 at H > kWbW0LdsUnits reads W_ih0 from global memory (L1 / L2: every producer thread of a workgroup
+// reads the same 320 B per step) instead of staging it in LDS
+template <bool L0, bool W0G = false>
 __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -105,19 +114,22 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a)
     const bool elive = b0 + er < a.NB;
     float up = 0.0f;
     if (producer) {
-        float m = a.rm_c[eb] + fmaxf(a.rm_h[eb], a.rm_h[a.NB + eb]);
-        if (a.rm_d) m += fmaxf(a.rm_d[eb], a.rm_d[a.NB + eb]);
+        float mh = 0.0f, md = 0.0f;
+        for (int k = 0; k < a.nrh; ++k) mh = fmaxf(mh, a.rm_h[(size_t)k * a.NB + eb]);
+        if (a.rm_d)
+            for (int k = 0; k < a.nrd; ++k) md = fmaxf(md, a.rm_d[(size_t)k * a.NB + eb]);
+        const float m = a.rm_c[eb] + mh + md;
         const int ex = m > 0.0f ? __builtin_amdgcn_frexp_expf(m) : 0;   // every |dgate| < 2^ex (times (kL-1)/4: forget)
         up = __builtin_amdgcn_ldexpf(1.0f, kWideDgExp - ex);
         if (ep == 0) reinterpret_cast<float *>(lds + kWbOffDown)[er] = __builtin_amdgcn_ldexpf(1.0f, ex - kWideDgExp);
     }
-    float *w0l = reinterpret_cast<float *>(lds + kWbOffW0);
-    if constexpr (L0) {   // W_ih0 [4H][kIn] -> LDS [unit][gate][kIn]
-        for (int i = tid; i < 4 * H * kIn; i += kWbThreads) {
-            const int rw = i / kIn, c = i % kIn, g = rw / H, u = rw % H;
-            w0l[(u * 4 + g) * kIn + c] = a.wih0[i];
-        }
+    float *w0s = reinterpret_cast<float *>(lds + kWbOffW0);
+    if constexpr (L0 && !W0G) {   // W_ih0, packed [unit][gate][kIn] by the host, into LDS as it is (16-B copies)
+        const f32x4 *src = reinterpret_cast<const f32x4 *>(a.wih0);
+        f32x4 *dst = reinterpret_cast<f32x4 *>(w0s);
+        for (int i = tid; i < H * kIn; i += kWbThreads) dst[i] = src[i];   // 4 H kIn floats = H kIn quads
     }
+    const float *w0l = W0G ? a.wih0 : w0s;
 
     // ---- consumers: A by LDS-DMA pieces (16 rows x 64 B of [A hi (16 pieces) | A lo (16)]; lane i lands at +16 i).
     // Issued from inline asm: with the intrinsic anywhere in the kernel the compiler's wait insertion drains every
@@ -357,31 +369,39 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a)
             md = fmaxf(md, red[(w * kWbN + tid) * 2 + 1]);
         }
         const int b = b0 + tid;
-        if (a.rm_h_out) {
-            a.rm_h_out[(size_t)cb * a.NB + b] = mh;
-            if (ny == 1) a.rm_h_out[(size_t)a.NB + b] = 0.0f;
-        }
-        if (a.rm_d_out) {
-            a.rm_d_out[(size_t)cb * a.NB + b] = md;
-            if (ny == 1) a.rm_d_out[(size_t)a.NB + b] = 0.0f;
-        }
+        if (a.rm_h_out) a.rm_h_out[(size_t)cb * a.NB + b] = mh;
+        if (a.rm_d_out) a.rm_d_out[(size_t)cb * a.NB + b] = md;
     }
 }
 
-// A of the gradient product, transposed and split: dst_hi / dst_lo [NO][4H], row n = output column n of
-// [W_ih | W_hh] (layers >= 1, NO = 2H; `wih` null for layer 0: W_hh only, NO = H), column r' = 4 unit + gate
-// (unit-major: a K step of the fused kernel is 8 whole units) holding torch's gate row gate H + unit.
-__global__ void wide_split_bt_kernel(const float *__restrict__ wih, const float *__restrict__ whh, int H, int NO,
-                                     _Float16 *dst_hi, _Float16 *dst_lo) {
+// A of the gradient product, transposed and split: dst_hi / dst_lo [NO][4Hp], row n = output column n of
+// [W_ih | W_hh] (layers >= 1, NO = 2Hp; `wih` null for layer 0: W_hh only, NO = Hp), column r' = 4 unit + gate
+// (unit-major: a K step of the fused kernel is 8 whole units) holding torch's gate row gate H + unit; zero for the
+// padding units (unit or column >= H) of the padded hidden size Hp.
+__global__ void wide_split_bt_kernel(const float *__restrict__ wih, const float *__restrict__ whh, int H, int Hp,
+                                     int NO, _Float16 *dst_hi, _Float16 *dst_lo) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int K = 4 * H;
+    const int K = 4 * Hp;
     if (idx >= (size_t)NO * K) return;
     const int n = (int)(idx / K), rp = (int)(idx % K);
-    const int r = (rp & 3) * H + (rp >> 2);
-    const float v = (wih && n < H) ? wih[(size_t)r * H + n] : whh[(size_t)r * H + (wih ? n - H : n)];
+    const int unit = rp >> 2, r = (rp & 3) * H + unit;
+    const int col = (wih && n >= Hp) ? n - Hp : n;   // column of W_ih (n < Hp) or of W_hh
+    float v = 0.0f;
+    if (unit < H && col < H) v = (wih && n < Hp) ? wih[(size_t)r * H + col] : whh[(size_t)r * H + col];
     const _Float16 hi = (_Float16)v;
     dst_hi[idx] = hi;
     dst_lo[idx] = (_Float16)(v - (float)hi);
 }
 
+}  // namespace fcr
+
+namespace fcr {
+// W_ih0 [4H][kIn] (torch) -> [unit][gate][kIn] over the padded Hp units (zero past H): the fused layer-0 cell's
+// window-row gradient reads it by unit (fcr_wbwd.h)
+__global__ void wide_pack_w0_kernel(const float *__restrict__ wih0, int H, int Hp, float *__restrict__ dst) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= 4 * Hp * kIn) return;
+    const int u = i / (4 * kIn), g = (i / kIn) % 4, c = i % kIn;
+    dst[i] = u < H ? wih0[((size_t)g * H + u) * kIn + c] : 0.0f;
+}
 }  // namespace fcr

@@ -8,7 +8,7 @@
 // Data (fcr_abi.hip, wide layout), all row-major with the batch index outermost inside a slice:
 //   X0  [10][B][5]        layer-0 input rows of the current window (Functions.py:1395-1396, 1433-1434)
 //   Hs, Cs [3][10][B][H]  h_t, c_t of every cell of the current window
-//   Act [3][10][B][4H]    gate activations (i, f, g, o) of the window, kept by the backward's recompute
+//   Act [3][10][B][4H]    gate pre-activations of the window (the surrogate: activations), kept for the backward
 //   G   [B][4H]           gate pre-activations (forward) / d loss / d pre-activations (backward)
 //   rowg [N+9][B][5]      d loss / d (extended window row r): every window's layer-0 input gradient
 //                         lands in rows j..j+9 — the row-gradient bookkeeping of fcr_bwd.h, batch-wide
@@ -27,19 +27,14 @@ struct WideArgs {
     float *xhat, *pred, *tot, *cmd, *err;
     float *X0, *Hs, *Cs, *Act, *G, *dH, *dC, *rowg, *dv;
     const float *dloss;
-    _Float16 *xb0;   // split-f16 rollout: layer-0 operand rows (slot stride B 6H, row stride xb0_ld), else null
+    _Float16 *wr;    // split-f16 rollout: layer 0's window records [10][B][2 kWgRecX0] (hi | lo), else null
     const float *wsc;   // window-column scales of the split's range guard (fcr_pack.h)
 };
 
-// layer 0's K = 5 window-row input as the last kX16 columns of its split-f16 operand rows and weights:
-// [x_hi (5) | x_lo (5) | x_hi (5) | 0] against [Wih_hi | Wih_hi | Wih_lo | 0]; 32 columns keep layer 0's K
-// (3H + kX16, or kX16 at t = 0) a whole number of the fused cell kernel's K steps (fcr_wgemm.h)
-constexpr int kX16 = 32;
-static_assert(3 * kIn < kX16, "layer-0 input split exceeds its padded block");
-// row stride of layer 0's operand rows [h part 3H | x part kX16], padded to whole 128-B lines (rows that
-// straddle lines cost the GEMM's operand loads)
-__host__ __device__ constexpr int xb0_ld(int H) { return (3 * H + kX16 + 63) / 64 * 64; }
-
+// layer 0's window record (the x part of its cell products, fcr_wgemm.h): [hi (32) | lo (32)] halves per
+// trajectory and row, the 5 window columns first, zero after
+constexpr int kWideRecX0 = 32;
+static_assert(kIn <= kWideRecX0, "window columns exceed their record block");
 
 // controller (FNNModel.forward, Functions.py:261-289) pre-Hardtanh output, and its ReLU inputs' signs
 __device__ __forceinline__ float wide_fnn(const WideArgs &a, float x0, float x3, float ref) {
@@ -89,43 +84,43 @@ __global__ void wide_window_kernel(WideArgs a, int j) {
         float x[kIn];
         for (int col = 0; col < kIn; ++col) {
             x[col] = ext_row(a, b, j + t, col);
-            a.X0[((size_t)t * a.B + b) * kIn + col] = x[col];
+            if (a.X0) a.X0[((size_t)t * a.B + b) * kIn + col] = x[col];
         }
-        if (a.xb0) {
-            _Float16 *p = a.xb0 + (size_t)t * a.B * 6 * a.H + (size_t)b * xb0_ld(a.H) + 3 * a.H;
+        if (a.wr) {
+            typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+            h8 hi = {}, lo = {};
+#pragma unroll
             for (int col = 0; col < kIn; ++col) {
                 const float v = x[col] * a.wsc[col];   // range guard (fcr_pack.h): v 2^-s_c against W_ih0 2^s_c
-                const _Float16 hi = (_Float16)v;
-                p[col] = hi;
-                p[kIn + col] = (_Float16)(v - (float)hi);
-                p[2 * kIn + col] = hi;
+                hi[col] = (_Float16)v;
+                lo[col] = (_Float16)(v - (float)hi[col]);
             }
-            for (int k = 3 * kIn; k < kX16; ++k) p[k] = (_Float16)0.0f;
+            h8 *p = reinterpret_cast<h8 *>(a.wr + ((size_t)t * a.B + b) * 2 * kWideRecX0);
+            const h8 z = {};
+#pragma unroll
+            for (int k = 0; k < kWideRecX0 / 8; ++k) {
+                p[k] = k == 0 ? hi : z;
+                p[kWideRecX0 / 8 + k] = k == 0 ? lo : z;
+            }
         }
     }
 }
 
-// Cell update from the gate pre-activations G [B][4H] (torch gate order i|f|g|o): c, h; and, for the
-// backward's recompute, the activations. tanh is the library's (a few ulp RELATIVE to tanh): these
-// memory-bound kernels can afford it, and the weight gradients of the surrogate step need it when the
-// hidden states are small (1 - 2/(1 + e^{2x}) is only accurate to ~1e-7 absolute).
-// xb_h / xb_x (split-f16 path, else null): the GEMM operand rows that take this h — the h part of the
-// same layer's next cell and the x part of the layer above's cell t — as (hi, lo, hi), row strides sh / sx.
-// V consecutive units per thread (V = 4 when H % 4 == 0: 16-B gate / state accesses, 8-B f16 stores —
-// the kernel is HBM-bound and the wide accesses are what it runs at; V = 2 for even H, else 1).
+// The surrogate's fp32 cell update (H > 52; the rollout's cells are fcr_wgemm.h): from the gate pre-activations G
+// [B][4H] (torch gate order i|f|g|o): c, h; and, for the backward, the activations. tanh is the library's (a few ulp
+// RELATIVE to tanh): these memory-bound kernels can afford it, and the weight gradients need it when the hidden states
+// are small (1 - 2/(1 + e^{2x}) is only accurate to ~1e-7 absolute). V consecutive units per thread (V = 4 when
+// H % 4 == 0: 16-B accesses; V = 2 for even H, else 1).
 template <int V>
 struct WideVec {
     typedef float F __attribute__((ext_vector_type(V)));
-    typedef _Float16 h __attribute__((ext_vector_type(V)));
     static __device__ __forceinline__ F ld(const float *p) { return *(const F *)p; }
     static __device__ __forceinline__ void st(float *p, F v) { *(F *)p = v; }
-    static __device__ __forceinline__ void st16(_Float16 *p, h v) { *(h *)p = v; }
 };
 
 template <int V>
 __global__ void wide_cell_kernel(const float *__restrict__ G, const float *__restrict__ c_prev, float *c_out,
-                                 float *h_out, float *act, _Float16 *xb_h, int sh, _Float16 *xb_x, int sx, int B,
-                                 int H) {
+                                 float *h_out, float *act, int B, int H) {
     using W = WideVec<V>;
     const int HV = H / V;
     const size_t iv = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -135,7 +130,6 @@ __global__ void wide_cell_kernel(const float *__restrict__ G, const float *__res
     const typename W::F gi = W::ld(g4), gf = W::ld(g4 + H), gg = W::ld(g4 + 2 * H), go = W::ld(g4 + 3 * H);
     typename W::F cp = {}, i, f, g, o, c, h;
     if (c_prev) cp = W::ld(c_prev + idx);
-    typename W::h hi, lo;
 #pragma unroll
     for (int k = 0; k < V; ++k) {
         i[k] = sigm(gi[k]);
@@ -144,23 +138,9 @@ __global__ void wide_cell_kernel(const float *__restrict__ G, const float *__res
         o[k] = sigm(go[k]);
         c[k] = (c_prev ? f[k] * cp[k] : 0.0f) + i[k] * g[k];
         h[k] = o[k] * tanhf(c[k]);
-        hi[k] = (_Float16)h[k];
-        lo[k] = (_Float16)(h[k] - (float)hi[k]);
     }
     W::st(c_out + idx, c);
     if (h_out) W::st(h_out + idx, h);
-    if (xb_h) {
-        _Float16 *p = xb_h + b * sh + u;
-        W::st16(p, hi);
-        W::st16(p + H, lo);
-        W::st16(p + 2 * H, hi);
-    }
-    if (xb_x) {
-        _Float16 *p = xb_x + b * sx + u;
-        W::st16(p, hi);
-        W::st16(p + H, lo);
-        W::st16(p + 2 * H, hi);
-    }
     if (act) {
         float *a4 = act + b * 4 * H + u;
         W::st(a4, i);
@@ -254,8 +234,7 @@ __device__ __forceinline__ void wide_head_dxhat(const WideArgs &a, int j, int b,
     d[2] = d2;
     d[3] = d3;
 }
-// rmh (the fused backward, fcr_wbwd.h), or null: the row bound max_u |dH[b][u]| into rmh[b] (rmh[B + b] = 0: the
-// second column block's slot)
+// rmh (the fused backward, fcr_wbwd.h), or null: the row bound max_u |dH[b][u]| into rmh[b]
 __global__ void wide_head_kernel(WideArgs a, int j, float *rmh) {
     const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int b = (int)(gid / kRoLanes), q = (int)(gid % kRoLanes);
@@ -274,17 +253,9 @@ __global__ void wide_head_kernel(WideArgs a, int j, float *rmh) {
     if (!rmh) return;
 #pragma unroll
     for (int s = kRoLanes / 2; s > 0; s >>= 1) m = fmaxf(m, __shfl_xor(m, s, kRoLanes));
-    if (live && q == 0) {
-        rmh[b] = m;
-        rmh[a.B + b] = 0.0f;
-    }
+    if (live && q == 0) rmh[b] = m;   // slot 0: the layer-2 cell at t = 9 reads one slot (WbArgs.nrh = 1)
 }
 
-// Backward of one cell: from the activations, c_t, c_{t-1}, the incoming dh (carried dH + din from the
-// layer above; see dh_scaled) and the carried dc: d loss / d (gate pre-activations) into dG, and dc_{t-1} into dC.
-// act: the gate activations (i, f, g, o) kept by the recompute, or with PRE their pre-activations (the
-// split-f16 rollout keeps the GEMM output per cell instead of writing a second 4H-wide array), from which
-// the activations are rebuilt with the forward's arithmetic. dG (fp32) may be null when only dgsp is used.
 // The per-row dgate scale of the fused backward cell (fcr_wbwd.h) is 2^(kWideDgExp - e), e the exponent of a bound m on
 // the row's |dc_t| (m >= |dc| + |dh|): the i, g, o rows are |dc_t| or |dh| times a local derivative <= 1, so below
 // 2^kWideDgExp scaled; the forget row is dc_t c_{t-1} f (1 - f) with |c_{t-1}| <= t <= kL - 1 (|c_t| <= |c_{t-1}| + 1
@@ -296,195 +267,49 @@ __global__ void wide_head_kernel(WideArgs a, int j, float *rmh) {
 // test_wide_forget_dgates_near_their_f16_margin drives the forget row to 2 of the 9/4 this allows).
 constexpr int kWideDgExp = 13;
 static_assert((kL - 1) * (1 << kWideDgExp) / 4 < 65504, "f16 overflow of the forget-gate dgates: lower kWideDgExp");
-// With PRE, c_t is recomputed from the pre-activations and c_{t-1} rather than loaded (round 3d: bit-identical,
-// backward -2.4 % at config 5).
-template <bool PRE, int V, int T = 1>
+
+// The surrogate's fp32 backward of one cell (H > 52): from the activations, c_t, c_{t-1}, the incoming dh (carried dH
+// + din from the layer above) and the carried dc: d loss / d (gate pre-activations) into dG, dc_{t-1} into dC.
+template <int V>
 __global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restrict__ act, const float *__restrict__ c,
-                                     const float *__restrict__ c_prev, const float *__restrict__ dH,
-                                     const float *__restrict__ din, float *dC, float *dG, _Float16 *dgsp,
-                                     const float *__restrict__ consts, int dh_scaled, int ldh, int ldx, int B,
-                                     int H, int dg3, const float *__restrict__ wih0 = nullptr, float *rowg = nullptr) {
+                                                            const float *__restrict__ c_prev, const float *__restrict__ dH,
+                                                            const float *__restrict__ din, float *dC, float *dG, int B,
+                                                            int H) {
     using W = WideVec<V>;
-    // with consts (split-f16 rollout) din, and dH unless it is the head's, come from gemm16_bwd in the
-    // scaled units of the dgates: back by 1/scale = consts[0], one fp32 product each
-    const float c0 = consts ? consts[0] : 1.0f, mh = dh_scaled ? c0 : 1.0f;
     const int HV = H / V;
-    // a thread owns V units of T consecutive trajectories (T > 1 only for layer 0's row gradient: its W_ih0
-    // rows, 4 V kIn floats, are loaded once for the T trajectories instead of once per trajectory)
     const size_t iv = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (iv >= ((size_t)B + T - 1) / T * HV) return;
-    const size_t bg = iv / HV, u = (iv % HV) * V;
-    float wr[4][V * kIn];
-    if (rowg) {
-        static_assert(V * kIn % 4 == 0 || V == 1 || V == 2, "row block in 16-B pieces");
+    if (iv >= (size_t)B * HV) return;
+    const size_t b = iv / HV, u = (iv % HV) * V, idx = b * H + u;
+    const float *a4 = act + b * 4 * H + u;
+    const typename W::F ai = W::ld(a4), af = W::ld(a4 + H), ag = W::ld(a4 + 2 * H), ao = W::ld(a4 + 3 * H);
+    const typename W::F dhv = W::ld(dH + idx), dcv = W::ld(dC + idx), cv = W::ld(c + idx);
+    typename W::F cp = {}, dn = {}, dg[4], dco;
+    if (c_prev) cp = W::ld(c_prev + idx);
+    if (din) dn = W::ld(din + idx);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            // V consecutive rows of kIn floats: V * kIn / 4 16-B loads (80 B at V = 4, 16-B aligned as u % 4 == 0)
-            if constexpr (V == 4) {
-                const f32x4 *w4 = reinterpret_cast<const f32x4 *>(wih0 + ((size_t)k * H + u) * kIn);
-#pragma unroll
-                for (int q = 0; q < V * kIn / 4; ++q) {
-                    const f32x4 v = w4[q];
-                    wr[k][4 * q] = v[0]; wr[k][4 * q + 1] = v[1]; wr[k][4 * q + 2] = v[2]; wr[k][4 * q + 3] = v[3];
-                }
-            } else {
-#pragma unroll
-                for (int q = 0; q < V * kIn; ++q) wr[k][q] = wih0[((size_t)k * H + u) * kIn + q];
-            }
-        }
+    for (int k = 0; k < V; ++k) {
+        const float i = ai[k], f = af[k], g = ag[k], o = ao[k];
+        const float tc = tanhf(cv[k]);
+        const float dh = dhv[k] + dn[k];
+        const float dct = dcv[k] + dh * o * (1.0f - tc * tc);
+        dg[0][k] = dct * g * i * (1.0f - i);
+        dg[1][k] = dct * cp[k] * f * (1.0f - f);
+        dg[2][k] = dct * i * (1.0f - g * g);
+        dg[3][k] = dh * tc * o * (1.0f - o);
+        dco[k] = dct * f;
     }
-    for (int t = 0; t < T; ++t) {
-        const size_t b = bg * T + t, idx = b * H + u;
-        if (b >= (size_t)B) break;   // uniform over the trajectory's H / V threads
-        const float *a4 = act + b * 4 * H + u;
-        const typename W::F ai = W::ld(a4), af = W::ld(a4 + H), ag = W::ld(a4 + 2 * H), ao = W::ld(a4 + 3 * H);
-        const typename W::F dhv = W::ld(dH + b * ldh + u), dcv = W::ld(dC + idx);
-        typename W::F cp = {}, dn = {}, dg[4], dco, cv;
-        if (c_prev) cp = W::ld(c_prev + idx);
-        if (!PRE) cv = W::ld(c + idx);
-        if (din) dn = W::ld(din + b * ldx + u);
+    float *d4 = dG + b * 4 * H + u;
 #pragma unroll
-        for (int k = 0; k < V; ++k) {
-            const float i = PRE ? sigm(ai[k]) : ai[k], f = PRE ? sigm(af[k]) : af[k], g = PRE ? tanhf(ag[k]) : ag[k],
-                        o = PRE ? sigm(ao[k]) : ao[k];
-            // c_t rebuilt as the forward's cell formed it (fcr_wgemm.h epilogue: f c_{t-1} + i g) instead of read: 1 of the
-            // ~14 KB a trajectory row moves through this HBM-bound kernel
-            const float tc = tanhf(PRE ? (c_prev ? f * cp[k] : 0.0f) + i * g : cv[k]);
-            const float dh = dhv[k] * mh + dn[k] * c0;
-            const float dct = dcv[k] + dh * o * (1.0f - tc * tc);
-            dg[0][k] = dct * g * i * (1.0f - i);
-            dg[1][k] = dct * cp[k] * f * (1.0f - f);
-            dg[2][k] = dct * i * (1.0f - g * g);
-            dg[3][k] = dh * tc * o * (1.0f - o);
-            dco[k] = dct * f;
-        }
-        if (dG) {
-            float *d4 = dG + b * 4 * H + u;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) W::st(d4 + k * H, dg[k]);
-        }
-        if (dgsp) {   // split-f16 operand row [hi | lo | hi] of W^T dG, scaled into the f16 range (wide_bscale_kernel)
-            const float sc = consts[3];
-            _Float16 *o16 = dgsp + b * 12 * H + u;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                typename W::h hi, lo;
-#pragma unroll
-                for (int e = 0; e < V; ++e) {
-                    const float v = dg[k][e] * sc;
-                    hi[e] = (_Float16)v;
-                    lo[e] = (_Float16)(v - (float)hi[e]);
-                }
-                W::st16(o16 + k * H, hi);
-                W::st16(o16 + (4 + k) * H, lo);
-                if (dg3) W::st16(o16 + (8 + k) * H, hi);
-            }
-        }
-        W::st(dC + idx, dco);
-        if (rowg) {   // layer 0: the window-row gradient sum_r dG[b][r] W_ih0[r][c] (c < kIn), fp32 from these
-            // dgates, reduced over the trajectory's H / V threads (one aligned segment of a wave: the host checks
-            // 64 % (H / V) == 0) — in place of kIn + 3 more columns in the backward product
-            float pc[kIn] = {};
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-#pragma unroll
-                for (int e = 0; e < V; ++e)
-#pragma unroll
-                    for (int cc = 0; cc < kIn; ++cc) pc[cc] = fmaf(dg[k][e], wr[k][e * kIn + cc], pc[cc]);
-            // (a DPP form of the first four butterfly levels measured within the noise, round 2g)
-#pragma unroll
-            for (int cc = 0; cc < kIn; ++cc)
-                for (int o = 1; o < HV; o <<= 1) pc[cc] += __shfl_xor(pc[cc], o);
-            if (u == 0)
-#pragma unroll
-                for (int cc = 0; cc < kIn; ++cc) rowg[b * kIn + cc] += pc[cc];
-        }
-    }
+    for (int k = 0; k < 4; ++k) W::st(d4 + k * H, dg[k]);
+    W::st(dC + idx, dco);
 }
 
-// Split-f16 operands of the config-5 gate GEMMs (fp32-accurate on the matrix cores, as fcr_f16.h does
-// for the fused kernels): every product a.b becomes a_hi b_hi + a_hi b_lo + a_lo b_hi, laid out as ONE
-// K-concatenated GEMM per cell so the fp32 gate matrix is written once (C traffic, not the MFMA, bounded
-// the per-term calls). Forward A, row-major [4H][6H] = [Wih_hi | Wih_hi | Wih_lo | Whh_hi | Whh_hi | Whh_lo]
-// against operand rows [x_hi | x_lo | x_hi | h_hi | h_lo | h_hi] (layer 0: [h part | x part of kX16 columns]);
-// backward A (below) stacks [W_hi ; W_hi ; W_lo] (12H rows) against the dgate rows [dG_hi | dG_lo | dG_hi].
-__global__ void wide_split_fa_kernel(const float *__restrict__ Wih, const float *__restrict__ Whh, int H, int layer0,
-                                     const float *__restrict__ wsc, _Float16 *dst) {
-    const int KA = layer0 ? 3 * H + kX16 : 6 * H;
-    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (size_t)4 * H * KA) return;
-    const int r = (int)(idx / KA), k = (int)(idx % KA);
-    float v;
-    int term;
-    if (layer0) {
-        if (k < 3 * H) {
-            term = k / H;
-            v = Whh[(size_t)r * H + k % H];
-        } else {
-            const int kk = k - 3 * H;
-            if (kk >= 3 * kIn) {
-                dst[idx] = (_Float16)0.0f;
-                return;
-            }
-            term = kk / kIn;
-            v = Wih[(size_t)r * kIn + kk % kIn] / wsc[kk % kIn];   // range guard (fcr_pack.h): exact
-        }
-    } else {
-        const int part = k / (3 * H), kk = k % (3 * H), u = kk % H;
-        term = kk / H;
-        v = (part == 0 ? Wih : Whh)[(size_t)r * H + u];
-    }
-    const _Float16 hi = (_Float16)v;
-    dst[idx] = term < 2 ? hi : (_Float16)(v - (float)hi);
-}
-
-// Layer 0's backward A, row-major [12H][H + 8]: per split row the W_hh row (H columns), then the W_ih row
-// (kIn columns) and zero padding — ONE product gives dh_{t-1} and the window-row gradient of the cell.
-__global__ void wide_split_bx0_kernel(const float *__restrict__ Wih, const float *__restrict__ Whh, int H,
-                                      const float *__restrict__ wsc, _Float16 *dst) {
-    const int ld = H + 8;
-    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (size_t)12 * H * ld) return;
-    const int r = (int)(idx / ld), col = (int)(idx % ld), term = r / (4 * H), g = r % (4 * H);
-    float v = 0.0f;
-    if (col < H) v = Whh[(size_t)g * H + col];
-    else if (col < H + kIn) v = Wih[(size_t)g * kIn + col - H] / wsc[col - H];
-    const _Float16 hi = (_Float16)v;
-    dst[idx] = term < 2 ? hi : (_Float16)(v - (float)hi);
-}
-// Layers >= 1: backward A row-major [12H][2H], per split row [W_ih row | W_hh row] — ONE product gives the
-// cell's input gradient (the layer below's incoming dh) and dh_{t-1}, side by side in rows of 2H.
-__global__ void wide_split_bcat_kernel(const float *__restrict__ Wih, const float *__restrict__ Whh, int H,
-                                       _Float16 *dst) {
-    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (size_t)24 * H * H) return;
-    const int r = (int)(idx / (2 * H)), col = (int)(idx % (2 * H)), term = r / (4 * H), g = r % (4 * H);
-    const float v = col < H ? Wih[(size_t)g * H + col] : Whh[(size_t)g * H + col - H];
-    const _Float16 hi = (_Float16)v;
-    dst[idx] = term < 2 ? hi : (_Float16)(v - (float)hi);
-}
-// rowg row += the window-row gradient part of layer 0's backward product (scaled units, see dh_scaled; the
-// range guard's column scale back, fcr_pack.h)
-__global__ void wide_rowg_kernel(const float *__restrict__ E, int ldE, const float *__restrict__ consts,
-                                 const float *__restrict__ wsc, float *rowg, int B) {
-    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (size_t)B * kIn) return;
-    const size_t b = idx / kIn, col = idx % kIn;
-    rowg[idx] += consts[0] * E[b * ldE + col] * wsc[col];
-}
-
-// The dgates are split as dG * 2^k / dloss (|dG| ~ dloss / (B N): without it they would sit in the f16
-// subnormals); the backward GEMMs' outputs stay in those units and wide_cell_bwd_kernel scales them back by
-// consts[0] = dloss * 2^-k on load (no host sync for dloss). consts = [1/scale, 0, 1, scale].
-__global__ void wide_bscale_kernel(const float *__restrict__ dloss, int k, float *consts) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    // dloss = 0: every gradient is 0 (no 0 * inf). A non-finite dloss must come out non-finite (as torch's
-    // would, for GradScaler / anomaly detection): the NaN scale turns every dgate operand into NaN.
-    const float d = dloss[0];
-    consts[0] = d != 0.0f ? ldexpf(d, -k) : 0.0f;
-    consts[1] = 0.0f;
-    consts[2] = 1.0f;
-    consts[3] = !isfinite(d) ? __builtin_nanf("") : d != 0.0f ? ldexpf(1.0f, k) / d : 0.0f;
+// fc.W [4][H] -> [4][Hp] with zero padding units: the rollout's readout and head run at the padded size
+__global__ void wide_pad_fc_kernel(const float *__restrict__ fcw, int H, int Hp, float *__restrict__ dst) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= kOut * Hp) return;
+    const int o = i / Hp, u = i % Hp;
+    dst[i] = u < H ? fcw[(size_t)o * H + u] : 0.0f;
 }
 
 // d loss / d u0 (Functions.py:1396 row 9 col 4, and the command costs cmd_0, cmd_1)

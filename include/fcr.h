@@ -276,7 +276,7 @@ int64_t fcr_get_wide_keep_budget(void);
  * TEST HOOK (not a reference interface; nothing on the rollout path calls it): ONE backward cell of the H > 52 path,
  * i.e. the autograd backward of one nn.LSTM cell (Functions.py:325, inside loss.backward() at :655), run by the same
  * kernel and launcher fcr_backward uses (wide_bwd_fused_kernel), on caller-given inputs, so a test can compare every
- * output element with an fp64 evaluation. H % 8 == 0 and H <= 256 (the fused cell's tiling). Per trajectory b:
+ * output element with an fp64 evaluation. H % 8 == 0, H <= 2048 (the fused cell's tiling). Per trajectory b:
  *   pre (B,4H)  gate pre-activations, torch order i|f|g|o;  c_prev (B,H) or NULL (t = 0);
  *   dh (B,H) incoming dh_t of the recurrence;  din (B,H) the layer above's input gradient at t, or NULL;
  *   dc (B,H) carried dc_t;  ->  dc_out (B,H) = dc_{t-1};

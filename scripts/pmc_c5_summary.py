@@ -9,7 +9,7 @@ import shutil
 import sys
 
 tag, root = sys.argv[1], sys.argv[2]
-KERNELS = ("wide_gemm_cell_kernel", "wide_bwd_fused_kernel", "wide_head_kernel", "wide_cell_bwd_kernel")
+KERNELS = ("wide_cell_fwd_kernel", "wide_bwd_fused_kernel", "wide_head_kernel")
 INST = ("SQ_INSTS_VALU_MFMA_F16", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_INST_ANY",
         "SQ_LDS_BANK_CONFLICT", "GRBM_GUI_ACTIVE")
 

@@ -241,8 +241,8 @@ def test_any_hidden_size_up_to_52(H, B, N):
 
 @pytest.mark.parametrize("dloss", [1e-4, 1e4])
 def test_wide_path_any_incoming_gradient_scale(dloss):
-    """H > 52 (config 5's path, split-f16 GEMMs): the dgates enter the f16 GEMM operands as dG 2^k / dloss
-    (wide_bscale_kernel), so a scaled loss (loss * dloss).backward() neither underflows nor overflows them."""
+    """H > 52 (config 5's path, split-f16 products): the dgates enter the f16 operands scaled by each trajectory row's
+    own power of two (fcr_wbwd.h), so a scaled loss (loss * dloss).backward() neither underflows nor overflows them."""
     c, params = load_case("h64_b24_n3")
     o = run(params, c["X"], c["u0"], c["states"], c["N"], c["alpha"], c["noise"], dloss=dloss)
     for k, _ in GRADS:
@@ -252,14 +252,12 @@ def test_wide_path_any_incoming_gradient_scale(dloss):
 @pytest.mark.parametrize("H,B,N", [(54, 300, 3), (57, 77, 2), (96, 520, 4), (64, 129, 2), (128, 300, 3), (192, 260, 2),
                                    (200, 140, 2), (264, 130, 2)])
 def test_wide_path_hidden_sizes(H, B, N):
-    """H > 52 at sizes the golden cases do not hit: even H not a multiple of 4 (cell kernels 2 units per
-    thread), odd H (1 unit per thread), a multiple of 4 at a few hundred trajectories, and multiples of 64
-    (the fused GEMM + cell kernel, fcr_wgemm.h) with a ragged last block of 128 trajectories — the window-row
-    columns inside layer 0's split GEMM and the combined [input gradient | dh] backward products. The fused
-    backward cell (fcr_wbwd.h, H % 8 == 0 and H <= 256): one column block (H <= 128), two with the dh columns
-    straddling them (H = 192, 200: the row bounds' partial slots), the rocBLAS forward beside it (H = 200); H = 264
-    the rocBLAS backward path. Against the fp64 oracle on seeded synthetic weights (parity unpinned: no reference
-    output at these sizes)."""
+    """H > 52 at sizes the golden cases do not hit. Every H runs the hand-written cells (round 5: no rocBLAS on the
+    rollout) at H padded to whole 64-unit blocks with zero-weight units: H = 54, 57 (10 and 7 padding units, the odd
+    H), 200 (56) and 264 (56: Hp = 320, so the fused backward cell's [input gradient | dh_{t-1}] product spans three
+    column blocks of 256 and its row bounds three slots), beside the unpadded 64, 96 (padded to 128), 128 and 192 (two
+    column blocks with the dh columns straddling them); ragged last blocks of 128 trajectories. Against the fp64
+    oracle on seeded synthetic weights (parity unpinned: no reference output at these sizes)."""
     from tests.golden.make_golden import synth_params
     params = synth_params(H, 300 + H)
     X, S, _ = _synth(B, N, 400 + H)
@@ -306,7 +304,7 @@ def test_wide_path_kept_windows_equal_recompute():
 def test_nonfinite_incoming_gradient_propagates(case):
     """A non-finite upstream gradient (an overflowed loss scale) must come out non-finite, as torch's does —
     not as partly-zeroed finite gradients that hide the overflow from GradScaler / anomaly detection — on the
-    fused path (H <= 52) and the GEMM path (H > 52, wide_bscale_kernel)."""
+    fused path (H <= 52) and the wide path (H > 52, whose per-row dgate scales see the non-finite bound)."""
     c, params = load_case(case)
     o = run(params, c["X"], c["u0"], c["states"], c["N"], c["alpha"], c["noise"], dloss=float("inf"))
     for k, _ in GRADS:

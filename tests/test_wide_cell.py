@@ -93,6 +93,7 @@ def _check(got, want, bound, what, tol=1e-6):
 CASES = [  # (H, B, t0, top): nk = H / 8
     (64, 300, False, False), (96, 300, False, False), (200, 300, False, False), (256, 300, False, False),
     (200, 131, True, False), (256, 77, False, True), (256, 257, True, True),
+    (264, 300, False, False),   # three column blocks (2H = 528), three row-bound slots in the rollout
 ]
 
 
@@ -112,7 +113,8 @@ def test_layer_cell_product_every_element(H, B, t0, top):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("H,B,t0", [(64, 300, False), (256, 300, False), (200, 129, True)])
+@pytest.mark.parametrize("H,B,t0", [(64, 300, False), (256, 300, False), (200, 129, True),
+                                    (1000, 64, False)])   # H > 768: W_ih0 read from global memory, not LDS
 def test_layer0_cell_product_and_row_gradient(H, B, t0):
     x = _inputs(B, H, 8000 + H + B, t0, False, True)
     out, dc_out, rowg = run_cell(x, True)
