@@ -577,7 +577,7 @@ int cell_hook_check(int B, int H) {
 
 // One backward cell of the H > 52 path exactly as wide_backward launches it (launch_fb, fcr_wbwd.h), on caller-given
 // inputs: the standalone form the per-element tests of tests/test_wide_cell.py compare with an fp64 product
-int wide_bwd_cell_hook(int B, int H, int layer0, const float *w_ih, const float *w_hh, const float *pre,
+int wide_bwd_cell_hook(int B, int H, int layer0, const float *w_ih, const float *w_hh, const float *act,
                        const float *c_prev, const float *dh, const float *din, const float *dc, float *out,
                        float *dc_out, float *rowg, char *base, hipStream_t s) {
     const CellHookLayout L = cell_hook_layout(B, H, layer0);
@@ -606,7 +606,7 @@ int wide_bwd_cell_hook(int B, int H, int layer0, const float *w_ih, const float 
     wa.Alo = bt + nbt;
     wa.NB = B;
     wa.H = H;
-    wa.pre = pre;
+    wa.act = act;
     wa.c_prev = c_prev;
     wa.dh = dh;
     wa.ldh = H;
@@ -641,8 +641,8 @@ int wide_bwd_cell_hook(int B, int H, int layer0, const float *w_ih, const float 
 }
 
 // One window's 30 cells, forward (the rollout, and the backward's recompute of a window that was not kept): layer by
-// layer, t = 0..9, each cell one wide_cell_fwd_kernel launch. keep_act: the cells' gate pre-activations into `Act`
-// (the backward rebuilds i, f, g, o from them).
+// layer, t = 0..9, each cell one wide_cell_fwd_kernel launch. keep_act: the cells' gate activations into `Act` (the
+// backward's dgates read them, as autograd reads the activations its forward saved).
 int wide_cells(const WideArgs &a, const WideLayout &L, char *base, bool keep_act, hipStream_t s) {
     const int B = a.B, Hp = L.Hp;
     const size_t cell = (size_t)B * Hp;
@@ -663,7 +663,7 @@ int wide_cells(const WideArgs &a, const WideLayout &L, char *base, bool keep_act
             wa.c_prev = t > 0 ? a.Cs + ((size_t)l * kL + t - 1) * cell : nullptr;
             wa.c_out = a.Cs + ((size_t)l * kL + t) * cell;
             wa.h_out = (l == kLayers - 1 && t == kL - 1) ? a.Hs : nullptr;
-            wa.preact = keep_act ? a.Act + ((size_t)l * kL + t) * cell * 4 : nullptr;
+            wa.act = keep_act ? a.Act + ((size_t)l * kL + t) * cell * 4 : nullptr;
             wa.h_rec = rec(l, t);
             if ((rc = launch_wgemm_cell(wa, s))) return rc;
         }
@@ -781,7 +781,7 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
                 wa.Alo = wa.Ahi + (size_t)(l == 0 ? Hp : 2 * Hp) * 4 * Hp;
                 wa.NB = B;
                 wa.H = Hp;
-                wa.pre = a.Act + c_off * 4;
+                wa.act = a.Act + c_off * 4;
                 wa.c_prev = t > 0 ? a.Cs + c_off - cell : nullptr;
                 wa.dh = dh_src;
                 wa.ldh = t == kL - 1 || l == 0 ? Hp : 2 * Hp;
@@ -1231,17 +1231,17 @@ int fcr_wide_bwd_cell_workspace(int32_t B, int32_t H, int32_t layer0, size_t *by
     return FCR_OK;
 }
 
-int fcr_wide_bwd_cell(int32_t B, int32_t H, int32_t layer0, const float *w_ih, const float *w_hh, const float *pre,
+int fcr_wide_bwd_cell(int32_t B, int32_t H, int32_t layer0, const float *w_ih, const float *w_hh, const float *act,
                       const float *c_prev, const float *dh, const float *din, const float *dc, float *out,
                       float *dc_out, float *rowg, void *ws, size_t ws_bytes, void *stream) {
     if (const int rc = cell_hook_check(B, H)) return rc;
-    if (!w_hh || !pre || !dh || !dc || !dc_out || !ws || (!layer0 && !w_ih) || (layer0 && (!w_ih || !rowg)) ||
+    if (!w_hh || !act || !dh || !dc || !dc_out || !ws || (!layer0 && !w_ih) || (layer0 && (!w_ih || !rowg)) ||
         ((c_prev || !layer0) && !out))
         return fail(FCR_EINVAL, "fcr_wide_bwd_cell: a required pointer is NULL");
     if (((uintptr_t)ws) & 255) return fail(FCR_EINVAL, "fcr_wide_bwd_cell: ws must be 256-byte aligned");
     const size_t need = cell_hook_layout(B, H, layer0).total;
     if (ws_bytes < need) return fail(FCR_EWORKSPACE, "fcr_wide_bwd_cell: ws has %zu bytes, needs %zu", ws_bytes, need);
-    return wide_bwd_cell_hook(B, H, layer0, w_ih, w_hh, pre, c_prev, dh, din, dc, out, dc_out, rowg, (char *)ws,
+    return wide_bwd_cell_hook(B, H, layer0, w_ih, w_hh, act, c_prev, dh, din, dc, out, dc_out, rowg, (char *)ws,
                               (hipStream_t)stream);
 }
 

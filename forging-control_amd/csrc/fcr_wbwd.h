@@ -62,7 +62,8 @@ struct WbArgs {
     const _Float16 *Ahi, *Alo;   // [NP][4H], unit-major K
     float *out;                  // [B][ldo], columns [0, NO); NO = 0: no product (layer 0, t = 0)
     int ldo, NO, NB, H;
-    const float *pre;            // [B][4H] gate pre-activations (i | f | g | o blocks of H) of the cell
+    const float *act;            // [B][4H] gate activations (i | f | g | o blocks of H) of the cell, as its forward
+                                 // evaluated them (fcr_wgemm.h)
     const float *c_prev;         // [B][H] or null (t = 0)
     const float *dh;             // [B][ldh] incoming dh of the recurrence (the head's, or the next cell's product)
     const float *din;            // [B][ldx] the layer above's input gradient at t, or null
@@ -162,7 +163,7 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a)
     };
 
     // ---- producers: inputs one step ahead, the tile one step ahead of the MFMAs ----
-    const float *pre = a.pre + (size_t)eb * K;
+    const float *pre = a.act + (size_t)eb * K;
     const float *cpr = a.c_prev ? a.c_prev + (size_t)eb * H : nullptr;
     const float *dhr = a.dh + (size_t)eb * a.ldh;
     const float *dnr = a.din ? a.din + (size_t)eb * a.ldx : nullptr;
@@ -191,7 +192,7 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a)
         const int u = 8 * s + kWbUnits * ep;
 #pragma unroll
         for (int k = 0; k < kWbUnits; ++k) {
-            const float i = sigm(x.pi[k]), f = sigm(x.pf[k]), g = tanh_f(x.pg[k]), o = sigm(x.po[k]);
+            const float i = x.pi[k], f = x.pf[k], g = x.pg[k], o = x.po[k];   // the forward's activations
             const float cp = x.cp[k];
             const float tc = tanh_f(fmaf(f, cp, i * g));   // c_t rebuilt as the forward formed it (f c_{t-1} + i g)
             const float dh = x.dh[k] + x.dn[k];

@@ -61,7 +61,8 @@ struct WgArgs {
     const float *c_prev;   // [B][H] or null (t = 0)
     float *c_out;          // [B][H]
     float *h_out;          // [B][H] fp32 or null (the readout's cell only)
-    float *preact;         // [B][4H] or null: the gate pre-activations (a kept window's backward reads them)
+    float *act;            // [B][4H] or null: the gate activations i | f | g | o, as the cell update evaluated them
+                           // (the backward's dgates read them: no sigmoid / tanh of its own but tanh(c_t))
     _Float16 *h_rec;       // [B][2H] this cell's h record (hi | lo): the next cell's and the layer above's operand
 };
 
@@ -216,6 +217,7 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_cell_fwd_kernel(WgArgs a) 
             const f32x4 g4 = acc[m][n];
             const float cp = a.c_prev ? cs[r * CSTR + ul] : 0.0f;
             const float i = sigm(g4[0]), f = sigm(g4[1]), g = tanhf(g4[2]), o = sigm(g4[3]);
+            acc[m][n] = f32x4{i, f, g, o};   // the accumulators become the activations the act rows store
             const float c = (a.c_prev ? f * cp : 0.0f) + i * g;
             const float h = o * tanhf(c);
             const _Float16 hi = (_Float16)h;
@@ -238,7 +240,7 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_cell_fwd_kernel(WgArgs a) 
         *reinterpret_cast<u32x4 *>(a.h_rec + (size_t)b * 2 * H + (ec < 8 ? 0 : H) + u0 + 8 * e) =
             *reinterpret_cast<const u32x4 *>(src);
     }
-    if (a.preact) {   // gate by gate through the c tile: rows of 64 pre-activations
+    if (a.act) {   // gate by gate through the c tile: rows of 64 activations
 #pragma unroll
         for (int gt = 0; gt < 4; ++gt) {
             __syncthreads();
@@ -251,7 +253,7 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_cell_fwd_kernel(WgArgs a) 
             for (int p = 0; p < kWgN / ERS; ++p) {
                 const int r = er + ERS * p, b = b0 + r;
                 if (b < a.B)
-                    *reinterpret_cast<f32x4 *>(a.preact + (size_t)b * 4 * H + gt * H + u0 + 4 * ec) =
+                    *reinterpret_cast<f32x4 *>(a.act + (size_t)b * 4 * H + gt * H + u0 + 4 * ec) =
                         *reinterpret_cast<const f32x4 *>(cs + r * CSTR + 4 * ec);
             }
         }

@@ -277,7 +277,8 @@ int64_t fcr_get_wide_keep_budget(void);
  * i.e. the autograd backward of one nn.LSTM cell (Functions.py:325, inside loss.backward() at :655), run by the same
  * kernel and launcher fcr_backward uses (wide_bwd_fused_kernel), on caller-given inputs, so a test can compare every
  * output element with an fp64 evaluation. H % 8 == 0, H <= 2048 (the fused cell's tiling). Per trajectory b:
- *   pre (B,4H)  gate pre-activations, torch order i|f|g|o;  c_prev (B,H) or NULL (t = 0);
+ *   act (B,4H)  gate activations i = sigmoid, f = sigmoid, g = tanh, o = sigmoid of the pre-activations (torch
+ *               order i|f|g|o), as the forward cell saved them;  c_prev (B,H) or NULL (t = 0);
  *   dh (B,H) incoming dh_t of the recurrence;  din (B,H) the layer above's input gradient at t, or NULL;
  *   dc (B,H) carried dc_t;  ->  dc_out (B,H) = dc_{t-1};
  *   layer0 == 0: out (B,2H) = dG [W_ih | W_hh] (input gradient | dh_{t-1}; only the first H columns without c_prev),
@@ -288,7 +289,7 @@ int64_t fcr_get_wide_keep_budget(void);
  * fcr_wide_bwd_cell_workspace bytes, 256-byte aligned.
  */
 int fcr_wide_bwd_cell_workspace(int32_t B, int32_t H, int32_t layer0, size_t *bytes);
-int fcr_wide_bwd_cell(int32_t B, int32_t H, int32_t layer0, const float *w_ih, const float *w_hh, const float *pre,
+int fcr_wide_bwd_cell(int32_t B, int32_t H, int32_t layer0, const float *w_ih, const float *w_hh, const float *act,
                       const float *c_prev, const float *dh, const float *din, const float *dc, float *out,
                       float *dc_out, float *rowg, void *ws, size_t ws_bytes, void *stream);
 

@@ -29,10 +29,11 @@ def _sig(x):
     return 1.0 / (1.0 + np.exp(-x))
 
 
-def ref_cell(pre, c_prev, dh, din, dc, w_ih, w_hh):
-    """fp64: (dG (B,4H), dc_{t-1} (B,H), dG w_ih, dG w_hh) and the magnitude bounds |dG| |W| of the two products."""
+def ref_cell(act, c_prev, dh, din, dc, w_ih, w_hh):
+    """fp64: (dG (B,4H), dc_{t-1} (B,H), dG w_ih, dG w_hh) and the magnitude bounds |dG| |W| of the two products, from
+    the gate activations the forward saved (i, f, g, o = act blocks)."""
     H = dh.shape[1]
-    i, f, g, o = _sig(pre[:, :H]), _sig(pre[:, H:2 * H]), np.tanh(pre[:, 2 * H:3 * H]), _sig(pre[:, 3 * H:])
+    i, f, g, o = act[:, :H], act[:, H:2 * H], act[:, 2 * H:3 * H], act[:, 3 * H:]
     cp = np.zeros_like(dh) if c_prev is None else c_prev
     c = f * cp + i * g
     tc = np.tanh(c)
@@ -49,8 +50,10 @@ def _inputs(B, H, seed, t0, top, layer0):
     # per-row gradient magnitudes over 8 decades: the kernel's per-row power-of-two scales
     scale = 10.0 ** g.uniform(-6, 2, (B, 1))
     k = 1.0 / np.sqrt(H)
+    pre = g.normal(0, 1.5, (B, 4 * H))
+    act = np.concatenate([_sig(pre[:, :2 * H]), np.tanh(pre[:, 2 * H:3 * H]), _sig(pre[:, 3 * H:])], axis=1)
     return {
-        "pre": f32(g.normal(0, 1.5, (B, 4 * H))),
+        "act": f32(act),   # the forward's saved activations (fp32)
         "c_prev": None if t0 else f32(g.uniform(-2.5, 2.5, (B, H))),
         "dh": f32(g.normal(0, 1, (B, H)) * scale),
         "din": None if (top or layer0) else f32(g.normal(0, 1, (B, H)) * scale),
@@ -74,7 +77,7 @@ def run_cell(x, layer0):
     ws = torch.empty(nbytes.value, dtype=torch.uint8, device=DEV)
     p = lambda v: None if v is None else v.data_ptr()
     stream = torch.cuda.current_stream(DEV).cuda_stream
-    native.check(lib.fcr_wide_bwd_cell(B, H, int(layer0), p(t["w_ih"]), p(t["w_hh"]), p(t["pre"]), p(t["c_prev"]),
+    native.check(lib.fcr_wide_bwd_cell(B, H, int(layer0), p(t["w_ih"]), p(t["w_hh"]), p(t["act"]), p(t["c_prev"]),
                                        p(t["dh"]), p(t["din"]), p(t["dc"]), p(out), p(dc_out), p(rowg), p(ws),
                                        ws.numel(), stream), "fcr_wide_bwd_cell")
     torch.cuda.synchronize()
@@ -102,7 +105,7 @@ CASES = [  # (H, B, t0, top): nk = H / 8
 def test_layer_cell_product_every_element(H, B, t0, top):
     x = _inputs(B, H, 7000 + H + B, t0, top, False)
     out, dc_out, _ = run_cell(x, False)
-    dG, dcp, o_ih, o_hh, b_ih, b_hh = ref_cell(x["pre"], x["c_prev"], x["dh"], x["din"], x["dc"], x["w_ih"], x["w_hh"])
+    dG, dcp, o_ih, o_hh, b_ih, b_hh = ref_cell(x["act"], x["c_prev"], x["dh"], x["din"], x["dc"], x["w_ih"], x["w_hh"])
     _check(out[:, :H], o_ih, b_ih, "input gradient")
     if not t0:
         _check(out[:, H:], o_hh, b_hh, "dh_{t-1}")
@@ -118,7 +121,7 @@ def test_layer_cell_product_every_element(H, B, t0, top):
 def test_layer0_cell_product_and_row_gradient(H, B, t0):
     x = _inputs(B, H, 8000 + H + B, t0, False, True)
     out, dc_out, rowg = run_cell(x, True)
-    dG, dcp, o_ih, o_hh, b_ih, b_hh = ref_cell(x["pre"], x["c_prev"], x["dh"], None, x["dc"], x["w_ih"], x["w_hh"])
+    dG, dcp, o_ih, o_hh, b_ih, b_hh = ref_cell(x["act"], x["c_prev"], x["dh"], None, x["dc"], x["w_ih"], x["w_hh"])
     if not t0:
         _check(out, o_hh, b_hh, "dh_{t-1}")
     _check(rowg, o_ih, b_ih, "window-row gradient")   # fp32 sums of fp32 dgates, not the split product
