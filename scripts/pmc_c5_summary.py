@@ -1,5 +1,5 @@
 """Config-5 PMC summary (scripts/profile.sh TAG c5|c5max): HBM bytes per launch of the main H = 256 kernels, and the
-HBM bytes of one whole backward pass (every dispatch from wide_bscale_kernel to the ctrl_grad_kernel after it),
+HBM bytes of one whole backward pass (every dispatch from its first wide_head_kernel to the ctrl_grad_kernel after it),
 FETCH_SIZE / WRITE_SIZE in separate passes with the gfx950 correction (2 x FETCH + WRITE, MI355X_MICROARCH.md).
     python scripts/pmc_c5_summary.py TAG DIR  ->  profiles/TAG_c5_pmc.json, profiles/TAG_c5_kernel_stats.csv"""
 import csv
@@ -35,11 +35,14 @@ for kind, cnt in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         if vals:
             out.setdefault(name, {})[cnt + "_KB_per_launch"] = sum(vals) / len(vals)
             out[name]["launches"] = len(vals)
-    # backward passes: wide_bscale_kernel .. the next ctrl_grad_kernel (inclusive); the last one profiled counts
-    tot, on, last = 0.0, False, None
+    # backward passes: the first wide_head_kernel after a forward's loss_reduce_kernel .. the next ctrl_grad_kernel
+    # (inclusive); the last one profiled counts
+    tot, on, last, fwd_done = 0.0, False, None, False
     for n, v in ds:
-        if "wide_bscale_kernel" in n:
-            on, tot = True, 0.0
+        if "loss_reduce_kernel" in n:
+            fwd_done = True
+        if fwd_done and "wide_head_kernel" in n and not on:
+            on, tot, fwd_done = True, 0.0, False
         if on:
             tot += v
         if on and "ctrl_grad_kernel" in n:
@@ -59,7 +62,7 @@ if passes.get("FETCH_SIZE") is not None and passes.get("WRITE_SIZE") is not None
 out["_note"] = ("rocprofv3 PMC passes of bench.py --hidden 256 --horizon 25 --batch 65536 (config 5), KB; "
                 "hbm_bytes_corrected = 2*FETCH + WRITE (gfx950); SQ_* / GRBM_* per launch from one more pass (SQ_WAVE_CYCLES and "
                 "SQ_WAIT_INST_ANY in quad-cycles, MI355X_MICROARCH.md). bwd_pass = every dispatch of the last profiled "
-                "backward pass, wide_bscale_kernel .. ctrl_grad_kernel.")
+                "backward pass, its first wide_head_kernel .. ctrl_grad_kernel.")
 stats = glob.glob(f"{root}/trace/**/*kernel_stats.csv", recursive=True)
 if stats:
     shutil.copy(stats[0], f"profiles/{tag}_c5_kernel_stats.csv")
