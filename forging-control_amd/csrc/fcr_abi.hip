@@ -6,7 +6,6 @@
 // /root/reference/Unsupervised Learning/Functions.py:646 and :655. All launches are stream-ordered on
 // the caller's stream; nothing here allocates or synchronises.
 #include <hip/hip_runtime.h>
-#include <rocblas/rocblas.h>
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -28,6 +27,7 @@
 #include "fcr_wide.h"
 #include "fcr_wbwd.h"
 #include "fcr_wgemm.h"
+#include "fcr_wgrad.h"
 
 namespace fcr {
 
@@ -377,33 +377,6 @@ long long wide_default_cap() {
     return cap_of[dev];
 }
 
-rocblas_handle blas_on(hipStream_t s) {
-    thread_local rocblas_handle h = nullptr;
-    if (!h) {
-        if (rocblas_create_handle(&h) != rocblas_status_success) return nullptr;
-        // no split-K solutions that sum through atomics: every GEMM here is run-to-run deterministic
-        // (the surrogate's gradients and graph replays repeat bit for bit)
-        rocblas_set_atomics_mode(h, rocblas_atomics_not_allowed);
-    }
-    rocblas_set_stream(h, s);
-    return h;
-}
-
-// G (row-major B x 4H) (+)= X (B x K) . W^T, W row-major (4H x K) as torch stores it
-int gemm_xwt(rocblas_handle h, int B, int H4, int K, const float *W, const float *X, float beta, float *G) {
-    const float one = 1.0f;
-    const rocblas_status st = rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, H4, B, K, &one,
-                                            W, K, X, K, &beta, G, H4);
-    return st == rocblas_status_success ? FCR_OK : fail(FCR_EHIP, "rocblas_sgemm (forward) failed: %d", (int)st);
-}
-// dX (row-major B x K) (+)= dG (B x 4H) . W (4H x K)
-int gemm_gw(rocblas_handle h, int B, int H4, int K, const float *W, const float *dG, float beta, float *dX) {
-    const float one = 1.0f;
-    const rocblas_status st = rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, K, B, H4, &one, W,
-                                            K, dG, H4, &beta, dX, K);
-    return st == rocblas_status_success ? FCR_OK : fail(FCR_EHIP, "rocblas_sgemm (backward) failed: %d", (int)st);
-}
-
 // The rollout's per-call packs of the current weights: forward split weights per layer, the backward product's A
 // and W_ih0 (with_backward), the readout's fc.W, all at the padded Hp
 int wide_pack(const fcr_weights *w, int H, const WideLayout &L, bool backward, char *base, const float *wsc,
@@ -460,31 +433,6 @@ WideArgs wide_args(const fcr_dims *d, const WideLayout &L, char *base) {
     a.wsc = (const float *)(base + L.wsc);
     a.wr = (_Float16 *)(base + L.WR);
     return a;
-}
-
-// The cell kernels' vector width (fcr_wide.h): 16-B accesses when H % 4 == 0, 8-B when H is even.
-int cell_vec(int H) { return H % 4 == 0 ? 4 : (H % 2 == 0 ? 2 : 1); }
-
-// the surrogate's fp32 cell update (fcr_wide.h wide_cell_kernel)
-int launch_cell(int B, int H, hipStream_t s, const float *G, const float *c_prev, float *c_out, float *h_out,
-                float *act) {
-    const int V = cell_vec(H);
-    const dim3 grid((unsigned)(((size_t)B * (H / V) + 255) / 256)), blk(256);
-    if (V == 4) hipLaunchKernelGGL(wide_cell_kernel<4>, grid, blk, 0, s, G, c_prev, c_out, h_out, act, B, H);
-    else if (V == 2) hipLaunchKernelGGL(wide_cell_kernel<2>, grid, blk, 0, s, G, c_prev, c_out, h_out, act, B, H);
-    else hipLaunchKernelGGL(wide_cell_kernel<1>, grid, blk, 0, s, G, c_prev, c_out, h_out, act, B, H);
-    return launch_check("wide_cell_kernel");
-}
-
-// the surrogate's fp32 backward cell (fcr_wide.h wide_cell_bwd_kernel)
-int launch_cell_bwd(int B, int H, hipStream_t s, const float *act, const float *c, const float *c_prev, const float *dH,
-                    const float *din, float *dC, float *dG) {
-    const int V = cell_vec(H);
-    const dim3 grid((unsigned)(((size_t)B * (H / V) + 255) / 256)), blk(256);
-    if (V == 4) hipLaunchKernelGGL((wide_cell_bwd_kernel<4>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, B, H);
-    else if (V == 2) hipLaunchKernelGGL((wide_cell_bwd_kernel<2>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, B, H);
-    else hipLaunchKernelGGL((wide_cell_bwd_kernel<1>), grid, blk, 0, s, act, c, c_prev, dH, din, dC, dG, B, H);
-    return launch_check("wide_cell_bwd_kernel");
 }
 
 // The per-call weight packs (pack_fwd16_item, pack_img_item, pack_misc_item) as jobs of one launch:
@@ -643,17 +591,19 @@ int wide_bwd_cell_hook(int B, int H, int layer0, const float *w_ih, const float 
 // One window's 30 cells, forward (the rollout, and the backward's recompute of a window that was not kept): layer by
 // layer, t = 0..9, each cell one wide_cell_fwd_kernel launch. keep_act: the cells' gate activations into `Act` (the
 // backward's dgates read them, as autograd reads the activations its forward saved).
-int wide_cells(const WideArgs &a, const WideLayout &L, char *base, bool keep_act, hipStream_t s) {
-    const int B = a.B, Hp = L.Hp;
+// fw: the layers' split weights; HR: h records of `slots` layers (layer l in slot l % slots: the rollout keeps two, the
+// surrogate all three for its weight gradients)
+int wide_cells(const WideArgs &a, const _Float16 *const *fw, _Float16 *HR, int Hp, int slots, bool keep_act,
+               hipStream_t s) {
+    const int B = a.B;
     const size_t cell = (size_t)B * Hp;
-    _Float16 *HR = (_Float16 *)(base + L.HR);
-    auto rec = [&](int l, int t) { return HR + ((size_t)(l & 1) * kL + t) * B * 2 * Hp; };   // h record of cell (l, t)
+    auto rec = [&](int l, int t) { return HR + ((size_t)(l % slots) * kL + t) * B * 2 * Hp; };   // h record of (l, t)
     int rc;
     for (int l = 0; l < kLayers; ++l) {
         const size_t K = (l == 0 ? kWgRecX0 : Hp) + Hp;
         for (int t = 0; t < kL; ++t) {
             WgArgs wa{};
-            wa.W = (const _Float16 *)(base + L.fw[l]);
+            wa.W = fw[l];
             wa.K = (int)K;
             wa.kx = l == 0 ? kWgRecX0 : Hp;
             wa.xr = l == 0 ? a.wr + (size_t)t * B * 2 * kWgRecX0 : rec(l - 1, t);
@@ -669,6 +619,13 @@ int wide_cells(const WideArgs &a, const WideLayout &L, char *base, bool keep_act
         }
     }
     return FCR_OK;
+}
+
+// the rollout's window cells (two record slots)
+int wide_window_cells(const WideArgs &a, const WideLayout &L, char *base, bool keep_act, hipStream_t s) {
+    const _Float16 *fw[kLayers];
+    for (int l = 0; l < kLayers; ++l) fw[l] = (const _Float16 *)(base + L.fw[l]);
+    return wide_cells(a, fw, (_Float16 *)(base + L.HR), L.Hp, 2, keep_act, s);
 }
 
 int wide_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const float *u0, const float *states,
@@ -715,8 +672,8 @@ int wide_forward(const fcr_dims *d, const fcr_weights *w, const float *X, const 
             WideArgs ak = a;
             ak.Act = kept_act(L, base, d, j);
             ak.Cs = kept_c(L, base, d, j);
-            if ((rc = wide_cells(ak, L, base, true, s))) return rc;
-        } else if ((rc = wide_cells(a, L, base, false, s))) {
+            if ((rc = wide_window_cells(ak, L, base, true, s))) return rc;
+        } else if ((rc = wide_window_cells(a, L, base, false, s))) {
             return rc;
         }
         hipLaunchKernelGGL(wide_readout_kernel, dim3((unsigned)(((size_t)d->B * kRoLanes + 255) / 256)), dim3(256), 0, s, a, j,
@@ -762,7 +719,7 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
             a.Cs = (float *)(base + L.Cs);
             hipLaunchKernelGGL(wide_window_kernel<false>, dim3(nb), dim3(256), 0, s, a, j);
             if ((rc = launch_check("wide_window_kernel"))) return rc;
-            if ((rc = wide_cells(a, L, base, true, s))) return rc;   // checkpoint: recompute the window
+            if ((rc = wide_window_cells(a, L, base, true, s))) return rc;   // checkpoint: recompute the window
         }
         for (int l = kLayers - 1; l >= 0; --l) {
             if (l < kLayers - 1 && hipMemsetAsync(a.dH, 0, sizeof(float) * cell, s) != hipSuccess)
@@ -850,122 +807,249 @@ int check_lstm_dims(const fcr_dims *d) {
     return FCR_OK;
 }
 
-// Split of the weight-gradient reduction: S chunks of `rows` rows each (S·rows >= n), S partial R x K products.
-// A single GEMM over n = 10·B rows has a tiny output (e.g. 200 x 50) and so only a handful of tiles: the
-// library runs the whole reduction on one or two workgroups. Chunking turns it into a strided-batched GEMM
-// with hundreds of independent tiles plus one fixed-order sum (deterministic).
-struct WgradSplit {
+// H > 52: the surrogate's step on the rollout's wide kernels (no vendor library): the forward cells of fcr_wgemm.h
+// over the window batch (every cell's activations, c and h records kept), the fused backward cells of fcr_wbwd.h
+// (which also write each cell's dgates), and the weight gradients as reductions over all 10 B (step, sample) rows
+// on the fp32 matrix cores (fcr_wgrad.h). Hidden size padded to Hp as on the rollout's wide path.
+struct SurWideLayout {
+    int Hp, ns;
+    size_t fcw, wsc, rng, xt, WR, HR, Cs, Act, Hs, fw[3], bt[3], w0p, dH, dC, DC2, D[2], E0, RMc, RMh, RMd, rowg, dG,
+        fcpart, part, total;
+};
+constexpr int kSurFcSlices = 64;   // batch slices of the readout's weight gradient (fixed: deterministic)
+
+// n slices of one weight-gradient reduction: enough workgroups to fill the chip, whole kWgrN steps per slice
+struct WgSplit {
     int S;
-    long long rows;
+    long long n_per;
 };
-WgradSplit wgrad_split(long long n, int R, int K) {
-    const long long kPartFloats = 16LL << 20;                // 64 MiB of partials at most
-    long long S = n / 8192;                                  // >= 8192 rows per chunk, <= 64 chunks: the
-    S = S < 1 ? 1 : (S > 64 ? 64 : S);                       // fixed-order sum stays a small fraction
-    while (S > 1 && S * R * K > kPartFloats) S >>= 1;
-    const long long rows = (n + S - 1) / S;
-    return {(int)((n + rows - 1) / rows), rows};
-}
-size_t wgrad_part_floats(long long n, int R, int K) {
-    const WgradSplit w = wgrad_split(n, R, K);
-    return w.S > 1 ? (size_t)w.S * R * K : 0;
+WgSplit wg_split(long long n, int R, int K) {
+    const long long tiles = (long long)((R + kWgrT - 1) / kWgrT) * ((K + kWgrT - 1) / kWgrT);
+    long long S = (512 + tiles - 1) / tiles;
+    S = S < 1 ? 1 : (S > 64 ? 64 : S);
+    long long per = (n + S - 1) / S;
+    per = (per + kWgrN - 1) / kWgrN * kWgrN;
+    return {(int)((n + per - 1) / per), per};
 }
 
-struct LstmLayout {
-    size_t X0, Hs, Cs, G, Act, dGs, dH, dC, D[2], gx, part, total;
-};
-
-LstmLayout make_lstm(const fcr_dims *d, int with_backward) {
-    LstmLayout L{};
+SurWideLayout make_surw(const fcr_dims *d, int with_backward) {
+    SurWideLayout L{};
     size_t off = 0;
     auto take = [&](size_t bytes) {
         const size_t o = off;
         off += align_up(bytes);
         return o;
     };
-    const size_t B = d->B, H = d->H, F = sizeof(float);
-    L.X0 = take(F * kL * B * kIn);
-    L.Hs = take(F * kLayers * kL * B * H);
-    L.Cs = take(F * kLayers * kL * B * H);
-    L.G = take(F * B * 4 * H);
+    const size_t B = d->B, F = sizeof(float), F16 = sizeof(_Float16), Hp = (size_t)wide_hp(d->H);
+    L.Hp = (int)Hp;
+    L.ns = wide_nslots((int)Hp);
+    L.fcw = take(F * kOut * Hp);
+    L.wsc = take(F * 8);
+    L.rng = take(F * 8 * kRangeBlocks);
+    L.xt = take(F * kL * B * kIn);
+    L.WR = take(F16 * kL * B * 2 * kWgRecX0);
+    L.HR = take(F16 * kLayers * kL * B * 2 * Hp);
+    L.Cs = take(F * kLayers * kL * B * Hp);
+    L.Act = take(F * kLayers * kL * B * 4 * Hp);
+    L.Hs = take(F * B * Hp);
+    for (int l = 0; l < kLayers; ++l) {
+        L.fw[l] = take(F16 * 2 * 4 * Hp * ((l == 0 ? kWgRecX0 : Hp) + Hp));
+        if (with_backward) L.bt[l] = take(F16 * 2 * (l == 0 ? Hp : 2 * Hp) * 4 * Hp);
+    }
     if (with_backward) {
-        L.Act = take(F * kLayers * kL * B * 4 * H);
-        L.dGs = take(F * kL * B * 4 * H);
-        L.dH = take(F * B * H);
-        L.dC = take(F * B * H);
-        L.D[0] = take(F * kL * B * H);
-        L.D[1] = take(F * kL * B * H);
-        L.gx = take(F * kL * B * kIn);
-        size_t pf = wgrad_part_floats((long long)B, kOut, H);   // the largest split of any weight gradient
-        for (int K : {kIn, (int)H}) {
-            const size_t a = wgrad_part_floats((long long)kL * B, 4 * H, K);
+        L.w0p = take(F * Hp * 4 * kIn);
+        L.dH = take(F * B * Hp);
+        L.dC = take(F * B * Hp);
+        L.DC2 = take(F * B * Hp);
+        L.D[0] = take(F * kL * B * 2 * Hp);
+        L.D[1] = take(F * kL * B * 2 * Hp);
+        L.E0 = take(F * B * Hp);
+        L.RMc = take(F * 2 * B);
+        L.RMh = take(F * 2 * L.ns * B);
+        L.RMd = take(F * 2 * kL * L.ns * B);
+        L.rowg = take(F * kL * B * kIn);
+        L.dG = take(F * kL * B * 4 * Hp);   // one layer's dgates, every step
+        L.fcpart = take(F * kSurFcSlices * kOut * Hp);
+        size_t pf = 0;   // the largest set of weight-gradient partials
+        for (int K : {kIn, d->H}) {
+            const WgSplit w = wg_split((long long)kL * B, 4 * (int)Hp, K);
+            const size_t a = (size_t)w.S * 4 * Hp * K;
             pf = a > pf ? a : pf;
         }
-        L.part = take(F * (pf ? pf : 1));
+        L.part = take(F * pf);
     }
     L.total = off;
     return L;
 }
 
-__global__ void wgrad_sum_kernel(const float *__restrict__ part, int S, long long RK, float *__restrict__ dW) {
-    const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= RK) return;
-    float acc = 0.0f;
-    for (int s = 0; s < S; ++s) acc += part[(long long)s * RK + e];
-    dW[e] = acc;
-}
-
-// dW (row-major R x K) = Σ_n dG[n][r] · X[n][k]: dG (n x R), X (n x K) row-major — the weight gradient of one
-// LSTM weight matrix with the reduction over n = (window step, sample) rows. `part` holds
-// wgrad_part_floats(n, R, K) floats (unused when the reduction is not split).
-int gemm_wgrad(rocblas_handle h, long long n, int R, int K, const float *dG, const float *X, float *part, float *dW,
-               hipStream_t s) {
-    const float one = 1.0f, zero = 0.0f;
-    const WgradSplit w = wgrad_split(n, R, K);
-    rocblas_status st;
-    if (w.S == 1) {
-        st = rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, K, R, (int)n, &one, X, K, dG, R,
-                           &zero, dW, K);
-    } else {
-        // full chunks as one strided-batched call, the ragged last chunk as its own GEMM
-        const int full = (int)(n / w.rows);
-        st = rocblas_sgemm_strided_batched(h, rocblas_operation_none, rocblas_operation_transpose, K, R, (int)w.rows,
-                                           &one, X, K, w.rows * K, dG, R, w.rows * R, &zero, part, K, (long long)R * K,
-                                           full);
-        if (st == rocblas_status_success && full < w.S) {
-            const long long r0 = (long long)full * w.rows;
-            st = rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, K, R, (int)(n - r0), &one,
-                               X + r0 * K, K, dG + r0 * R, R, &zero, part + (long long)full * R * K, K);
-        }
-        if (st == rocblas_status_success) {
-            const long long RK = (long long)R * K;
-            hipLaunchKernelGGL(wgrad_sum_kernel, dim3((unsigned)((RK + 255) / 256)), dim3(256), 0, s, (const float *)part,
-                               w.S, RK, dW);
-            if (hipGetLastError() != hipSuccess) return fail(FCR_EHIP, "launch of wgrad_sum_kernel failed");
-        }
-    }
-    return st == rocblas_status_success ? FCR_OK : fail(FCR_EHIP, "rocblas_sgemm (weight gradient) failed: %d", (int)st);
-}
-
-// The surrogate's cells over one window batch at H > 52, fp32 (Model_NN/Functions.py:520-569 trains in fp32): per
-// cell the two gate GEMMs x_t W_ih^T + h_{t-1} W_hh^T on rocBLAS and the cell update; keep_act: the activations
-// i, f, g, o of every cell for the backward
-int sur_wide_cells(rocblas_handle h, const WideArgs &a, const float *const *w_ih, const float *const *w_hh, bool keep_act,
-                   hipStream_t s) {
-    const int B = a.B, H = a.H;
-    const size_t cell = (size_t)B * H;
+int surw_forward(const fcr_dims *d, const fcr_weights *w, const float *x, float *y, int with_backward, char *base,
+                 hipStream_t s) {
+    const SurWideLayout L = make_surw(d, with_backward);
+    const int B = d->B, Hp = L.Hp;
     int rc;
+    // range guard of the window columns from the batch itself (as the H <= 52 step: u0 = x, fcr_pack.h)
+    if ((rc = launch_range(d, x, x, nullptr, w->fc_w, w->fc_b, (float *)(base + L.rng), (float *)(base + L.wsc), s)))
+        return rc;
+    hipLaunchKernelGGL(sur_window_rec_kernel, dim3((unsigned)((B * kL + 255) / 256)), dim3(256), 0, s, x,
+                       (const float *)(base + L.wsc), B, (_Float16 *)(base + L.WR), (float *)(base + L.xt));
+    if ((rc = launch_check("sur_window_rec_kernel"))) return rc;
+    auto grid = [](size_t n) { return dim3((unsigned)((n + 255) / 256)); };
+    const _Float16 *fw[kLayers];
     for (int l = 0; l < kLayers; ++l) {
-        for (int t = 0; t < kL; ++t) {
-            const float *x = l == 0 ? a.X0 + (size_t)t * B * kIn : a.Hs + ((size_t)(l - 1) * kL + t) * cell;
-            if ((rc = gemm_xwt(h, B, 4 * H, l == 0 ? kIn : H, w_ih[l], x, 0.0f, a.G))) return rc;
-            if (t > 0 && (rc = gemm_xwt(h, B, 4 * H, H, w_hh[l], a.Hs + ((size_t)l * kL + t - 1) * cell, 1.0f, a.G)))
-                return rc;
-            if ((rc = launch_cell(B, H, s, a.G, t > 0 ? (const float *)(a.Cs + ((size_t)l * kL + t - 1) * cell) : nullptr,
-                                  a.Cs + ((size_t)l * kL + t) * cell, a.Hs + ((size_t)l * kL + t) * cell,
-                                  keep_act ? a.Act + ((size_t)l * kL + t) * cell * 4 : nullptr)))
-                return rc;
+        const size_t K = (l == 0 ? kWgRecX0 : Hp) + Hp, n = (size_t)4 * Hp * K;
+        _Float16 *p = (_Float16 *)(base + L.fw[l]);
+        hipLaunchKernelGGL(wide_split_fw_kernel, grid(n), dim3(256), 0, s, w->w_ih[l], w->w_hh[l], d->H, Hp, (int)(l == 0),
+                           (const float *)(base + L.wsc), p, p + n);
+        if ((rc = launch_check("wide_split_fw_kernel"))) return rc;
+        fw[l] = p;
+    }
+    hipLaunchKernelGGL(wide_pad_fc_kernel, grid((size_t)kOut * Hp), dim3(256), 0, s, w->fc_w, d->H, Hp, (float *)(base + L.fcw));
+    if ((rc = launch_check("wide_pad_fc_kernel"))) return rc;
+    WideArgs a{};
+    a.B = B;
+    a.N = 1;
+    a.H = Hp;
+    a.Cs = (float *)(base + L.Cs);
+    a.Act = (float *)(base + L.Act);
+    a.Hs = (float *)(base + L.Hs);
+    a.wr = (_Float16 *)(base + L.WR);
+    if ((rc = wide_cells(a, fw, (_Float16 *)(base + L.HR), Hp, kLayers, with_backward != 0, s))) return rc;
+    hipLaunchKernelGGL(surrogate::readout_kernel, dim3((B + 255) / 256), dim3(256), 0, s, (const float *)a.Hs,
+                       (const float *)(base + L.fcw), w->fc_b, y, B, Hp);
+    return launch_check("readout_kernel");
+}
+
+// one weight gradient: dW [4H][K] = sum_n A[n][.] X[n][.] (fcr_wgrad.h), X fp32 rows or split records
+int surw_wgrad(const float *A, long long n, int Hp, int H, int K, const float *X, int ldx, const _Float16 *XR,
+               float *part, float *dW, hipStream_t s) {
+    const WgSplit sp = wg_split(n, 4 * Hp, K);
+    WgradArgs g{};
+    g.A = A;
+    g.lda = 4 * Hp;
+    g.X = X;
+    g.XR = XR;
+    g.ldx = ldx;
+    g.Hx = Hp;
+    g.n = n;
+    g.R = 4 * Hp;
+    g.K = K;
+    g.n_per = sp.n_per;
+    g.part = part;
+    hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)((4 * Hp + kWgrT - 1) / kWgrT), (unsigned)((K + kWgrT - 1) / kWgrT),
+                                          (unsigned)sp.S),
+                       dim3(kWgrThreads), 0, s, g);
+    int rc = launch_check("wgrad_kernel");
+    if (rc) return rc;
+    const long long e = (long long)4 * H * K;
+    hipLaunchKernelGGL(wgrad_sum_pad_kernel, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, s, (const float *)part, sp.S,
+                       H, Hp, K, dW);
+    return launch_check("wgrad_sum_pad_kernel");
+}
+
+int surw_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, float *const *g_w_ih, float *const *g_w_hh,
+                  float *g_fc_w, float *g_fc_b, float *g_x, char *base, hipStream_t s) {
+    const SurWideLayout L = make_surw(d, 1);
+    const int B = d->B, H = d->H, Hp = L.Hp, ns = L.ns, nd = wide_dslots(Hp);
+    const size_t cell = (size_t)B * Hp;
+    int rc;
+    auto grid = [](size_t n) { return dim3((unsigned)((n + 255) / 256)); };
+    // the backward's packs (the forward's split weights and padded fc.W are still in ws)
+    for (int l = 0; l < kLayers; ++l) {
+        const int NO = l == 0 ? Hp : 2 * Hp;
+        const size_t nbt = (size_t)NO * 4 * Hp;
+        _Float16 *bt = (_Float16 *)(base + L.bt[l]);
+        hipLaunchKernelGGL(wide_split_bt_kernel, grid(nbt), dim3(256), 0, s, l == 0 ? (const float *)nullptr : w->w_ih[l],
+                           w->w_hh[l], H, Hp, NO, bt, bt + nbt);
+        if ((rc = launch_check("wide_split_bt_kernel"))) return rc;
+    }
+    hipLaunchKernelGGL(wide_pack_w0_kernel, grid((size_t)4 * Hp * kIn), dim3(256), 0, s, w->w_ih[0], H, Hp,
+                       (float *)(base + L.w0p));
+    if ((rc = launch_check("wide_pack_w0_kernel"))) return rc;
+    const float *Hs = (const float *)(base + L.Hs), *fcw = (const float *)(base + L.fcw);
+    // readout: d fc.W = dy^T h_9 (fixed batch slices), d fc.b = sum dy, dh_9 = dy fc.W (its row bound: slot 0)
+    const int b_per = (B + kSurFcSlices - 1) / kSurFcSlices;
+    float *fcpart = (float *)(base + L.fcpart);
+    hipLaunchKernelGGL(fc_wgrad_part_kernel, dim3((unsigned)((Hp + 255) / 256), kSurFcSlices), dim3(256), 0, s, dy, Hs, B,
+                       Hp, b_per, fcpart);
+    hipLaunchKernelGGL(fc_wgrad_sum_kernel, grid((size_t)kOut * H), dim3(256), 0, s, (const float *)fcpart,
+                       kSurFcSlices, H, Hp, g_fc_w);
+    hipLaunchKernelGGL(surrogate::bias_grad_kernel, dim3(kOut), dim3(surrogate::kSurBlock), 0, s, dy, g_fc_b, B);
+    float *dH = (float *)(base + L.dH);
+    float *RMc = (float *)(base + L.RMc), *RMh = (float *)(base + L.RMh), *RMd = (float *)(base + L.RMd);
+    hipLaunchKernelGGL(sur_head_kernel, grid(cell), dim3(256), 0, s, dy, fcw, B, Hp, dH);
+    hipLaunchKernelGGL(row_absmax_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, (const float *)dH, Hp, Hp, B, RMh);
+    if ((rc = launch_check("readout backward"))) return rc;
+    float *D[2] = {(float *)(base + L.D[0]), (float *)(base + L.D[1])};
+    float *DC[2] = {(float *)(base + L.dC), (float *)(base + L.DC2)};
+    float *E0 = (float *)(base + L.E0), *rowg = (float *)(base + L.rowg), *dG = (float *)(base + L.dG);
+    float *part = (float *)(base + L.part);
+    const float *Cs = (const float *)(base + L.Cs), *Act = (const float *)(base + L.Act);
+    const _Float16 *HR = (const _Float16 *)(base + L.HR);
+    if (hipMemsetAsync(rowg, 0, sizeof(float) * kL * B * kIn, s) != hipSuccess) return fail(FCR_EHIP, "hipMemsetAsync failed");
+    for (int l = kLayers - 1; l >= 0; --l) {
+        if ((l < kLayers - 1 && hipMemsetAsync(dH, 0, sizeof(float) * cell, s) != hipSuccess) ||
+            hipMemsetAsync(DC[0], 0, sizeof(float) * cell, s) != hipSuccess ||
+            hipMemsetAsync(RMc, 0, sizeof(float) * B, s) != hipSuccess ||
+            (l < kLayers - 1 && hipMemsetAsync(RMh, 0, sizeof(float) * B, s) != hipSuccess))
+            return fail(FCR_EHIP, "hipMemsetAsync failed");
+        for (int t = kL - 1; t >= 0; --t) {   // the rollout's backward cells (wide_backward), one window
+            const size_t c_off = ((size_t)l * kL + t) * cell;
+            WbArgs wa{};
+            wa.Ahi = (const _Float16 *)(base + L.bt[l]);
+            wa.Alo = wa.Ahi + (size_t)(l == 0 ? Hp : 2 * Hp) * 4 * Hp;
+            wa.NB = B;
+            wa.H = Hp;
+            wa.act = Act + c_off * 4;
+            wa.c_prev = t > 0 ? Cs + c_off - cell : nullptr;
+            wa.dh = t == kL - 1 ? dH : l == 0 ? E0 : D[l - 1] + (size_t)(t + 1) * 2 * cell + Hp;
+            wa.ldh = t == kL - 1 || l == 0 ? Hp : 2 * Hp;
+            wa.din = l < kLayers - 1 ? D[l] + (size_t)t * 2 * cell : nullptr;
+            wa.ldx = 2 * Hp;
+            wa.dC = DC[(t + 1) & 1];
+            wa.dC_out = DC[t & 1];
+            wa.rm_c = RMc + (size_t)((t + 1) & 1) * B;
+            wa.rm_c_out = t > 0 ? RMc + (size_t)(t & 1) * B : nullptr;
+            wa.rm_h = RMh + (size_t)((t + 1) & 1) * ns * B;
+            wa.nrh = t == kL - 1 ? 1 : (l > 0 ? ns : nd);
+            wa.rm_h_out = t > 0 ? RMh + (size_t)(t & 1) * ns * B : nullptr;
+            wa.rm_d = l < kLayers - 1 ? RMd + ((size_t)((l + 1) & 1) * kL + t) * ns * B : nullptr;
+            wa.nrd = nd;
+            wa.rm_d_out = l > 0 ? RMd + ((size_t)(l & 1) * kL + t) * ns * B : nullptr;
+            wa.dg = dG + (size_t)t * cell * 4;
+            if (l > 0) {
+                wa.out = D[l - 1] + (size_t)t * 2 * cell;
+                wa.ldo = 2 * Hp;
+                wa.NO = t > 0 ? 2 * Hp : Hp;
+                wa.h0 = Hp;
+                wa.h1 = t > 0 ? 2 * Hp : Hp;
+                wa.d1 = Hp;
+            } else {
+                wa.out = E0;
+                wa.ldo = Hp;
+                wa.NO = t > 0 ? Hp : 0;
+                wa.h0 = 0;
+                wa.h1 = Hp;
+                wa.d1 = 0;
+                wa.wih0 = (const float *)(base + L.w0p);
+                wa.rowg = rowg + (size_t)t * B * kIn;   // dL/dx of window row t (the cell's window-row gradient)
+            }
+            if ((rc = launch_fb(wa, l == 0, s))) return rc;
         }
+        // the layer's weight gradients over all (step, sample) rows: x_t = the window rows (layer 0, fp32) or the
+        // layer below's h records; h_{t-1} = this layer's records of steps 0..8 against the dgates of steps 1..9
+        const long long n10 = (long long)kL * B, n9 = (long long)(kL - 1) * B;
+        if ((rc = surw_wgrad(dG, n10, Hp, H, l == 0 ? kIn : H, l == 0 ? (const float *)(base + L.xt) : nullptr, kIn,
+                             l == 0 ? nullptr : HR + (size_t)(l - 1) * kL * B * 2 * Hp, part, g_w_ih[l], s)))
+            return rc;
+        if ((rc = surw_wgrad(dG + (size_t)B * 4 * Hp, n9, Hp, H, H, nullptr, 0, HR + (size_t)l * kL * B * 2 * Hp, part,
+                             g_w_hh[l], s)))
+            return rc;
+    }
+    if (g_x) {   // the window-row gradients [t][B][5] -> (B, 10, 5)
+        const long long nx = (long long)B * kL * kIn;
+        hipLaunchKernelGGL(surrogate::window_transpose_kernel, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, s,
+                           (const float *)rowg, g_x, B, kIn, true);
+        if ((rc = launch_check("window_transpose_kernel"))) return rc;
     }
     return FCR_OK;
 }
@@ -975,21 +1059,6 @@ int lstm_weights_ok(const fcr_weights *w) {
     for (int l = 0; l < kLayers; ++l)
         if (!w->w_ih[l] || !w->w_hh[l]) return 0;
     return 1;
-}
-
-WideArgs lstm_args(const fcr_dims *d, const LstmLayout &L, char *base) {
-    WideArgs a{};
-    a.B = d->B;
-    a.N = 1;
-    a.H = d->H;
-    a.X0 = (float *)(base + L.X0);
-    a.Hs = (float *)(base + L.Hs);
-    a.Cs = (float *)(base + L.Cs);
-    a.G = (float *)(base + L.G);
-    a.Act = L.Act ? (float *)(base + L.Act) : nullptr;
-    a.dH = L.dH ? (float *)(base + L.dH) : nullptr;
-    a.dC = L.dC ? (float *)(base + L.dC) : nullptr;
-    return a;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1442,7 +1511,7 @@ int fcr_lstm_workspace_size(const fcr_dims *dims, int with_backward, size_t *byt
     int rc = check_lstm_dims(dims);
     if (rc) return rc;
     if (!bytes) return fail(FCR_EINVAL, "bytes is NULL");
-    *bytes = is_wide(dims) ? make_lstm(dims, with_backward).total : make_sur(dims, with_backward).total;
+    *bytes = is_wide(dims) ? make_surw(dims, with_backward).total : make_sur(dims, with_backward).total;
     return FCR_OK;
 }
 
@@ -1458,22 +1527,9 @@ int fcr_lstm_forward(const fcr_dims *d, const fcr_weights *w, const float *x, fl
         if (ws_bytes < need) return fail(FCR_EWORKSPACE, "fcr_lstm_forward: ws has %zu bytes, needs %zu", ws_bytes, need);
         return sur_forward(d, w, x, y, with_backward, (char *)ws, (hipStream_t)stream);
     }
-    const LstmLayout L = make_lstm(d, with_backward);
-    if (ws_bytes < L.total) return fail(FCR_EWORKSPACE, "fcr_lstm_forward: ws has %zu bytes, needs %zu", ws_bytes, L.total);
-    hipStream_t s = (hipStream_t)stream;
-    char *base = (char *)ws;
-    const int B = d->B, H = d->H;
-    const long long nx = (long long)B * kL * kIn;
-    hipLaunchKernelGGL(surrogate::window_transpose_kernel, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, s, x,
-                       (float *)(base + L.X0), B, kIn, false);
-    if ((rc = launch_check("window_transpose_kernel"))) return rc;
-    rocblas_handle h = blas_on(s);
-    if (!h) return fail(FCR_EHIP, "rocblas_create_handle failed");
-    const WideArgs a = lstm_args(d, L, base);
-    if ((rc = sur_wide_cells(h, a, w->w_ih, w->w_hh, with_backward != 0, s))) return rc;
-    hipLaunchKernelGGL(surrogate::readout_kernel, dim3((B + 255) / 256), dim3(256), 0, s,
-                       (const float *)(a.Hs + ((size_t)(kLayers - 1) * kL + kL - 1) * B * H), w->fc_w, w->fc_b, y, B, H);
-    return launch_check("readout_kernel");
+    const size_t need = make_surw(d, with_backward).total;
+    if (ws_bytes < need) return fail(FCR_EWORKSPACE, "fcr_lstm_forward: ws has %zu bytes, needs %zu", ws_bytes, need);
+    return surw_forward(d, w, x, y, with_backward, (char *)ws, (hipStream_t)stream);
 }
 
 int fcr_lstm_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, float *const *g_w_ih,
@@ -1492,59 +1548,9 @@ int fcr_lstm_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, 
         if (ws_bytes < need) return fail(FCR_EWORKSPACE, "fcr_lstm_backward: ws has %zu bytes, needs %zu", ws_bytes, need);
         return sur_backward(d, dy, g_w_ih, g_w_hh, g_fc_w, g_fc_b, g_x, (char *)ws, (hipStream_t)stream);
     }
-    const LstmLayout L = make_lstm(d, 1);
-    if (ws_bytes < L.total) return fail(FCR_EWORKSPACE, "fcr_lstm_backward: ws has %zu bytes, needs %zu", ws_bytes, L.total);
-    hipStream_t s = (hipStream_t)stream;
-    char *base = (char *)ws;
-    const int B = d->B, H = d->H;
-    const size_t cell = (size_t)B * H, gcell = (size_t)B * 4 * H;
-    const int nc = (int)((cell + 255) / 256);
-    rocblas_handle h = blas_on(s);
-    if (!h) return fail(FCR_EHIP, "rocblas_create_handle failed");
-    const WideArgs a = lstm_args(d, L, base);
-    float *dGs = (float *)(base + L.dGs);
-    float *D[2] = {(float *)(base + L.D[0]), (float *)(base + L.D[1])};
-    float *gx = (float *)(base + L.gx);
-    const float *htop = a.Hs + ((size_t)(kLayers - 1) * kL + kL - 1) * cell;
-    // readout: d fc.W = dy^T h_9, d fc.b = Σ dy, dh_9 = dy fc.W
-    float *part = (float *)(base + L.part);
-    if ((rc = gemm_wgrad(h, B, kOut, H, dy, htop, part, g_fc_w, s))) return rc;
-    hipLaunchKernelGGL(surrogate::bias_grad_kernel, dim3(kOut), dim3(surrogate::kSurBlock), 0, s, dy, g_fc_b, B);
-    if ((rc = launch_check("bias_grad_kernel"))) return rc;
-    hipLaunchKernelGGL(surrogate::readout_bwd_kernel, dim3(nc), dim3(256), 0, s, dy, w->fc_w, a.dH, B, H);
-    if ((rc = launch_check("readout_bwd_kernel"))) return rc;
-    for (int l = kLayers - 1; l >= 0; --l) {
-        const int K = l == 0 ? kIn : H;
-        if (l < kLayers - 1 && hipMemsetAsync(a.dH, 0, sizeof(float) * cell, s) != hipSuccess)
-            return fail(FCR_EHIP, "hipMemsetAsync failed");
-        if (hipMemsetAsync(a.dC, 0, sizeof(float) * cell, s) != hipSuccess) return fail(FCR_EHIP, "hipMemsetAsync failed");
-        for (int t = kL - 1; t >= 0; --t) {
-            const size_t c_off = ((size_t)l * kL + t) * cell;
-            float *dG = dGs + (size_t)t * gcell;
-            if ((rc = launch_cell_bwd(B, H, s, a.Act + c_off * 4, a.Cs + c_off, t > 0 ? a.Cs + c_off - cell : nullptr,
-                                      a.dH, l < kLayers - 1 ? D[l] + (size_t)t * cell : nullptr, a.dC, dG)))
-                return rc;
-            if (l > 0) {
-                if ((rc = gemm_gw(h, B, 4 * H, H, w->w_ih[l], dG, 0.0f, D[l - 1] + (size_t)t * cell))) return rc;
-            } else if (g_x) {
-                if ((rc = gemm_gw(h, B, 4 * H, kIn, w->w_ih[0], dG, 0.0f, gx + (size_t)t * B * kIn))) return rc;
-            }
-            if (t > 0 && (rc = gemm_gw(h, B, 4 * H, H, w->w_hh[l], dG, 0.0f, a.dH))) return rc;
-        }
-        // the layer's weight gradients: one GEMM each over all (step, sample) rows
-        const float *xin = l == 0 ? a.X0 : a.Hs + (size_t)(l - 1) * kL * cell;
-        if ((rc = gemm_wgrad(h, (long long)kL * B, 4 * H, K, dGs, xin, part, g_w_ih[l], s))) return rc;
-        if ((rc = gemm_wgrad(h, (long long)(kL - 1) * B, 4 * H, H, dGs + gcell, a.Hs + (size_t)l * kL * cell, part,
-                             g_w_hh[l], s)))
-            return rc;
-    }
-    if (g_x) {
-        const long long nx = (long long)B * kL * kIn;
-        hipLaunchKernelGGL(surrogate::window_transpose_kernel, dim3((unsigned)((nx + 255) / 256)), dim3(256), 0, s,
-                           (const float *)gx, g_x, B, kIn, true);
-        if ((rc = launch_check("window_transpose_kernel"))) return rc;
-    }
-    return FCR_OK;
+    const size_t need = make_surw(d, 1).total;
+    if (ws_bytes < need) return fail(FCR_EWORKSPACE, "fcr_lstm_backward: ws has %zu bytes, needs %zu", ws_bytes, need);
+    return surw_backward(d, w, dy, g_w_ih, g_w_hh, g_fc_w, g_fc_b, g_x, (char *)ws, (hipStream_t)stream);
 }
 
 int fcr_fnn_workspace_size(int32_t B, int32_t hidden, size_t *bytes) {

@@ -1,5 +1,5 @@
 // fcr_wbwd.h — H > 52 (config 5): ONE kernel per backward cell: the cell's gate gradients (the backward of the LSTM
-// cell update, formerly wide_cell_bwd_kernel) formed in the prologue of the gradient product
+// cell update) formed in the prologue of the gradient product
 // [input grad | dh_{t-1}] = dG · [W_ih | W_hh], so the dgate rows never go to HBM. Reference: the autograd backward of
 // nn.LSTM inside loss.backward() (Functions.py:325, :655).
 //
@@ -18,7 +18,7 @@
 // steps of 32: A through a 2-stage LDS-DMA ring issued by the consumers (W^T is L2-resident); the B tile of step
 // ks + 1 is formed while the consumers multiply step ks. Producer thread (row r = tid / 2, half p = tid % 2) loads
 // units 8s + 4p .. + 3 of its trajectory (pre-activations, c_{t-1}, dh, din, dc: 16-B loads, one step ahead), forms
-// their 16 dgates and dc_{t-1} (fcr_wide.h wide_cell_bwd_kernel's algebra), splits them into the two 16-B chunks of
+// their 16 dgates and dc_{t-1} from the forward's saved activations, splits them into the two 16-B chunks of
 // its row half. With two column blocks (NO > 256) both form the same dgates; the first writes dc_{t-1}.
 // Row scale: 2^(13 - e), e the exponent of a bound on the row's |dgates|: |dgate| <= |dc_t| <= |dc| + |dh_rec| +
 // |din| (forget row: x (kL - 1) / 4, fcr_wide.h kWideDgExp). The three maxima come from the kernels that wrote those
@@ -77,6 +77,8 @@ struct WbArgs {
                                              // [column block][B] (every block writes its slot, 0 where it has none)
     int h0, h1, d1;              // output columns [h0, h1) are dh_{t-1}, [0, d1) the layer below's input gradient
     const float *wih0;           // layer 0: W_ih0 packed [unit][gate][kIn] (the window-row gradient), else null
+    float *dg;                   // [B][4H] the cell's dgates (fp32, rows gate H + unit), or null: the surrogate's weight
+                                 // gradients (fcr_wgrad.h) read them; the rollout needs none
     float *rowg;                 // layer 0: [B][kIn] window-row gradient row (+=), else null
 };
 
@@ -204,6 +206,12 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a)
             dco[k] = dct * f;
         }
         if (wr_dc) *reinterpret_cast<f32x4 *>(dco_r + u) = dco;
+        if (a.dg && wr_dc) {   // (column block 0 writes them: every block forms the same)
+            float *d = a.dg + (size_t)eb * K + u;
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                *reinterpret_cast<f32x4 *>(d + g * H) = f32x4{dg[g], dg[4 + g], dg[8 + g], dg[12 + g]};
+        }
 #pragma unroll
         for (int k = 0; k < kWbUnits; ++k) mdc = fmaxf(mdc, fabsf(dco[k]));
         if constexpr (L0) {   // sum_r dG[b][r] W_ih0[r][c] over this thread's 16 gate rows, fp32

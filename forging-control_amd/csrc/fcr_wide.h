@@ -106,50 +106,6 @@ __global__ void wide_window_kernel(WideArgs a, int j) {
     }
 }
 
-// The surrogate's fp32 cell update (H > 52; the rollout's cells are fcr_wgemm.h): from the gate pre-activations G
-// [B][4H] (torch gate order i|f|g|o): c, h; and, for the backward, the activations. tanh is the library's (a few ulp
-// RELATIVE to tanh): these memory-bound kernels can afford it, and the weight gradients need it when the hidden states
-// are small (1 - 2/(1 + e^{2x}) is only accurate to ~1e-7 absolute). V consecutive units per thread (V = 4 when
-// H % 4 == 0: 16-B accesses; V = 2 for even H, else 1).
-template <int V>
-struct WideVec {
-    typedef float F __attribute__((ext_vector_type(V)));
-    static __device__ __forceinline__ F ld(const float *p) { return *(const F *)p; }
-    static __device__ __forceinline__ void st(float *p, F v) { *(F *)p = v; }
-};
-
-template <int V>
-__global__ void wide_cell_kernel(const float *__restrict__ G, const float *__restrict__ c_prev, float *c_out,
-                                 float *h_out, float *act, int B, int H) {
-    using W = WideVec<V>;
-    const int HV = H / V;
-    const size_t iv = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (iv >= (size_t)B * HV) return;
-    const size_t b = iv / HV, u = (iv % HV) * V, idx = b * H + u;
-    const float *g4 = G + b * 4 * H + u;
-    const typename W::F gi = W::ld(g4), gf = W::ld(g4 + H), gg = W::ld(g4 + 2 * H), go = W::ld(g4 + 3 * H);
-    typename W::F cp = {}, i, f, g, o, c, h;
-    if (c_prev) cp = W::ld(c_prev + idx);
-#pragma unroll
-    for (int k = 0; k < V; ++k) {
-        i[k] = sigm(gi[k]);
-        f[k] = sigm(gf[k]);
-        g[k] = tanhf(gg[k]);
-        o[k] = sigm(go[k]);
-        c[k] = (c_prev ? f[k] * cp[k] : 0.0f) + i[k] * g[k];
-        h[k] = o[k] * tanhf(c[k]);
-    }
-    W::st(c_out + idx, c);
-    if (h_out) W::st(h_out + idx, h);
-    if (act) {
-        float *a4 = act + b * 4 * H + u;
-        W::st(a4, i);
-        W::st(a4 + H, f);
-        W::st(a4 + 2 * H, g);
-        W::st(a4 + 3 * H, o);
-    }
-}
-
 // Readout fc(h_9 of layer 2) (Functions.py:377), noise (:1400-1402), and the step's error and
 // constraint costs (:1405-1414, :1443-1452).
 // kRoLanes lanes per trajectory: each lane reads a strided slice of the trajectory's h row (the group's
@@ -267,42 +223,6 @@ __global__ void wide_head_kernel(WideArgs a, int j, float *rmh) {
 // test_wide_forget_dgates_near_their_f16_margin drives the forget row to 2 of the 9/4 this allows).
 constexpr int kWideDgExp = 13;
 static_assert((kL - 1) * (1 << kWideDgExp) / 4 < 65504, "f16 overflow of the forget-gate dgates: lower kWideDgExp");
-
-// The surrogate's fp32 backward of one cell (H > 52): from the activations, c_t, c_{t-1}, the incoming dh (carried dH
-// + din from the layer above) and the carried dc: d loss / d (gate pre-activations) into dG, dc_{t-1} into dC.
-template <int V>
-__global__ __launch_bounds__(256) void wide_cell_bwd_kernel(const float *__restrict__ act, const float *__restrict__ c,
-                                                            const float *__restrict__ c_prev, const float *__restrict__ dH,
-                                                            const float *__restrict__ din, float *dC, float *dG, int B,
-                                                            int H) {
-    using W = WideVec<V>;
-    const int HV = H / V;
-    const size_t iv = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (iv >= (size_t)B * HV) return;
-    const size_t b = iv / HV, u = (iv % HV) * V, idx = b * H + u;
-    const float *a4 = act + b * 4 * H + u;
-    const typename W::F ai = W::ld(a4), af = W::ld(a4 + H), ag = W::ld(a4 + 2 * H), ao = W::ld(a4 + 3 * H);
-    const typename W::F dhv = W::ld(dH + idx), dcv = W::ld(dC + idx), cv = W::ld(c + idx);
-    typename W::F cp = {}, dn = {}, dg[4], dco;
-    if (c_prev) cp = W::ld(c_prev + idx);
-    if (din) dn = W::ld(din + idx);
-#pragma unroll
-    for (int k = 0; k < V; ++k) {
-        const float i = ai[k], f = af[k], g = ag[k], o = ao[k];
-        const float tc = tanhf(cv[k]);
-        const float dh = dhv[k] + dn[k];
-        const float dct = dcv[k] + dh * o * (1.0f - tc * tc);
-        dg[0][k] = dct * g * i * (1.0f - i);
-        dg[1][k] = dct * cp[k] * f * (1.0f - f);
-        dg[2][k] = dct * i * (1.0f - g * g);
-        dg[3][k] = dh * tc * o * (1.0f - o);
-        dco[k] = dct * f;
-    }
-    float *d4 = dG + b * 4 * H + u;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) W::st(d4 + k * H, dg[k]);
-    W::st(dC + idx, dco);
-}
 
 // fc.W [4][H] -> [4][Hp] with zero padding units: the rollout's readout and head run at the padded size
 __global__ void wide_pad_fc_kernel(const float *__restrict__ fcw, int H, int Hp, float *__restrict__ dst) {

@@ -7,5 +7,5 @@ mkdir -p lib_ab
 git archive $REV forging-control_amd/csrc include | tar -x -C $T
 /opt/rocm/bin/hipcc -O3 -fno-slp-vectorize --offload-arch=gfx950 -std=c++17 -shared -fPIC -I $T/include \
   -I $T/forging-control_amd/csrc $T/forging-control_amd/csrc/fcr_abi.hip $T/forging-control_amd/csrc/fcr_rows.hip \
-  -o lib_ab/$NAME.so -lrocblas
+  -o lib_ab/$NAME.so
 rm -rf $T

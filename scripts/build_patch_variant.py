@@ -22,7 +22,7 @@ for f, old, new in json.load(open(spec)):
 os.makedirs(os.path.join(ROOT, "lib_ab"), exist_ok=True)
 cmd = ["/opt/rocm/bin/hipcc", "-O3", "-fno-slp-vectorize", "--offload-arch=gfx950", "-std=c++17", "-shared", "-fPIC",
        "-I", os.path.join(ROOT, "include"), "-I", src, *sys.argv[3:], os.path.join(src, "fcr_abi.hip"),
-       os.path.join(src, "fcr_rows.hip"), "-o", os.path.join(ROOT, "lib_ab", name + ".so"), "-lrocblas"]
+       os.path.join(src, "fcr_rows.hip"), "-o", os.path.join(ROOT, "lib_ab", name + ".so")]
 subprocess.check_call(cmd)
 shutil.rmtree(tmp)
 print("built lib_ab/%s.so" % name)

@@ -6,4 +6,4 @@ NAME=$1; shift
 mkdir -p lib_ab
 /opt/rocm/bin/hipcc -O3 -fno-slp-vectorize --offload-arch=gfx950 -std=c++17 -shared -fPIC -I include \
   -I forging-control_amd/csrc "$@" forging-control_amd/csrc/fcr_abi.hip forging-control_amd/csrc/fcr_rows.hip \
-  -o lib_ab/$NAME.so -lrocblas
+  -o lib_ab/$NAME.so

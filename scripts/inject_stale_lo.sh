@@ -21,7 +21,7 @@ assert s.count(a) == 1, "injection site moved"
 open(p, "w").write(s.replace(a, b))
 PY
 /opt/rocm/bin/hipcc -O3 -fno-slp-vectorize --offload-arch=gfx950 -std=c++17 -shared -fPIC -I $R/include -I $T/csrc \
-  $T/csrc/fcr_abi.hip $T/csrc/fcr_rows.hip -o $R/lib_ab/inject_stale_lo.so -lrocblas
+  $T/csrc/fcr_abi.hip $T/csrc/fcr_rows.hip -o $R/lib_ab/inject_stale_lo.so
 rm -rf $T
 exit 0
 fi
