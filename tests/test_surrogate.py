@@ -108,7 +108,8 @@ def grads_of(m):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("H,B", [(50, 256), (50, 1), (50, 4099), (7, 33), (24, 1000), (64, 100), (256, 64)])
+@pytest.mark.parametrize("H,B", [(50, 256), (50, 1), (50, 4099), (7, 33), (24, 1000), (64, 100), (256, 64), (96, 300),
+                                 (264, 40)])
 def test_gpu_training_step_matches_oracle(H, B):
     p = params_for(H, seed=H)
     x, target = batch(B, seed=B + H)
@@ -214,10 +215,12 @@ def test_gpu_full_batch_step_matches_oracle():
 
 
 @pytest.mark.gpu
-def test_gpu_rows_without_or_with_tiny_gradient():
-    """Per-row dgate scales: windows with dL/dy = 0, ~1e-30 and ~1e4 in one batch (the weight-gradient kernel
-    rescales every row to its workgroup's largest; zero rows must not set that scale)."""
-    p = ref_params()
+@pytest.mark.parametrize("H", [50, 256])
+def test_gpu_rows_without_or_with_tiny_gradient(H):
+    """Per-row dgate scales: windows with dL/dy = 0, ~1e-30 and ~1e4 in one batch (H <= 52: the weight-gradient kernel
+    rescales every row to its workgroup's largest, and zero rows must not set that scale; H > 52: the fused backward
+    cells' per-row powers of two, and the fp32 weight-gradient reductions)."""
+    p = ref_params() if H == 50 else params_for(H, seed=H)
     x, _ = batch(4099, seed=11)
     rng = np.random.default_rng(12)
     dy = rng.uniform(-1, 1, (4099, 4))
@@ -238,13 +241,14 @@ def test_gpu_rows_without_or_with_tiny_gradient():
 
 
 @pytest.mark.gpu
-def test_gpu_range_guarded_window_columns():
+@pytest.mark.parametrize("H", [50, 96])
+def test_gpu_range_guarded_window_columns(H):
     """Unscaled window columns (|x| up to 3e4 and 1e5, beyond f16's range: hi = f16(x) would be inf): the range guard
     (fcr_pack.h) runs them on x 2^-s_c against W_ih0 2^s_c and scales their weight gradients back. Against O(1) weights
     the layer-0 gates cancel terms of ~1e4, where any fp32 implementation is off fp64 by ~|W||x| 2^-24 (stock torch
     fp32: 4e-4 on W_ih0's gradient here) — so, as the rollout's test of the guard (test_gpu_parity.py), every tensor is
-    held to max(1e-5, 4 x torch fp32's own distance to fp64)."""
-    p = ref_params()
+    held to max(1e-5, 4 x torch fp32's own distance to fp64). H = 96: the wide path's window records carry the guard."""
+    p = ref_params() if H == 50 else params_for(H, seed=H)
     x, target = batch(300, seed=13)
     x[..., 0] *= 3e4
     x[..., 4] *= 1e5
