@@ -34,9 +34,10 @@ def main():
     ap.add_argument("--B", type=int, nargs="+", default=[256, 4096, 65536])
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--cpu-budget", type=float, default=5.0)
+    ap.add_argument("--hidden", type=int, default=50, help="LSTM hidden size (> 52: the wide kernels, seeded weights)")
     args = ap.parse_args()
-    from test_surrogate import ref_params, model_for, batch
-    p = ref_params()
+    from test_surrogate import params_for, model_for, batch
+    p = params_for(args.hidden, seed=args.hidden)
     for B in args.B:
         x, t = batch(B, seed=B)
         m = model_for(p)
@@ -56,7 +57,7 @@ def main():
         ms = e0.elapsed_time(e1) / args.steps
         line = {"metric": "surrogate training windows/s", "value": B / (ms * 1e-3), "unit": "windows/s",
                 "ms_per_step": ms, "dtype": "f32",
-                "config": {"workload": "LSTMModel(5,50,4,3) MSE + AdamW step", "B": B}}
+                "config": {"workload": f"LSTMModel(5,{args.hidden},4,3) MSE + AdamW step", "B": B}}
         # CPU: the reference's arithmetic (stock torch fp32 on the host), bounded
         tm = S.build(p, torch.float32)
         topt = torch.optim.AdamW(tm.parameters(), lr=1e-3, weight_decay=0.0)
