@@ -5,11 +5,11 @@
 // NeuralNetwork.train_model (Model_NN/Functions.py:520-569): forward on a (B, 10, 5) window batch,
 // loss.backward() for EVERY weight, optimizer.step().
 //
-// The step runs on the per-cell path of fcr_wide.h (gate products as rocBLAS fp32 GEMMs, the
-// pointwise cell work in HIP): the forward keeps every cell's h, c and gate activations, the backward
-// writes each layer's 10 dgate blocks into one slab so the weight gradients are ONE GEMM per weight
-// matrix with the reduction over all 10·B (window step, sample) rows:
+// H > 52 runs the rollout's wide kernels over one window (fcr_wgemm.h forward cells, fcr_wbwd.h backward cells that
+// also write each cell's dgates) and the weight gradients as ONE reduction per weight matrix over all 10·B
+// (window step, sample) rows (fcr_wgrad.h):
 //   dW_ih[l] = Σ_t dG_t^T · x_t        (k = 10·B),    dW_hh[l] = Σ_{t>=1} dG_t^T · h_{t-1}   (k = 9·B).
+// H <= 52 runs the fused cells of fcr_sur.h.
 // The kernels here are the glue: batch-first <-> time-major window transposes and the fc readout.
 #pragma once
 #include <hip/hip_runtime.h>

@@ -1,19 +1,20 @@
 // fcr_wide.h — device kernels of the rollout for hidden sizes above the LDS-resident tiers (H > 52;
 // H = 256, N = 25). There a layer's weights (4H x (in+H) fp32, 2 MB at H = 256)
-// no longer fit in LDS next to anything else, and one cell of one trajectory is a 1 MFLOP GEMV, so the
-// cell product is done batch-wide as a plain fp32 GEMM on rocBLAS (M = B trajectories) and everything
-// around it — cell update, window build, controller, readout, costs, their backward — is hand-written
-// here, one thread per (trajectory, unit) or per trajectory, batch-major so every access is coalesced.
+// no longer fit in LDS next to anything else, and one cell of one trajectory is a 1 MFLOP GEMV, so each cell
+// runs batch-wide: the gate GEMM with the cell update in its epilogue (fcr_wgemm.h), the backward cell as one fused
+// kernel (fcr_wbwd.h); everything around them — window rows, controller, readout, costs, their backward — is here,
+// one thread per trajectory (or a few lanes per trajectory), batch-major so every access is coalesced. All of it runs
+// at Hp, H padded to whole 64-unit blocks with zero-weight units (fcr_abi.hip wide_hp).
 //
-// Data (fcr_abi.hip, wide layout), all row-major with the batch index outermost inside a slice:
-//   X0  [10][B][5]        layer-0 input rows of the current window (Functions.py:1395-1396, 1433-1434)
-//   Hs, Cs [3][10][B][H]  h_t, c_t of every cell of the current window
-//   Act [3][10][B][4H]    gate pre-activations of the window (the surrogate: activations), kept for the backward
-//   G   [B][4H]           gate pre-activations (forward) / d loss / d pre-activations (backward)
-//   rowg [N+9][B][5]      d loss / d (extended window row r): every window's layer-0 input gradient
-//                         lands in rows j..j+9 — the row-gradient bookkeeping of fcr_bwd.h, batch-wide
-// The backward keeps nothing from the forward but xhat and the predictions: it recomputes each
-// window's cells (a checkpoint per window) before running that window's reverse pass.
+// Data (fcr_abi.hip WideLayout), row-major with the batch index outermost inside a slice:
+//   WR  [10][B][64] halves   layer-0 window records [hi | lo] of the current window (Functions.py:1395-1396, 1433-1434)
+//   HR  [2][10][B][2Hp]      h records [hi | lo] of two layers' cells (layer l in slot l & 1)
+//   Cs  [3][10][B][Hp]       c_t of every cell of the current window
+//   Act [3][10][B][4Hp]      gate activations i, f, g, o of every cell (the backward's dgates read them)
+//   rowg [N+9][B][5]         d loss / d (extended window row r): every window's layer-0 input gradient
+//                            lands in rows j..j+9 — the row-gradient bookkeeping of fcr_bwd.h, batch-wide
+// The backward keeps nothing from the forward but xhat, the predictions and the kept windows: it recomputes each
+// other window's cells (a checkpoint per window) before running that window's reverse pass.
 #pragma once
 #include "fcr_common.h"
 
@@ -25,7 +26,7 @@ struct WideArgs {
     const float *X, *u0, *states, *noise;
     const float *fcw, *fcb, *cwi, *cbi, *cwo;
     float *xhat, *pred, *tot, *cmd, *err;
-    float *X0, *Hs, *Cs, *Act, *G, *dH, *dC, *rowg, *dv;
+    float *Hs, *Cs, *Act, *dH, *dC, *rowg, *dv;
     const float *dloss;
     _Float16 *wr;    // split-f16 rollout: layer 0's window records [10][B][2 kWgRecX0] (hi | lo), else null
     const float *wsc;   // window-column scales of the split's range guard (fcr_pack.h)
@@ -82,10 +83,7 @@ __global__ void wide_window_kernel(WideArgs a, int j) {
     }
     for (int t = 0; t < kL; ++t) {
         float x[kIn];
-        for (int col = 0; col < kIn; ++col) {
-            x[col] = ext_row(a, b, j + t, col);
-            if (a.X0) a.X0[((size_t)t * a.B + b) * kIn + col] = x[col];
-        }
+        for (int col = 0; col < kIn; ++col) x[col] = ext_row(a, b, j + t, col);
         if (a.wr) {
             typedef _Float16 h8 __attribute__((ext_vector_type(8)));
             h8 hi = {}, lo = {};
