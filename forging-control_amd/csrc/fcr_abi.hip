@@ -252,9 +252,24 @@ int launch_sbwd_t(const BwdArgs &ba, const Layout &L, hipStream_t s) {
 // and every product they enter gains exact zeros (the H <= 52 tiers pad the same way, slot_tier). The split weights,
 // the readout's fc.W and the window-row gradient's W_ih0 are packed padded per call; the caller's tensors keep H.
 int wide_hp(int H) { return (H + kWgU - 1) / kWgU * kWgU; }
-// column blocks of the fused backward cell's [input gradient | dh_{t-1}] product (fcr_wbwd.h): the row-bound slots
-int wide_nslots(int Hp) { return (2 * Hp + kWbM - 1) / kWbM; }
-int wide_dslots(int Hp) { return (Hp + kWbM - 1) / kWbM; }   // the blocks holding the input-gradient columns [0, Hp)
+// The fused backward cell's geometry per layer (fcr_wbwd.h): 256 columns x 128 trajectories. Built with FCR_WB512=1,
+// layers >= 1 run 512 columns x 64 trajectories where that covers the [input gradient | dh_{t-1}] columns (2 Hp) in no
+// more padded columns than 256-column blocks do: each cell's dgates formed once instead of per column block, at twice
+// the A (weight) reads per trajectory; measured 3 % slower at config 5 (DESIGN.md §4 "Round 5"), so not the default.
+#ifndef FCR_WB512
+#define FCR_WB512 0
+#endif
+bool wb_wide(bool l0, int Hp) {
+    return FCR_WB512 && !l0 &&
+           (2 * Hp + WbG512::kM - 1) / WbG512::kM * WbG512::kM <= (2 * Hp + WbG256::kM - 1) / WbG256::kM * WbG256::kM;
+}
+int wb_cols(bool l0, int Hp) { return wb_wide(l0, Hp) ? WbG512::kM : WbG256::kM; }
+// row-bound slots: one per column block of the writing launch (every block writes its slot, 0 where it has no such
+// columns). dh of layer l: its own cells' [0, 2 Hp) (layer 0: [0, Hp)); the input gradient: layer l + 1's [0, Hp)
+int wb_hslots(int l, int Hp) { return ((l ? 2 * Hp : Hp) + wb_cols(l == 0, Hp) - 1) / wb_cols(l == 0, Hp); }
+int wb_dslots(int Hp) { return (Hp + wb_cols(false, Hp) - 1) / wb_cols(false, Hp); }
+// the slots allocated: the most any geometry writes
+int wide_nslots(int Hp) { return (2 * Hp + WbG256::kM - 1) / WbG256::kM; }
 
 struct WideLayout {
     int Hp, ns, keep, ctrl_blocks;
@@ -471,22 +486,32 @@ int launch_wgemm_cell(const WgArgs &wa, hipStream_t s) {
 // One backward cell of the fused path (fcr_wbwd.h): dgates formed in the product's prologue, out = dG [W_ih | W_hh]
 // (columns [0, NO), NO = 0: the dgate part only) in true units
 int launch_fb(const WbArgs &wa, bool l0, hipStream_t s) {
-    static std::atomic<unsigned long long> attr_done[3] = {{0}, {0}, {0}};
-    const bool w0g = l0 && wa.H > kWbW0LdsUnits;
-    const int kind = l0 ? (w0g ? 2 : 1) : 0;
-    const void *fn = kind == 0 ? (const void *)wide_bwd_fused_kernel<false>
-                     : kind == 1 ? (const void *)wide_bwd_fused_kernel<true, false>
-                                 : (const void *)wide_bwd_fused_kernel<true, true>;
-    if (const int rc = lds_attr(fn, kWbLds, attr_done[kind], "wbwd")) return rc;
+    static std::atomic<unsigned long long> attr_done[4] = {{0}, {0}, {0}, {0}};
+    const bool w0g = l0 && wa.H > kWbW0LdsUnits, wide = wb_wide(l0, wa.H);
+    const int kind = l0 ? (w0g ? 2 : 1) : (wide ? 3 : 0);
+    const void *fn = kind == 0   ? (const void *)wide_bwd_fused_kernel<WbG256, false>
+                     : kind == 1 ? (const void *)wide_bwd_fused_kernel<WbG256, true, false>
+#if FCR_WB512
+                     : kind == 3 ? (const void *)wide_bwd_fused_kernel<WbG512, false>
+#endif
+                                 : (const void *)wide_bwd_fused_kernel<WbG256, true, true>;
+    if (const int rc = lds_attr(fn, wide ? kWbLds512 : kWbLds256, attr_done[kind], "wbwd")) return rc;
     if (wa.NO < 0 || wa.NO > 2 * wa.H || wa.NO % 4 || wa.H % 8 || wa.NB <= 0 || wa.ldo % 4 || wa.ldh % 4 ||
         wa.ldx % 4 || wa.nrh < 1 || (wa.rm_d && wa.nrd < 1) || (l0 && (!wa.wih0 || !wa.rowg)))
         return fail(FCR_EINVAL, "wide_bwd_fused_kernel: NO %d H %d B %d ldo %d off its tiling", wa.NO, wa.H, wa.NB, wa.ldo);
-    const int nx = (wa.NB + kWbN - 1) / kWbN, ny = wa.NO > 0 ? (wa.NO + kWbM - 1) / kWbM : 1;
-    const int lds = wb_lds_bytes(l0, wa.H);
-    if (kind == 0) hipLaunchKernelGGL((wide_bwd_fused_kernel<false>), dim3((unsigned)(nx * ny)), dim3(kWbThreads), lds, s, wa);
+    const int M = wide ? WbG512::kM : WbG256::kM, N = wide ? WbG512::kN : WbG256::kN;
+    const dim3 grid((unsigned)((wa.NB + N - 1) / N * (wa.NO > 0 ? (wa.NO + M - 1) / M : 1)));
+#if FCR_WB512
+    if (kind == 3)
+        hipLaunchKernelGGL((wide_bwd_fused_kernel<WbG512, false>), grid, dim3(WbG512::kThreads), wb_lds_bytes<WbG512>(false, wa.H), s, wa);
+    else
+#endif
+    if (kind == 0)
+        hipLaunchKernelGGL((wide_bwd_fused_kernel<WbG256, false>), grid, dim3(WbG256::kThreads), wb_lds_bytes<WbG256>(false, wa.H), s, wa);
     else if (kind == 1)
-        hipLaunchKernelGGL((wide_bwd_fused_kernel<true, false>), dim3((unsigned)(nx * ny)), dim3(kWbThreads), lds, s, wa);
-    else hipLaunchKernelGGL((wide_bwd_fused_kernel<true, true>), dim3((unsigned)(nx * ny)), dim3(kWbThreads), lds, s, wa);
+        hipLaunchKernelGGL((wide_bwd_fused_kernel<WbG256, true, false>), grid, dim3(WbG256::kThreads), wb_lds_bytes<WbG256>(true, wa.H), s, wa);
+    else
+        hipLaunchKernelGGL((wide_bwd_fused_kernel<WbG256, true, true>), grid, dim3(WbG256::kThreads), wb_lds_bytes<WbG256>(true, wa.H), s, wa);
     return launch_check("wide_bwd_fused_kernel");
 }
 
@@ -690,7 +715,7 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
                   const float *dloss, float *g_u0, float *g_w_inp, float *g_b_inp, float *g_w_out, char *base,
                   size_t ws_bytes, hipStream_t s) {
     const WideLayout L = make_wide(d, 1, wide_keep_fit(d, ws_bytes));
-    const int B = d->B, Hp = L.Hp, ns = L.ns, nd = wide_dslots(Hp);
+    const int B = d->B, Hp = L.Hp, ns = L.ns, nd = wb_dslots(Hp);
     const size_t cell = (size_t)B * Hp;
     const int nb = (B + 255) / 256;
     int rc;
@@ -751,7 +776,7 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
                 // dh's bound: the head's one slot at t = 9 (zeroed for layers below 2, whose dh_9 is 0), else the
                 // column blocks of cell t + 1's product
                 wa.rm_h = RMh + (size_t)((t + 1) & 1) * ns * B;
-                wa.nrh = t == kL - 1 ? 1 : (l > 0 ? ns : nd);
+                wa.nrh = t == kL - 1 ? 1 : wb_hslots(l, Hp);
                 wa.rm_h_out = t > 0 ? RMh + (size_t)(t & 1) * ns * B : nullptr;
                 wa.rm_d = l < kLayers - 1 ? RMd + ((size_t)((l + 1) & 1) * kL + t) * ns * B : nullptr;
                 wa.nrd = nd;
@@ -949,7 +974,7 @@ int surw_wgrad(const float *A, long long n, int Hp, int H, int K, const float *X
 int surw_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, float *const *g_w_ih, float *const *g_w_hh,
                   float *g_fc_w, float *g_fc_b, float *g_x, char *base, hipStream_t s) {
     const SurWideLayout L = make_surw(d, 1);
-    const int B = d->B, H = d->H, Hp = L.Hp, ns = L.ns, nd = wide_dslots(Hp);
+    const int B = d->B, H = d->H, Hp = L.Hp, ns = L.ns, nd = wb_dslots(Hp);
     const size_t cell = (size_t)B * Hp;
     int rc;
     auto grid = [](size_t n) { return dim3((unsigned)((n + 255) / 256)); };
@@ -1010,7 +1035,7 @@ int surw_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, floa
             wa.rm_c = RMc + (size_t)((t + 1) & 1) * B;
             wa.rm_c_out = t > 0 ? RMc + (size_t)(t & 1) * B : nullptr;
             wa.rm_h = RMh + (size_t)((t + 1) & 1) * ns * B;
-            wa.nrh = t == kL - 1 ? 1 : (l > 0 ? ns : nd);
+            wa.nrh = t == kL - 1 ? 1 : wb_hslots(l, Hp);
             wa.rm_h_out = t > 0 ? RMh + (size_t)(t & 1) * ns * B : nullptr;
             wa.rm_d = l < kLayers - 1 ? RMd + ((size_t)((l + 1) & 1) * kL + t) * ns * B : nullptr;
             wa.nrd = nd;

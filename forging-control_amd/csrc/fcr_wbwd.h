@@ -33,29 +33,42 @@
 
 namespace fcr {
 
-constexpr int kWbM = 256;                 // output columns per workgroup
-constexpr int kWbN = 128;                 // trajectories per workgroup
 constexpr int kWbK = 32;                  // k per step (8 units x 4 gates)
-constexpr int kWbProd = 4, kWbCons = 4;   // producer (dgate) waves, consumer (MFMA) waves
-constexpr int kWbWaves = kWbProd + kWbCons;
-constexpr int kWbTM = kWbM / kWbCons / 16, kWbTN = kWbN / 16;   // D tiles per consumer wave: 4 x 8
-constexpr int kWbThreads = 64 * kWbWaves;
-constexpr int kWbUnits = 4;               // units per producer thread and K step (two threads per trajectory row)
-constexpr int kWbStageA = kWbM * kWbK * 2;                // bytes of one split half of A
-constexpr int kWbStage = 2 * kWbStageA;                   // hi A | lo A
-constexpr int kWbTileB = kWbN * kWbK * 2;                 // one split half of the dgate tile
-constexpr int kWbPieces = kWbStage / 1024 / kWbCons;      // LDS-DMA pieces per consumer wave per stage
-constexpr int kWbOffB = 2 * kWbStage;                     // [A stage 0 | A stage 1 | B tile 0 hi, lo | B tile 1 ...]
-constexpr int kWbOffDown = kWbOffB + 4 * kWbTileB;
-constexpr int kWbOffW0 = kWbOffDown + kWbN * 4;           // layer 0: W_ih0 as [unit][gate][kIn]
+constexpr int kWbProd = 4;                // producer (dgate) waves
+
+// Workgroup geometry: M output columns x N trajectories, 4 producer and CONS consumer waves, U units per producer
+// thread and K step (8 / U threads per trajectory row).
+template <int M, int N, int CONS, int U>
+struct WbGeo {
+    static constexpr int kM = M, kN = N, kCons = CONS, kUnits = U;
+    static constexpr int kWaves = kWbProd + CONS, kThreads = 64 * kWaves;
+    static constexpr int kTM = M / CONS / 16, kTN = N / 16;   // D tiles per consumer wave
+    static constexpr int kPPR = 8 / U;                          // producer threads per trajectory row
+    static constexpr int kStageA = M * kWbK * 2;                // bytes of one split half of A
+    static constexpr int kStage = 2 * kStageA;                  // hi A | lo A
+    static constexpr int kTileB = N * kWbK * 2;                 // one split half of the dgate tile
+    static constexpr int kPieces = kStage / 1024 / CONS;        // LDS-DMA pieces per consumer wave per stage
+    static constexpr int kHalfPieces = kStageA / 1024;
+    static constexpr int kOffB = 2 * kStage;                    // [A stage 0 | A stage 1 | B tile 0 hi, lo | B tile 1 ...]
+    static constexpr int kOffDown = kOffB + 4 * kTileB;
+    static constexpr int kOffW0 = kOffDown + N * 4;             // layer 0: W_ih0 as [unit][gate][kIn]
+    static_assert(kStage % (1024 * CONS) == 0, "DMA pieces");
+    static_assert(64 * kWbProd * U == 8 * N, "dgate mapping: a step's 8 units of every row over the producers");
+    static_assert(U == 2 || U == 4, "units per producer thread");
+};
+// 256 columns x 128 trajectories, 4 + 4 waves (round 4): every layer; two column blocks at Hp = 256 form the same dgates
+using WbG256 = WbGeo<256, 128, 4, 4>;
+// 512 columns x 64 trajectories, 4 + 8 waves: a layer >= 1 cell's whole [input gradient | dh_{t-1}] at Hp = 256 in one
+// workgroup, so its dgates are formed (and its rows read) once
+using WbG512 = WbGeo<512, 64, 8, 2>;
 constexpr int kWbW0LdsUnits = 768;                        // layer 0 with H above: W_ih0 read from global memory
-constexpr int kWbLds = kWbOffW0 + 4 * kWbW0LdsUnits * kIn * 4;
-static_assert(kWbStage % (1024 * kWbCons) == 0, "DMA pieces");
-static_assert(64 * kWbProd * kWbUnits == 8 * kWbN, "dgate mapping: a step's 8 units of every row over the producers");
-static_assert(kWbLds <= 163840, "LDS");
+constexpr int kWbLds256 = WbG256::kOffW0 + 4 * kWbW0LdsUnits * kIn * 4;
+constexpr int kWbLds512 = WbG512::kOffW0;                 // (layers >= 1 only: no W_ih0 block)
+static_assert(kWbLds256 <= 163840 && kWbLds512 <= 163840, "LDS");
 // LDS bytes of one launch: the W_ih0 block only for layer 0 with H <= kWbW0LdsUnits
+template <class G>
 __host__ __device__ constexpr int wb_lds_bytes(bool l0, int H) {
-    return kWbOffW0 + (l0 && H <= kWbW0LdsUnits ? 4 * H * kIn * 4 : 0);
+    return G::kOffW0 + (l0 && H <= kWbW0LdsUnits ? 4 * H * kIn * 4 : 0);
 }
 
 struct WbArgs {
@@ -86,15 +99,23 @@ struct WbArgs {
 // on distinct 16-B slots of a 128-B bank line (fcr_wgemm.h wg_off)
 __device__ __forceinline__ uint32_t wb_off(int r, int c) { return (uint32_t)(r * 64 + ((c ^ ((r >> 1) & 3)) << 4)); }
 
-// one step's inputs of a producer thread: four consecutive units of one trajectory
+// one step's inputs of a producer thread: U consecutive units of one trajectory
+template <int U>
 struct WbIn {
-    f32x4 pi, pf, pg, po, cp, dh, dn, dc;
+    typedef float fU __attribute__((ext_vector_type(U)));
+    fU pi, pf, pg, po, cp, dh, dn, dc;
 };
 
 // W0G: layer 0 at H > kWbW0LdsUnits reads W_ih0 from global memory (L1 / L2: every producer thread of a workgroup
-// reads the same 320 B per step) instead of staging it in LDS
-template <bool L0, bool W0G = false>
-__global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a) {
+// reads the same bytes per step) instead of staging it in LDS
+template <class G, bool L0, bool W0G = false>
+__global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a) {
+    constexpr int kWbM = G::kM, kWbN = G::kN, kWbCons = G::kCons, kWbUnits = G::kUnits, kWbTM = G::kTM,
+                  kWbTN = G::kTN, kWbThreads = G::kThreads, kWbStageA = G::kStageA, kWbStage = G::kStage,
+                  kWbTileB = G::kTileB, kWbPieces = G::kPieces, kWbOffB = G::kOffB, kWbOffDown = G::kOffDown,
+                  kWbOffW0 = G::kOffW0, kPPR = G::kPPR;
+    using In = WbIn<kWbUnits>;
+    using fU = typename In::fU;
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -104,15 +125,15 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a)
     const bool prod = a.NO > 0;
     const int ny = prod ? (a.NO + kWbM - 1) / kWbM : 1, total = gridDim.x, id = blockIdx.x;
     // XCD-aware order: consecutive ids go to different XCDs; each XCD's ids are renumbered contiguously and walk the
-    // column blocks fastest, so a trajectory block's two column blocks read its rows once into that XCD's L2
+    // column blocks fastest, so a trajectory block's column blocks read its rows once into that XCD's L2
     const int xcd = id & 7, loc = id >> 3, q8 = total >> 3, rr = total & 7;
     const int wg = (xcd < rr ? xcd * (q8 + 1) : rr * (q8 + 1) + (xcd - rr) * q8) + loc;
     const int cb = wg % ny;                                 // column block
     const int m0 = cb * kWbM;                               // first output column
     const int b0 = (wg / ny) * kWbN;                        // first trajectory
 
-    // ---- producer thread: its dgate row and unit half; the row's scale from the producers' bounds ----
-    const int er = (tid >> 1) & (kWbN - 1), ep = tid & 1;   // (consumers: unused)
+    // ---- producer thread: its dgate row and unit share; the row's scale from the producers' bounds ----
+    const int er = (tid / kPPR) & (kWbN - 1), ep = tid % kPPR;   // (consumers: unused)
     const int eb = b0 + er < a.NB ? b0 + er : a.NB - 1;    // tail rows recompute the last trajectory (not stored)
     const bool elive = b0 + er < a.NB;
     float up = 0.0f;
@@ -134,7 +155,7 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a)
     }
     const float *w0l = W0G ? a.wih0 : w0s;
 
-    // ---- consumers: A by LDS-DMA pieces (16 rows x 64 B of [A hi (16 pieces) | A lo (16)]; lane i lands at +16 i).
+    // ---- consumers: A by LDS-DMA pieces (16 rows x 64 B of [A hi | A lo]; lane i lands at +16 i).
     // Issued from inline asm: with the intrinsic anywhere in the kernel the compiler's wait insertion drains every
     // outstanding load (vmcnt(0)) before the use of a prefetched value, the producers' included. The step barrier's
     // vmcnt(0) retires each consumer's own pieces. M0 carries the wave's LDS base; nothing else in the kernel uses it.
@@ -143,8 +164,8 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a)
 #pragma unroll
     for (int q = 0; q < kWbPieces; ++q) {
         const int j = (producer ? 0 : cw) + kWbCons * q;
-        const bool lo = j >= 16;
-        const int r = 16 * (lo ? j - 16 : j) + (lane >> 2);
+        const bool lo = j >= G::kHalfPieces;
+        const int r = 16 * (lo ? j - G::kHalfPieces : j) + (lane >> 2);
         const int c = (lane & 3) ^ ((r >> 1) & 3);
         int n = m0 + r;
         if (n >= a.NO) n = a.NO > 0 ? a.NO - 1 : 0;        // tail columns recompute the last one (not stored)
@@ -164,33 +185,33 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a)
         }
     };
 
-    // ---- producers: inputs one step ahead, the tile one step ahead of the MFMAs ----
+    // ---- producers: inputs ahead, the tile one step ahead of the MFMAs ----
     const float *pre = a.act + (size_t)eb * K;
     const float *cpr = a.c_prev ? a.c_prev + (size_t)eb * H : nullptr;
     const float *dhr = a.dh + (size_t)eb * a.ldh;
     const float *dnr = a.din ? a.din + (size_t)eb * a.ldx : nullptr;
     const float *dcr = a.dC + (size_t)eb * H;
     float *dco_r = a.dC_out + (size_t)eb * H;
-    auto ld4 = [](const float *p) { return *reinterpret_cast<const f32x4 *>(p); };
+    auto ldu = [](const float *p) { return *reinterpret_cast<const fU *>(p); };
     auto load_in = [&](int s) {
-        WbIn x;
+        In x;
         const int u = 8 * s + kWbUnits * ep;
-        x.pi = ld4(pre + u);
-        x.pf = ld4(pre + H + u);
-        x.pg = ld4(pre + 2 * H + u);
-        x.po = ld4(pre + 3 * H + u);
-        x.cp = cpr ? ld4(cpr + u) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        x.dh = ld4(dhr + u);
-        x.dn = dnr ? ld4(dnr + u) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        x.dc = ld4(dcr + u);
+        x.pi = ldu(pre + u);
+        x.pf = ldu(pre + H + u);
+        x.pg = ldu(pre + 2 * H + u);
+        x.po = ldu(pre + 3 * H + u);
+        x.cp = cpr ? ldu(cpr + u) : fU{};
+        x.dh = ldu(dhr + u);
+        x.dn = dnr ? ldu(dnr + u) : fU{};
+        x.dc = ldu(dcr + u);
         return x;
     };
-    const bool wr_dc = cb == 0 && elive;   // both column blocks form the same dc_{t-1}: the first stores it
+    const bool wr_dc = cb == 0 && elive;   // every column block forms the same dc_{t-1}: the first stores it
     float mdc = 0.0f;                      // max |dc_{t-1}| of this thread's units
     float pc[kIn] = {};                    // layer 0: this thread's share of the window-row gradient
-    auto dgates = [&](int s, const WbIn &x, int buf) {
+    auto dgates = [&](int s, const In &x, int buf) {
         float dg[4 * kWbUnits];
-        f32x4 dco;
+        fU dco;
         const int u = 8 * s + kWbUnits * ep;
 #pragma unroll
         for (int k = 0; k < kWbUnits; ++k) {
@@ -205,17 +226,21 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a)
             dg[4 * k + 3] = dh * tc * (o - o * o);
             dco[k] = dct * f;
         }
-        if (wr_dc) *reinterpret_cast<f32x4 *>(dco_r + u) = dco;
+        if (wr_dc) *reinterpret_cast<fU *>(dco_r + u) = dco;
         if (a.dg && wr_dc) {   // (column block 0 writes them: every block forms the same)
             float *d = a.dg + (size_t)eb * K + u;
 #pragma unroll
-            for (int g = 0; g < 4; ++g)
-                *reinterpret_cast<f32x4 *>(d + g * H) = f32x4{dg[g], dg[4 + g], dg[8 + g], dg[12 + g]};
+            for (int g = 0; g < 4; ++g) {
+                fU v;
+#pragma unroll
+                for (int k = 0; k < kWbUnits; ++k) v[k] = dg[4 * k + g];
+                *reinterpret_cast<fU *>(d + g * H) = v;
+            }
         }
 #pragma unroll
         for (int k = 0; k < kWbUnits; ++k) mdc = fmaxf(mdc, fabsf(dco[k]));
-        if constexpr (L0) {   // sum_r dG[b][r] W_ih0[r][c] over this thread's 16 gate rows, fp32
-            const f32x4 *w4 = reinterpret_cast<const f32x4 *>(w0l + u * 4 * kIn);   // 80 floats: units u .. u + 3
+        if constexpr (L0) {   // sum_r dG[b][r] W_ih0[r][c] over this thread's 4 U gate rows, fp32
+            const f32x4 *w4 = reinterpret_cast<const f32x4 *>(w0l + u * 4 * kIn);   // 20 U floats: units u .. u + U - 1
 #pragma unroll
             for (int q = 0; q < kWbUnits * 4 * kIn / 4; ++q) {
                 const f32x4 wq = w4[q];
@@ -227,25 +252,38 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a)
             }
         }
         if (prod) {
-            // the split (fcr_f16.h mix_pair): hi = f16(up dg), lo = f16(up dg - hi); units 4 ep .. of the row's 8
+            // the split (fcr_f16.h mix_pair): hi = f16(up dg), lo = f16(up dg - hi); this thread's U units of the row's 8
+            // are 16-B chunks U / 2 * ep .. of the row
             typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            unsigned hw[8], lw[8];
+            constexpr int NW = 2 * kWbUnits;   // 32-bit words of halves
+            unsigned hw[NW], lw[NW];
 #pragma unroll
-            for (int p = 0; p < 8; ++p) mix_pair(dg[2 * p], up, dg[2 * p + 1], up, hw[p], lw[p]);
+            for (int p = 0; p < NW; ++p) mix_pair(dg[2 * p], up, dg[2 * p + 1], up, hw[p], lw[p]);
             char *bt = lds + kWbOffB + buf * 2 * kWbTileB;
-            const uint32_t o0 = wb_off(er, 2 * ep), o1 = wb_off(er, 2 * ep + 1);
-            *reinterpret_cast<u32x4 *>(bt + o0) = u32x4{hw[0], hw[1], hw[2], hw[3]};
-            *reinterpret_cast<u32x4 *>(bt + o1) = u32x4{hw[4], hw[5], hw[6], hw[7]};
-            *reinterpret_cast<u32x4 *>(bt + kWbTileB + o0) = u32x4{lw[0], lw[1], lw[2], lw[3]};
-            *reinterpret_cast<u32x4 *>(bt + kWbTileB + o1) = u32x4{lw[4], lw[5], lw[6], lw[7]};
+#pragma unroll
+            for (int c = 0; c < kWbUnits / 2; ++c) {
+                const uint32_t o = wb_off(er, kWbUnits / 2 * ep + c);
+                *reinterpret_cast<u32x4 *>(bt + o) = u32x4{hw[4 * c], hw[4 * c + 1], hw[4 * c + 2], hw[4 * c + 3]};
+                *reinterpret_cast<u32x4 *>(bt + kWbTileB + o) = u32x4{lw[4 * c], lw[4 * c + 1], lw[4 * c + 2], lw[4 * c + 3]};
+            }
         }
     };
 
     // The two roles run separate loops with the same barriers (one per K step, plus the prologue's and the
-    // epilogue's): a shared loop would keep the consumers' 128 accumulator registers live in the producers too.
+    // epilogue's): a shared loop would keep the consumers' accumulator registers live in the producers too.
     auto barrier = [] { asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
     const float *ldown = reinterpret_cast<const float *>(lds + kWbOffDown);
-    float *red = reinterpret_cast<float *>(lds);   // epilogue: [cw][128 rows][2] (the A stages are retired)
+    float *red = reinterpret_cast<float *>(lds);   // epilogue: [cw][kWbN rows][2] (the A stages are retired)
+    auto row_sum = [](float v) {   // over the kPPR producer threads of a row (consecutive lanes)
+#pragma unroll
+        for (int o = 1; o < kPPR; o <<= 1) v += __shfl_xor(v, o);
+        return v;
+    };
+    auto row_max = [](float v) {
+#pragma unroll
+        for (int o = 1; o < kPPR; o <<= 1) v = fmaxf(v, __shfl_xor(v, o));
+        return v;
+    };
     if (producer) {
         // a producer's barrier waits only for its LDS tile writes: its input loads stay in flight across it, and the
         // compiler's own wait before their first use (exact counts: no DMA intrinsic in the kernel) is all
@@ -253,12 +291,12 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a)
         if constexpr (!L0) {
             // inputs three steps ahead in rotating register sets (unrolled by three: a copy between sets would wait
             // for the loads)
-            WbIn x0 = load_in(0), x1, x2;
+            In x0 = load_in(0), x1, x2;
             if (nk > 1) x1 = load_in(1);
             if (nk > 2) x2 = load_in(2);
             barrier();   // W_ih0 and the row scales in LDS
             dgates(0, x0, 0);
-            auto pstep = [&](auto full, int ks, const WbIn &xuse, WbIn &xload) {
+            auto pstep = [&](auto full, int ks, const In &xuse, In &xload) {
                 constexpr bool FULL = decltype(full)::value;   // ks + 3 < nk: nothing conditional in the step
                 pbarrier();                                    // tile ks published
                 if (FULL || ks + 3 < nk) xload = load_in(ks + 3);
@@ -279,24 +317,24 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a)
             if (ks + 4 < nk) pstep(Tail{}, ks + 4, x2, x1);
         } else {
             // layer 0 (the window-row gradient's W_ih0 reads and accumulators) has registers for one set ahead
-            WbIn xc = load_in(0);
+            In xc = load_in(0);
             barrier();
             dgates(0, xc, 0);
             if (nk > 1) xc = load_in(1);
             for (int ks = 0; ks < nk; ++ks) {
                 pbarrier();
-                WbIn xn;
+                In xn;
                 if (ks + 2 < nk) xn = load_in(ks + 2);
                 if (ks + 1 < nk) dgates(ks + 1, xc, (ks & 1) ^ 1);
                 if (ks + 2 < nk) xc = xn;
             }
         }
         // per-row results: dc_{t-1} bound, layer 0's window-row gradient
-        mdc = fmaxf(mdc, __shfl_xor(mdc, 1));
+        mdc = row_max(mdc);
         if (a.rm_c_out && wr_dc && ep == 0) a.rm_c_out[eb] = mdc;
         if constexpr (L0) {
 #pragma unroll
-            for (int c = 0; c < kIn; ++c) pc[c] += __shfl_xor(pc[c], 1);
+            for (int c = 0; c < kIn; ++c) pc[c] = row_sum(pc[c]);
             if (a.rowg && elive && cb == 0 && ep == 0)
 #pragma unroll
                 for (int c = 0; c < kIn; ++c) a.rowg[(size_t)eb * kIn + c] += pc[c];
@@ -369,7 +407,7 @@ __global__ __launch_bounds__(kWbThreads, 1) void wide_bwd_fused_kernel(WbArgs a)
         barrier();
         return;
     }
-    // the producers (threads 0 .. 127 of them) reduce the consumers' row maxima over the column slices
+    // the producers (threads 0 .. kWbN - 1 of them) reduce the consumers' row maxima over the column slices
     if (tid < kWbN && b0 + tid < a.NB) {
         float mh = 0.0f, md = 0.0f;
 #pragma unroll
