@@ -52,7 +52,7 @@ def hbm_bytes_per_rollout_step(N=10):
 def pmc_traffic(kernel, suffix=""):
     """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of this workload
     (profiles/round<k><suffix>_pmc.json, scripts/profile_round.sh; older profiles/r<k>_pmc.json otherwise), or
-    None. suffix "_c5": config 5's summary, whose "bwd_pass" entry is the HBM bytes of one whole backward pass."""
+    None. suffix "_c3f16" / "_c3fp32": config 3's summaries (scripts/profile.sh c3 / c3f16); "_c5": config 5's summary, whose "bwd_pass" entry is the HBM bytes of one whole backward pass."""
     import glob
     import re
     pick = []
@@ -443,7 +443,9 @@ def main():
         hbm_roof = HBM_PEAK_GBS * 1e9 / hbm_bytes_per_rollout_step(N)
         default_cfg = (B, N, H, args.precision) == (65536, 10, 50, "fp32")
         c5_cfg = (B, N, H, args.precision) == (65536, 25, 256, "fp32")
+        c3_cfg = (B, N, H) == (262144, 10, 50)   # config 3 in either precision: its own PMC summary
         traffic, traffic_src = (pmc_traffic(f"fcr_{dom[0]}_kernel") if default_cfg else
+                                pmc_traffic(f"fcr_{dom[0]}_kernel", f"_c3{args.precision}") if c3_cfg else
                                 pmc_traffic("bwd_pass", "_c5") if c5_cfg and dom[0] == "bwd" else (None, None))
         # ceiling of the arithmetic as executed: an fp32-accurate product is three f16 MFMA products
         # (hi.hi + hi.lo + lo.hi, fcr_f16.h), so the fp32-equivalent ceiling is the f16 peak / 3;
