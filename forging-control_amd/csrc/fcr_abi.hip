@@ -497,7 +497,7 @@ int launch_fb(const WbArgs &wa, bool l0, hipStream_t s) {
                                  : (const void *)wide_bwd_fused_kernel<WbG256, true, true>;
     if (const int rc = lds_attr(fn, wide ? kWbLds512 : kWbLds256, attr_done[kind], "wbwd")) return rc;
     if (wa.NO < 0 || wa.NO > 2 * wa.H || wa.NO % 4 || wa.H % 8 || wa.NB <= 0 || wa.ldo % 4 || wa.ldh % 4 ||
-        wa.ldx % 4 || wa.nrh < 1 || (wa.rm_d && wa.nrd < 1) || (l0 && (!wa.wih0 || !wa.rowg)))
+        wa.ldx % 4 || (wa.rm_h && wa.nrh < 1) || (wa.rm_d && wa.nrd < 1) || (l0 && (!wa.wih0 || !wa.rowg)))
         return fail(FCR_EINVAL, "wide_bwd_fused_kernel: NO %d H %d B %d ldo %d off its tiling", wa.NO, wa.H, wa.NB, wa.ldo);
     const int M = wide ? WbG512::kM : WbG256::kM, N = wide ? WbG512::kN : WbG256::kN;
     const dim3 grid((unsigned)((wa.NB + N - 1) / N * (wa.NO > 0 ? (wa.NO + M - 1) / M : 1)));
@@ -747,17 +747,13 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
             if ((rc = wide_window_cells(a, L, base, true, s))) return rc;   // checkpoint: recompute the window
         }
         for (int l = kLayers - 1; l >= 0; --l) {
-            if (l < kLayers - 1 && hipMemsetAsync(a.dH, 0, sizeof(float) * cell, s) != hipSuccess)
-                return fail(FCR_EHIP, "hipMemsetAsync failed");
-            if (hipMemsetAsync(DC[0], 0, sizeof(float) * cell, s) != hipSuccess ||
-                hipMemsetAsync(RMc, 0, sizeof(float) * B, s) != hipSuccess ||
-                (l < kLayers - 1 && hipMemsetAsync(RMh, 0, sizeof(float) * B, s) != hipSuccess))
-                return fail(FCR_EHIP, "hipMemsetAsync failed");
             for (int t = kL - 1; t >= 0; --t) {
                 const size_t c_off = ((size_t)l * kL + t) * cell;
                 // dh_t below t = 9 comes from cell t+1's product: layer 0 columns 0..Hp-1 of E0, layers >= 1 columns
                 // Hp..2Hp-1 of D[l-1] row t+1; the layer above's input gradient from D[l] row t
-                const float *dh_src = t == kL - 1 ? a.dH : l == 0 ? E0 : D[l - 1] + (size_t)(t + 1) * 2 * cell + Hp;
+                // (t = 9: the head's dh for layer 2, zero below it, passed as null like the zero dc_9 and their bounds)
+                const bool top9 = t == kL - 1 && l == kLayers - 1, zero9 = t == kL - 1 && l < kLayers - 1;
+                const float *dh_src = top9 ? a.dH : zero9 ? nullptr : l == 0 ? E0 : D[l - 1] + (size_t)(t + 1) * 2 * cell + Hp;
                 WbArgs wa{};
                 wa.Ahi = (const _Float16 *)(base + L.bt[l]);
                 wa.Alo = wa.Ahi + (size_t)(l == 0 ? Hp : 2 * Hp) * 4 * Hp;
@@ -769,13 +765,13 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
                 wa.ldh = t == kL - 1 || l == 0 ? Hp : 2 * Hp;
                 wa.din = l < kLayers - 1 ? D[l] + (size_t)t * 2 * cell : nullptr;
                 wa.ldx = 2 * Hp;
-                wa.dC = DC[(t + 1) & 1];   // t = 9 reads buffer 0 (zeroed above), t writes buffer t & 1
+                wa.dC = t == kL - 1 ? nullptr : DC[(t + 1) & 1];   // t writes buffer t & 1
                 wa.dC_out = DC[t & 1];
-                wa.rm_c = RMc + (size_t)((t + 1) & 1) * B;
+                wa.rm_c = t == kL - 1 ? nullptr : RMc + (size_t)((t + 1) & 1) * B;
                 wa.rm_c_out = t > 0 ? RMc + (size_t)(t & 1) * B : nullptr;
-                // dh's bound: the head's one slot at t = 9 (zeroed for layers below 2, whose dh_9 is 0), else the
-                // column blocks of cell t + 1's product
-                wa.rm_h = RMh + (size_t)((t + 1) & 1) * ns * B;
+                // dh's bound: the head's one slot at t = 9 (none below layer 2), else the column blocks of cell t + 1's
+                // product
+                wa.rm_h = zero9 ? nullptr : RMh + (size_t)((t + 1) & 1) * ns * B;
                 wa.nrh = t == kL - 1 ? 1 : wb_hslots(l, Hp);
                 wa.rm_h_out = t > 0 ? RMh + (size_t)(t & 1) * ns * B : nullptr;
                 wa.rm_d = l < kLayers - 1 ? RMd + ((size_t)((l + 1) & 1) * kL + t) * ns * B : nullptr;
@@ -1012,11 +1008,6 @@ int surw_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, floa
     const _Float16 *HR = (const _Float16 *)(base + L.HR);
     if (hipMemsetAsync(rowg, 0, sizeof(float) * kL * B * kIn, s) != hipSuccess) return fail(FCR_EHIP, "hipMemsetAsync failed");
     for (int l = kLayers - 1; l >= 0; --l) {
-        if ((l < kLayers - 1 && hipMemsetAsync(dH, 0, sizeof(float) * cell, s) != hipSuccess) ||
-            hipMemsetAsync(DC[0], 0, sizeof(float) * cell, s) != hipSuccess ||
-            hipMemsetAsync(RMc, 0, sizeof(float) * B, s) != hipSuccess ||
-            (l < kLayers - 1 && hipMemsetAsync(RMh, 0, sizeof(float) * B, s) != hipSuccess))
-            return fail(FCR_EHIP, "hipMemsetAsync failed");
         for (int t = kL - 1; t >= 0; --t) {   // the rollout's backward cells (wide_backward), one window
             const size_t c_off = ((size_t)l * kL + t) * cell;
             WbArgs wa{};
@@ -1026,15 +1017,16 @@ int surw_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, floa
             wa.H = Hp;
             wa.act = Act + c_off * 4;
             wa.c_prev = t > 0 ? Cs + c_off - cell : nullptr;
-            wa.dh = t == kL - 1 ? dH : l == 0 ? E0 : D[l - 1] + (size_t)(t + 1) * 2 * cell + Hp;
+            const bool zero9 = t == kL - 1 && l < kLayers - 1;   // dh_9 below the top layer: zero (null)
+            wa.dh = t == kL - 1 ? (zero9 ? nullptr : dH) : l == 0 ? E0 : D[l - 1] + (size_t)(t + 1) * 2 * cell + Hp;
             wa.ldh = t == kL - 1 || l == 0 ? Hp : 2 * Hp;
             wa.din = l < kLayers - 1 ? D[l] + (size_t)t * 2 * cell : nullptr;
             wa.ldx = 2 * Hp;
-            wa.dC = DC[(t + 1) & 1];
+            wa.dC = t == kL - 1 ? nullptr : DC[(t + 1) & 1];
             wa.dC_out = DC[t & 1];
-            wa.rm_c = RMc + (size_t)((t + 1) & 1) * B;
+            wa.rm_c = t == kL - 1 ? nullptr : RMc + (size_t)((t + 1) & 1) * B;
             wa.rm_c_out = t > 0 ? RMc + (size_t)(t & 1) * B : nullptr;
-            wa.rm_h = RMh + (size_t)((t + 1) & 1) * ns * B;
+            wa.rm_h = zero9 ? nullptr : RMh + (size_t)((t + 1) & 1) * ns * B;
             wa.nrh = t == kL - 1 ? 1 : wb_hslots(l, Hp);
             wa.rm_h_out = t > 0 ? RMh + (size_t)(t & 1) * ns * B : nullptr;
             wa.rm_d = l < kLayers - 1 ? RMd + ((size_t)((l + 1) & 1) * kL + t) * ns * B : nullptr;

@@ -75,16 +75,17 @@ struct WbArgs {
     const _Float16 *Ahi, *Alo;   // [NP][4H], unit-major K
     float *out;                  // [B][ldo], columns [0, NO); NO = 0: no product (layer 0, t = 0)
     int ldo, NO, NB, H;
-    const float *act;            // [B][4H] gate activations (i | f | g | o blocks of H) of the cell, as its forward
-                                 // evaluated them (fcr_wgemm.h)
+    const float *act;            // [B][H][4] gate activations (i, f, g, o of each unit) of the cell, as its forward
+                                 // evaluated and stored them (fcr_wgemm.h)
     const float *c_prev;         // [B][H] or null (t = 0)
-    const float *dh;             // [B][ldh] incoming dh of the recurrence (the head's, or the next cell's product)
+    const float *dh;             // [B][ldh] incoming dh of the recurrence (the head's, or the next cell's product), or
+                                 // null: zero (layers below the top at t = 9)
     const float *din;            // [B][ldx] the layer above's input gradient at t, or null
-    const float *dC;             // [B][H] carried dc in
+    const float *dC;             // [B][H] carried dc in, or null: zero (t = 9)
     float *dC_out;               // [B][H] dc_{t-1} out (another buffer: the other column block still reads dC)
     int ldh, ldx;
     const float *rm_c, *rm_h, *rm_d;   // row bounds in: max|dc| [B], max|dh| [nrh][B] (per column block of their
-                                       // writer), max|din| [nrd][B] or null
+                                       // writer), max|din| [nrd][B]; each null where its rows are (zero or absent)
     int nrh, nrd;
     float *rm_c_out, *rm_h_out, *rm_d_out;   // row bounds out (or null): of dc_{t-1}, of the dh / input-grad columns,
                                              // [column block][B] (every block writes its slot, 0 where it has none)
@@ -103,7 +104,8 @@ __device__ __forceinline__ uint32_t wb_off(int r, int c) { return (uint32_t)(r *
 template <int U>
 struct WbIn {
     typedef float fU __attribute__((ext_vector_type(U)));
-    fU pi, pf, pg, po, cp, dh, dn, dc;
+    f32x4 ac[U];   // i, f, g, o of each unit (the forward's [unit][gate] activation row)
+    fU cp, dh, dn, dc;
 };
 
 // W0G: layer 0 at H > kWbW0LdsUnits reads W_ih0 from global memory (L1 / L2: every producer thread of a workgroup
@@ -139,10 +141,11 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
     float up = 0.0f;
     if (producer) {
         float mh = 0.0f, md = 0.0f;
-        for (int k = 0; k < a.nrh; ++k) mh = fmaxf(mh, a.rm_h[(size_t)k * a.NB + eb]);
+        if (a.rm_h)
+            for (int k = 0; k < a.nrh; ++k) mh = fmaxf(mh, a.rm_h[(size_t)k * a.NB + eb]);
         if (a.rm_d)
             for (int k = 0; k < a.nrd; ++k) md = fmaxf(md, a.rm_d[(size_t)k * a.NB + eb]);
-        const float m = a.rm_c[eb] + mh + md;
+        const float m = (a.rm_c ? a.rm_c[eb] : 0.0f) + mh + md;
         const int ex = m > 0.0f ? __builtin_amdgcn_frexp_expf(m) : 0;   // every |dgate| < 2^ex (times (kL-1)/4: forget)
         up = __builtin_amdgcn_ldexpf(1.0f, kWideDgExp - ex);
         if (ep == 0) reinterpret_cast<float *>(lds + kWbOffDown)[er] = __builtin_amdgcn_ldexpf(1.0f, ex - kWideDgExp);
@@ -188,22 +191,20 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
     // ---- producers: inputs ahead, the tile one step ahead of the MFMAs ----
     const float *pre = a.act + (size_t)eb * K;
     const float *cpr = a.c_prev ? a.c_prev + (size_t)eb * H : nullptr;
-    const float *dhr = a.dh + (size_t)eb * a.ldh;
+    const float *dhr = a.dh ? a.dh + (size_t)eb * a.ldh : nullptr;
     const float *dnr = a.din ? a.din + (size_t)eb * a.ldx : nullptr;
-    const float *dcr = a.dC + (size_t)eb * H;
+    const float *dcr = a.dC ? a.dC + (size_t)eb * H : nullptr;
     float *dco_r = a.dC_out + (size_t)eb * H;
     auto ldu = [](const float *p) { return *reinterpret_cast<const fU *>(p); };
     auto load_in = [&](int s) {
         In x;
         const int u = 8 * s + kWbUnits * ep;
-        x.pi = ldu(pre + u);
-        x.pf = ldu(pre + H + u);
-        x.pg = ldu(pre + 2 * H + u);
-        x.po = ldu(pre + 3 * H + u);
+#pragma unroll
+        for (int k = 0; k < kWbUnits; ++k) x.ac[k] = *reinterpret_cast<const f32x4 *>(pre + 4 * (u + k));
         x.cp = cpr ? ldu(cpr + u) : fU{};
-        x.dh = ldu(dhr + u);
+        x.dh = dhr ? ldu(dhr + u) : fU{};
         x.dn = dnr ? ldu(dnr + u) : fU{};
-        x.dc = ldu(dcr + u);
+        x.dc = dcr ? ldu(dcr + u) : fU{};
         return x;
     };
     const bool wr_dc = cb == 0 && elive;   // every column block forms the same dc_{t-1}: the first stores it
@@ -215,7 +216,7 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
         const int u = 8 * s + kWbUnits * ep;
 #pragma unroll
         for (int k = 0; k < kWbUnits; ++k) {
-            const float i = x.pi[k], f = x.pf[k], g = x.pg[k], o = x.po[k];   // the forward's activations
+            const float i = x.ac[k][0], f = x.ac[k][1], g = x.ac[k][2], o = x.ac[k][3];   // the forward's activations
             const float cp = x.cp[k];
             const float tc = tanh_f(fmaf(f, cp, i * g));   // c_t rebuilt as the forward formed it (f c_{t-1} + i g)
             const float dh = x.dh[k] + x.dn[k];

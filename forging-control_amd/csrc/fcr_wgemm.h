@@ -61,7 +61,8 @@ struct WgArgs {
     const float *c_prev;   // [B][H] or null (t = 0)
     float *c_out;          // [B][H]
     float *h_out;          // [B][H] fp32 or null (the readout's cell only)
-    float *act;            // [B][4H] or null: the gate activations i | f | g | o, as the cell update evaluated them
+    float *act;            // [B][H][4] or null: the gate activations i, f, g, o of each unit, as the cell update
+                           // evaluated them
                            // (the backward's dgates read them: no sigmoid / tanh of its own but tanh(c_t))
     _Float16 *h_rec;       // [B][2H] this cell's h record (hi | lo): the next cell's and the layer above's operand
 };
@@ -189,8 +190,8 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_cell_fwd_kernel(WgArgs a) 
     // ---- epilogue: the cell update on the accumulators, through LDS ----
     // A lane holds (trajectory, unit) pairs scattered over 16 rows; the records want whole rows. So the c_prev tile
     // comes in by rows, each lane updates its pairs in LDS tiles [trajectory][unit] (rows padded by 16 B: 2-way
-    // bank conflicts at most, chunks stay 16-B aligned), and c, the h record and (keep_act) the pre-activations go
-    // out by rows again.
+    // bank conflicts at most, chunks stay 16-B aligned), and c and the h record go out by rows again; the activations
+    // go straight from the registers ([unit][gate] rows, WgArgs.act).
     constexpr int CSTR = kWgU + 4;            // floats per c row
     constexpr int HSTR = kWgU + 8;            // halves per hi / lo row
     float *cs = reinterpret_cast<float *>(lds);                                   // [128][CSTR]
@@ -217,14 +218,16 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_cell_fwd_kernel(WgArgs a) 
             const f32x4 g4 = acc[m][n];
             const float cp = a.c_prev ? cs[r * CSTR + ul] : 0.0f;
             const float i = sigm(g4[0]), f = sigm(g4[1]), g = tanhf(g4[2]), o = sigm(g4[3]);
-            acc[m][n] = f32x4{i, f, g, o};   // the accumulators become the activations the act rows store
+            const int b = b0 + r;
+            // the activations, [unit][gate] rows: a lane's four gates are one 16-B store, a fragment's 4 units x 16
+            // trajectories 16 row pieces of 64 B (the next m fills the other half of each 128-B line)
+            if (a.act && b < a.B) *reinterpret_cast<f32x4 *>(a.act + ((size_t)b * H + u0 + ul) * 4) = f32x4{i, f, g, o};
             const float c = (a.c_prev ? f * cp : 0.0f) + i * g;
             const float h = o * tanhf(c);
             const _Float16 hi = (_Float16)h;
             cs[r * CSTR + ul] = c;
             hs[r * HSTR + ul] = hi;
             ls[r * HSTR + ul] = (_Float16)(h - (float)hi);
-            const int b = b0 + r;
             if (a.h_out && b < a.B) a.h_out[(size_t)b * H + u0 + ul] = h;   // the readout's cell only
         }
     }
@@ -239,24 +242,6 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_cell_fwd_kernel(WgArgs a) 
         const _Float16 *src = (ec < 8 ? hs : ls) + r * HSTR + 8 * e;
         *reinterpret_cast<u32x4 *>(a.h_rec + (size_t)b * 2 * H + (ec < 8 ? 0 : H) + u0 + 8 * e) =
             *reinterpret_cast<const u32x4 *>(src);
-    }
-    if (a.act) {   // gate by gate through the c tile: rows of 64 activations
-#pragma unroll
-        for (int gt = 0; gt < 4; ++gt) {
-            __syncthreads();
-#pragma unroll
-            for (int n = 0; n < kWgNT; ++n)
-#pragma unroll
-                for (int m = 0; m < 8; ++m) cs[(16 * (kWgNT * wc + n) + fr) * CSTR + 32 * wr + 4 * m + fq] = acc[m][n][gt];
-            __syncthreads();
-#pragma unroll
-            for (int p = 0; p < kWgN / ERS; ++p) {
-                const int r = er + ERS * p, b = b0 + r;
-                if (b < a.B)
-                    *reinterpret_cast<f32x4 *>(a.act + (size_t)b * 4 * H + gt * H + u0 + 4 * ec) =
-                        *reinterpret_cast<const f32x4 *>(cs + r * CSTR + 4 * ec);
-            }
-        }
     }
 }
 

@@ -10,7 +10,7 @@
 //   WR  [10][B][64] halves   layer-0 window records [hi | lo] of the current window (Functions.py:1395-1396, 1433-1434)
 //   HR  [2][10][B][2Hp]      h records [hi | lo] of two layers' cells (layer l in slot l & 1)
 //   Cs  [3][10][B][Hp]       c_t of every cell of the current window
-//   Act [3][10][B][4Hp]      gate activations i, f, g, o of every cell (the backward's dgates read them)
+//   Act [3][10][B][Hp][4]    gate activations i, f, g, o of every cell (the backward's dgates read them)
 //   rowg [N+9][B][5]         d loss / d (extended window row r): every window's layer-0 input gradient
 //                            lands in rows j..j+9 — the row-gradient bookkeeping of fcr_bwd.h, batch-wide
 // The backward keeps nothing from the forward but xhat, the predictions and the kept windows: it recomputes each

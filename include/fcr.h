@@ -260,7 +260,7 @@ int fcr_get_small_batch_limit(void);
 /*
  * H > 52 (the batch-wide GEMM path): how many bytes of "kept windows" fcr_workspace_size(with_backward = 1)
  * may add. The backward recomputes each window's cells from a per-window checkpoint (the rollout's memory
- * floor); a kept window instead holds the forward's gate pre-activations and c for all its 30 cells
+ * floor); a kept window instead holds the forward's gate activations and c for all its 30 cells
  * (30 B 5H floats: 10 GB at B = 65 536, H = 256 — torch's autograd keeps at least that for every window),
  * so its backward skips the recompute (config 5: a third of the step). The last windows are kept, as many
  * as the budget allows (fcr_wide_kept_windows).
@@ -277,8 +277,8 @@ int64_t fcr_get_wide_keep_budget(void);
  * i.e. the autograd backward of one nn.LSTM cell (Functions.py:325, inside loss.backward() at :655), run by the same
  * kernel and launcher fcr_backward uses (wide_bwd_fused_kernel), on caller-given inputs, so a test can compare every
  * output element with an fp64 evaluation. H % 8 == 0, H <= 2048 (the fused cell's tiling). Per trajectory b:
- *   act (B,4H)  gate activations i = sigmoid, f = sigmoid, g = tanh, o = sigmoid of the pre-activations (torch
- *               order i|f|g|o), as the forward cell saved them;  c_prev (B,H) or NULL (t = 0);
+ *   act (B,H,4) gate activations (i, f, g, o) = (sigmoid, sigmoid, tanh, sigmoid) of each unit's pre-activations, in
+ *               the [unit][gate] layout the forward cell saves them;  c_prev (B,H) or NULL (t = 0);
  *   dh (B,H) incoming dh_t of the recurrence;  din (B,H) the layer above's input gradient at t, or NULL;
  *   dc (B,H) carried dc_t;  ->  dc_out (B,H) = dc_{t-1};
  *   layer0 == 0: out (B,2H) = dG [W_ih | W_hh] (input gradient | dh_{t-1}; only the first H columns without c_prev),

@@ -68,6 +68,7 @@ def run_cell(x, layer0):
     B, H = x["dh"].shape
     d = lambda a: None if a is None else torch.as_tensor(np.ascontiguousarray(a, np.float32), device=DEV)
     t = {k: d(v) for k, v in x.items()}
+    t["act"] = d(x["act"].reshape(B, 4, H).transpose(0, 2, 1))   # the forward's [unit][gate] layout (include/fcr.h)
     nout = (H if layer0 else 2 * H)
     out = torch.full((B, nout), float("nan"), device=DEV)
     dc_out = torch.full((B, H), float("nan"), device=DEV)
