@@ -496,9 +496,9 @@ int launch_fb(const WbArgs &wa, bool l0, hipStream_t s) {
 #endif
                                  : (const void *)wide_bwd_fused_kernel<WbG256, true, true>;
     if (const int rc = lds_attr(fn, wide ? kWbLds512 : kWbLds256, attr_done[kind], "wbwd")) return rc;
-    if (wa.NO < 0 || wa.NO > 2 * wa.H || wa.NO % 4 || wa.H % 8 || wa.NB <= 0 || wa.ldo % 4 || wa.ldh % 4 ||
-        wa.ldx % 4 || (wa.rm_h && wa.nrh < 1) || (wa.rm_d && wa.nrd < 1) || (l0 && (!wa.wih0 || !wa.rowg)))
-        return fail(FCR_EINVAL, "wide_bwd_fused_kernel: NO %d H %d B %d ldo %d off its tiling", wa.NO, wa.H, wa.NB, wa.ldo);
+    if (wa.NO < 0 || wa.NO > 2 * wa.H || wa.NO % 8 || wa.H % 8 || wa.NB <= 0 || (wa.rm_h && wa.nrh < 1) ||
+        (wa.rm_d && wa.nrd < 1) || (l0 && (!wa.wih0 || !wa.rowg)))
+        return fail(FCR_EINVAL, "wide_bwd_fused_kernel: NO %d H %d B %d off its tiling", wa.NO, wa.H, wa.NB);
     const int M = wide ? WbG512::kM : WbG256::kM, N = wide ? WbG512::kN : WbG256::kN;
     const dim3 grid((unsigned)((wa.NB + N - 1) / N * (wa.NO > 0 ? (wa.NO + M - 1) / M : 1)));
 #if FCR_WB512
@@ -515,22 +515,32 @@ int launch_fb(const WbArgs &wa, bool l0, hipStream_t s) {
     return launch_check("wide_bwd_fused_kernel");
 }
 
-// |v| row maxima over the first n columns of B rows of stride ld (one wave per row): the row bounds fcr_wide_bwd_cell
-// hands the fused backward cell, which the rollout gets from the kernels that wrote those rows
+// |v| row maxima over the first n columns of B rows of stride ld, or of k8 rows (ld = 0; fcr_wide.h), one wave per
+// row: the row bounds fcr_wide_bwd_cell hands the fused backward cell, which the rollout gets from the kernels that
+// wrote those rows (the surrogate: its head's dh_9)
 __global__ __launch_bounds__(256) void row_absmax_kernel(const float *__restrict__ v, int n, int ld, int B,
                                                          float *__restrict__ out) {
     const int b = blockIdx.x * 4 + (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (b >= B) return;
     float m = 0.0f;
-    for (int i = lane; i < n; i += 64) m = fmaxf(m, fabsf(v[(size_t)b * ld + i]));
+    for (int i = lane; i < n; i += 64) m = fmaxf(m, fabsf(v[ld ? (size_t)b * ld + i : k8(B, b, i)]));
 #pragma unroll
     for (int o = 32; o; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
     if (lane == 0) out[b] = m;
 }
 
+// torch rows [B][ld] (first n columns) <-> k8 rows [n/8][B][8] (fcr_wide.h): the test hook's layout conversion
+__global__ void k8_rows_kernel(const float *__restrict__ src, int B, int n, int ld, float *__restrict__ dst, int to_k8) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (size_t)B * n) return;
+    const int b = (int)(i / n), u = (int)(i % n);
+    if (to_k8) dst[k8(B, b, u)] = src[(size_t)b * ld + u];
+    else dst[(size_t)b * ld + u] = src[k8(B, b, u)];
+}
+
 // fcr_wide_bwd_cell (test hook): the scratch of one standalone fused backward cell
 struct CellHookLayout {
-    size_t bt, w0, rm, total;
+    size_t bt, w0, rm, rows, total;
 };
 CellHookLayout cell_hook_layout(int B, int H, int layer0) {
     CellHookLayout L{};
@@ -538,7 +548,9 @@ CellHookLayout cell_hook_layout(int B, int H, int layer0) {
     L.bt = 0;
     L.w0 = align_up(sizeof(_Float16) * 2 * NP * 4 * H);
     L.rm = L.w0 + align_up(sizeof(float) * 4 * H * kIn);
-    L.total = L.rm + align_up(sizeof(float) * 3 * (size_t)B);   // rm_c [B], rm_h [1][B], rm_d [1][B]
+    L.rows = L.rm + align_up(sizeof(float) * 3 * (size_t)B);   // rm_c [B], rm_h [1][B], rm_d [1][B]
+    // k8 copies of c_prev, dh, din, dc, dc_out (B H each) and out (B NP)
+    L.total = L.rows + align_up(sizeof(float) * (size_t)B * (5 * (size_t)H + NP));
     return L;
 }
 int cell_hook_check(int B, int H) {
@@ -574,27 +586,33 @@ int wide_bwd_cell_hook(int B, int H, int layer0, const float *w_ih, const float 
     hipLaunchKernelGGL(row_absmax_kernel, rg, rb, 0, s, dh, H, H, B, rm_h);
     if (din) hipLaunchKernelGGL(row_absmax_kernel, rg, rb, 0, s, din, H, H, B, rm_d);
     if ((rc = launch_check("row_absmax_kernel"))) return rc;
+    // the cell reads and writes k8 rows: the caller's rows are converted around it
+    float *rows = (float *)(base + L.rows);
+    const size_t cell = (size_t)B * H;
+    auto to_k8 = [&](const float *src, float *dst) -> const float * {
+        if (!src) return nullptr;
+        hipLaunchKernelGGL(k8_rows_kernel, dim3((unsigned)((cell + 255) / 256)), dim3(256), 0, s, src, B, H, H, dst, 1);
+        return dst;
+    };
     WbArgs wa{};
     wa.Ahi = bt;
     wa.Alo = bt + nbt;
     wa.NB = B;
     wa.H = H;
     wa.act = act;
-    wa.c_prev = c_prev;
-    wa.dh = dh;
-    wa.ldh = H;
-    wa.din = din;
-    wa.ldx = H;
-    wa.dC = dc;
-    wa.dC_out = dc_out;
+    wa.c_prev = to_k8(c_prev, rows);
+    wa.dh = to_k8(dh, rows + cell);
+    wa.din = to_k8(din, rows + 2 * cell);
+    wa.dC = to_k8(dc, rows + 3 * cell);
+    wa.dC_out = rows + 4 * cell;
+    if ((rc = launch_check("k8_rows_kernel"))) return rc;
     wa.rm_c = rm_c;
     wa.rm_h = rm_h;
     wa.rm_d = din ? rm_d : nullptr;
     wa.nrh = 1;
     wa.nrd = 1;
-    wa.out = out;
+    wa.out = rows + 5 * cell;
     if (!layer0) {   // [input gradient | dh_{t-1}] (t = 0, no c_prev: the former only)
-        wa.ldo = 2 * H;
         wa.NO = c_prev ? 2 * H : H;
         wa.h0 = H;
         wa.h1 = c_prev ? 2 * H : H;
@@ -602,7 +620,6 @@ int wide_bwd_cell_hook(int B, int H, int layer0, const float *w_ih, const float 
     } else {         // dh_{t-1} (none at t = 0) and the window-row gradient
         if (hipMemsetAsync(rowg, 0, sizeof(float) * kIn * (size_t)B, s) != hipSuccess)
             return fail(FCR_EHIP, "hipMemsetAsync failed");
-        wa.ldo = H;
         wa.NO = c_prev ? H : 0;
         wa.h0 = 0;
         wa.h1 = H;
@@ -610,7 +627,13 @@ int wide_bwd_cell_hook(int B, int H, int layer0, const float *w_ih, const float 
         wa.wih0 = w0;
         wa.rowg = rowg;
     }
-    return launch_fb(wa, layer0 != 0, s);
+    if ((rc = launch_fb(wa, layer0 != 0, s))) return rc;
+    hipLaunchKernelGGL(k8_rows_kernel, dim3((unsigned)((cell + 255) / 256)), dim3(256), 0, s, (const float *)wa.dC_out, B,
+                       H, H, dc_out, 0);
+    if (wa.NO > 0)
+        hipLaunchKernelGGL(k8_rows_kernel, dim3((unsigned)(((size_t)B * wa.NO + 255) / 256)), dim3(256), 0, s,
+                           (const float *)wa.out, B, wa.NO, layer0 ? H : 2 * H, out, 0);
+    return launch_check("k8_rows_kernel");
 }
 
 // One window's 30 cells, forward (the rollout, and the backward's recompute of a window that was not kept): layer by
@@ -753,7 +776,8 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
                 // Hp..2Hp-1 of D[l-1] row t+1; the layer above's input gradient from D[l] row t
                 // (t = 9: the head's dh for layer 2, zero below it, passed as null like the zero dc_9 and their bounds)
                 const bool top9 = t == kL - 1 && l == kLayers - 1, zero9 = t == kL - 1 && l < kLayers - 1;
-                const float *dh_src = top9 ? a.dH : zero9 ? nullptr : l == 0 ? E0 : D[l - 1] + (size_t)(t + 1) * 2 * cell + Hp;
+                // (D rows are k8 rows of 2Hp columns: column Hp starts at + Hp B = + cell)
+                const float *dh_src = top9 ? a.dH : zero9 ? nullptr : l == 0 ? E0 : D[l - 1] + (size_t)(t + 1) * 2 * cell + cell;
                 WbArgs wa{};
                 wa.Ahi = (const _Float16 *)(base + L.bt[l]);
                 wa.Alo = wa.Ahi + (size_t)(l == 0 ? Hp : 2 * Hp) * 4 * Hp;
@@ -762,9 +786,7 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
                 wa.act = a.Act + c_off * 4;
                 wa.c_prev = t > 0 ? a.Cs + c_off - cell : nullptr;
                 wa.dh = dh_src;
-                wa.ldh = t == kL - 1 || l == 0 ? Hp : 2 * Hp;
                 wa.din = l < kLayers - 1 ? D[l] + (size_t)t * 2 * cell : nullptr;
-                wa.ldx = 2 * Hp;
                 wa.dC = t == kL - 1 ? nullptr : DC[(t + 1) & 1];   // t writes buffer t & 1
                 wa.dC_out = DC[t & 1];
                 wa.rm_c = t == kL - 1 ? nullptr : RMc + (size_t)((t + 1) & 1) * B;
@@ -779,14 +801,12 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
                 wa.rm_d_out = l > 0 ? RMd + ((size_t)(l & 1) * kL + t) * ns * B : nullptr;
                 if (l > 0) {   // [input gradient | dh_{t-1}] (t = 0: the former only) into D[l-1] row t
                     wa.out = D[l - 1] + (size_t)t * 2 * cell;
-                    wa.ldo = 2 * Hp;
                     wa.NO = t > 0 ? 2 * Hp : Hp;
                     wa.h0 = Hp;
                     wa.h1 = t > 0 ? 2 * Hp : Hp;
                     wa.d1 = Hp;
                 } else {       // dh_{t-1} into E0 (t = 0: none), and the window-row gradient into rowg row j + t
                     wa.out = E0;
-                    wa.ldo = Hp;
                     wa.NO = t > 0 ? Hp : 0;
                     wa.h0 = 0;
                     wa.h1 = Hp;
@@ -998,7 +1018,7 @@ int surw_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, floa
     float *dH = (float *)(base + L.dH);
     float *RMc = (float *)(base + L.RMc), *RMh = (float *)(base + L.RMh), *RMd = (float *)(base + L.RMd);
     hipLaunchKernelGGL(sur_head_kernel, grid(cell), dim3(256), 0, s, dy, fcw, B, Hp, dH);
-    hipLaunchKernelGGL(row_absmax_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, (const float *)dH, Hp, Hp, B, RMh);
+    hipLaunchKernelGGL(row_absmax_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, (const float *)dH, Hp, 0, B, RMh);
     if ((rc = launch_check("readout backward"))) return rc;
     float *D[2] = {(float *)(base + L.D[0]), (float *)(base + L.D[1])};
     float *DC[2] = {(float *)(base + L.dC), (float *)(base + L.DC2)};
@@ -1018,10 +1038,8 @@ int surw_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, floa
             wa.act = Act + c_off * 4;
             wa.c_prev = t > 0 ? Cs + c_off - cell : nullptr;
             const bool zero9 = t == kL - 1 && l < kLayers - 1;   // dh_9 below the top layer: zero (null)
-            wa.dh = t == kL - 1 ? (zero9 ? nullptr : dH) : l == 0 ? E0 : D[l - 1] + (size_t)(t + 1) * 2 * cell + Hp;
-            wa.ldh = t == kL - 1 || l == 0 ? Hp : 2 * Hp;
+            wa.dh = t == kL - 1 ? (zero9 ? nullptr : dH) : l == 0 ? E0 : D[l - 1] + (size_t)(t + 1) * 2 * cell + cell;
             wa.din = l < kLayers - 1 ? D[l] + (size_t)t * 2 * cell : nullptr;
-            wa.ldx = 2 * Hp;
             wa.dC = t == kL - 1 ? nullptr : DC[(t + 1) & 1];
             wa.dC_out = DC[t & 1];
             wa.rm_c = t == kL - 1 ? nullptr : RMc + (size_t)((t + 1) & 1) * B;
@@ -1035,14 +1053,12 @@ int surw_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, floa
             wa.dg = dG + (size_t)t * cell * 4;
             if (l > 0) {
                 wa.out = D[l - 1] + (size_t)t * 2 * cell;
-                wa.ldo = 2 * Hp;
                 wa.NO = t > 0 ? 2 * Hp : Hp;
                 wa.h0 = Hp;
                 wa.h1 = t > 0 ? 2 * Hp : Hp;
                 wa.d1 = Hp;
             } else {
                 wa.out = E0;
-                wa.ldo = Hp;
                 wa.NO = t > 0 ? Hp : 0;
                 wa.h0 = 0;
                 wa.h1 = Hp;

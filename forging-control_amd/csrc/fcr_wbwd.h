@@ -73,17 +73,17 @@ __host__ __device__ constexpr int wb_lds_bytes(bool l0, int H) {
 
 struct WbArgs {
     const _Float16 *Ahi, *Alo;   // [NP][4H], unit-major K
-    float *out;                  // [B][ldo], columns [0, NO); NO = 0: no product (layer 0, t = 0)
-    int ldo, NO, NB, H;
+    float *out;                  // k8 rows (fcr_wide.h) of NO columns; NO = 0: no product (layer 0, t = 0)
+    int NO, NB, H;
     const float *act;            // [B][H][4] gate activations (i, f, g, o of each unit) of the cell, as its forward
                                  // evaluated and stored them (fcr_wgemm.h)
-    const float *c_prev;         // [B][H] or null (t = 0)
-    const float *dh;             // [B][ldh] incoming dh of the recurrence (the head's, or the next cell's product), or
-                                 // null: zero (layers below the top at t = 9)
-    const float *din;            // [B][ldx] the layer above's input gradient at t, or null
-    const float *dC;             // [B][H] carried dc in, or null: zero (t = 9)
-    float *dC_out;               // [B][H] dc_{t-1} out (another buffer: the other column block still reads dC)
-    int ldh, ldx;
+    // the per-unit rows below are k8 rows of H units ([H/8][NB][8], fcr_wide.h)
+    const float *c_prev;         // c_{t-1}, or null (t = 0)
+    const float *dh;             // incoming dh of the recurrence (the head's, or the next cell's product), or null: zero
+                                 // (layers below the top at t = 9)
+    const float *din;            // the layer above's input gradient at t, or null
+    const float *dC;             // carried dc in, or null: zero (t = 9)
+    float *dC_out;               // dc_{t-1} out (another buffer: the other column block still reads dC)
     const float *rm_c, *rm_h, *rm_d;   // row bounds in: max|dc| [B], max|dh| [nrh][B] (per column block of their
                                        // writer), max|din| [nrd][B]; each null where its rows are (zero or absent)
     int nrh, nrd;
@@ -190,21 +190,24 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
 
     // ---- producers: inputs ahead, the tile one step ahead of the MFMAs ----
     const float *pre = a.act + (size_t)eb * K;
-    const float *cpr = a.c_prev ? a.c_prev + (size_t)eb * H : nullptr;
-    const float *dhr = a.dh ? a.dh + (size_t)eb * a.ldh : nullptr;
-    const float *dnr = a.din ? a.din + (size_t)eb * a.ldx : nullptr;
-    const float *dcr = a.dC ? a.dC + (size_t)eb * H : nullptr;
-    float *dco_r = a.dC_out + (size_t)eb * H;
+    // k8 rows: this thread's U units of step s at + s * 8 NB
+    const size_t kso = (size_t)8 * a.NB, ko = (size_t)eb * 8 + kWbUnits * ep;
+    const float *cpr = a.c_prev ? a.c_prev + ko : nullptr;
+    const float *dhr = a.dh ? a.dh + ko : nullptr;
+    const float *dnr = a.din ? a.din + ko : nullptr;
+    const float *dcr = a.dC ? a.dC + ko : nullptr;
+    float *dco_r = a.dC_out + ko;
     auto ldu = [](const float *p) { return *reinterpret_cast<const fU *>(p); };
     auto load_in = [&](int s) {
         In x;
         const int u = 8 * s + kWbUnits * ep;
+        const size_t so = s * kso;
 #pragma unroll
         for (int k = 0; k < kWbUnits; ++k) x.ac[k] = *reinterpret_cast<const f32x4 *>(pre + 4 * (u + k));
-        x.cp = cpr ? ldu(cpr + u) : fU{};
-        x.dh = dhr ? ldu(dhr + u) : fU{};
-        x.dn = dnr ? ldu(dnr + u) : fU{};
-        x.dc = dcr ? ldu(dcr + u) : fU{};
+        x.cp = cpr ? ldu(cpr + so) : fU{};
+        x.dh = dhr ? ldu(dhr + so) : fU{};
+        x.dn = dnr ? ldu(dnr + so) : fU{};
+        x.dc = dcr ? ldu(dcr + so) : fU{};
         return x;
     };
     const bool wr_dc = cb == 0 && elive;   // every column block forms the same dc_{t-1}: the first stores it
@@ -227,7 +230,7 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
             dg[4 * k + 3] = dh * tc * (o - o * o);
             dco[k] = dct * f;
         }
-        if (wr_dc) *reinterpret_cast<fU *>(dco_r + u) = dco;
+        if (wr_dc) *reinterpret_cast<fU *>(dco_r + s * kso) = dco;
         if (a.dg && wr_dc) {   // (column block 0 writes them: every block forms the same)
             float *d = a.dg + (size_t)eb * K + u;
 #pragma unroll
@@ -394,7 +397,7 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
                     if (col + e >= a.h0 && col + e < a.h1) mh = fmaxf(mh, av);
                     if (col + e < a.d1) md = fmaxf(md, av);
                 }
-                if (b < a.NB && col < a.NO) *reinterpret_cast<f32x4 *>(a.out + (size_t)b * a.ldo + col) = v;
+                if (b < a.NB && col < a.NO) *reinterpret_cast<f32x4 *>(a.out + k8(a.NB, b, col)) = v;
             }
             mh = fmaxf(mh, __shfl_xor(mh, 16));
             mh = fmaxf(mh, __shfl_xor(mh, 32));

@@ -58,8 +58,8 @@ struct WgArgs {
     int kx;                // k of the x part (H, or kWgRecX0 for layer 0)
     const _Float16 *hr;    // h part records [B][2H] (hi | lo) of this layer's cell t - 1, or null (t = 0: x part only)
     int B, H;              // H: the padded hidden size (a multiple of kWgU)
-    const float *c_prev;   // [B][H] or null (t = 0)
-    float *c_out;          // [B][H]
+    const float *c_prev;   // k8 rows [H/8][B][8] (fcr_wide.h) or null (t = 0)
+    float *c_out;          // k8 rows [H/8][B][8]
     float *h_out;          // [B][H] fp32 or null (the readout's cell only)
     float *act;            // [B][H][4] or null: the gate activations i, f, g, o of each unit, as the cell update
                            // evaluated them
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_cell_fwd_kernel(WgArgs a) 
             const int r = er + ERS * p, b = b0 + r;
             if (b < a.B)
                 *reinterpret_cast<f32x4 *>(cs + r * CSTR + 4 * ec) =
-                    *reinterpret_cast<const f32x4 *>(a.c_prev + (size_t)b * H + u0 + 4 * ec);
+                    *reinterpret_cast<const f32x4 *>(a.c_prev + k8(a.B, b, u0 + 4 * ec));
         }
     }
     __syncthreads();
@@ -236,7 +236,7 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_cell_fwd_kernel(WgArgs a) 
     for (int p = 0; p < kWgN / ERS; ++p) {
         const int r = er + ERS * p, b = b0 + r;
         if (b >= a.B) continue;
-        *reinterpret_cast<f32x4 *>(a.c_out + (size_t)b * H + u0 + 4 * ec) = *reinterpret_cast<const f32x4 *>(cs + r * CSTR + 4 * ec);
+        *reinterpret_cast<f32x4 *>(a.c_out + k8(a.B, b, u0 + 4 * ec)) = *reinterpret_cast<const f32x4 *>(cs + r * CSTR + 4 * ec);
         // 8 chunks of 8 halves per row and half: the hi halves of the 64 units (ec < 8), then the lo halves
         const int e = ec & 7;
         const _Float16 *src = (ec < 8 ? hs : ls) + r * HSTR + 8 * e;

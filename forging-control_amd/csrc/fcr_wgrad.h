@@ -134,7 +134,7 @@ __global__ void fc_wgrad_sum_kernel(const float *__restrict__ part, int S, int H
     g[e] = s;
 }
 
-// dh_9 of the top layer = dy fc.W (rows of Hp; fc.W padded with zero units)
+// dh_9 of the top layer = dy fc.W (k8 rows of Hp, fcr_wide.h; fc.W padded with zero units)
 __global__ void sur_head_kernel(const float *__restrict__ dy, const float *__restrict__ fcw, int B, int Hp,
                                 float *__restrict__ dH) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -143,7 +143,7 @@ __global__ void sur_head_kernel(const float *__restrict__ dy, const float *__res
     float v = 0.0f;
 #pragma unroll
     for (int o = 0; o < kOut; ++o) v = fmaf(dy[b * kOut + o], fcw[(size_t)o * Hp + u], v);
-    dH[i] = v;
+    dH[k8(B, (int)b, (int)u)] = v;
 }
 
 // the surrogate's window records at H > 52: layer 0's x part of the forward cells (fcr_wgemm.h), [10][B][2 kWideRecX0]

@@ -9,7 +9,7 @@
 // Data (fcr_abi.hip WideLayout), row-major with the batch index outermost inside a slice:
 //   WR  [10][B][64] halves   layer-0 window records [hi | lo] of the current window (Functions.py:1395-1396, 1433-1434)
 //   HR  [2][10][B][2Hp]      h records [hi | lo] of two layers' cells (layer l in slot l & 1)
-//   Cs  [3][10][B][Hp]       c_t of every cell of the current window
+//   Cs  [3][10][Hp/8][B][8]  c_t of every cell of the current window (k8 rows, below)
 //   Act [3][10][B][Hp][4]    gate activations i, f, g, o of every cell (the backward's dgates read them)
 //   rowg [N+9][B][5]         d loss / d (extended window row r): every window's layer-0 input gradient
 //                            lands in rows j..j+9 — the row-gradient bookkeeping of fcr_bwd.h, batch-wide
@@ -31,6 +31,12 @@ struct WideArgs {
     _Float16 *wr;    // split-f16 rollout: layer 0's window records [10][B][2 kWgRecX0] (hi | lo), else null
     const float *wsc;   // window-column scales of the split's range guard (fcr_pack.h)
 };
+
+// "k8" rows of the fp32 per-unit arrays the backward cells stream K step by K step — c, dh, the input gradients, dc
+// (fcr_wbwd.h): element (b, u) of a B x n array at ((u >> 3) B + b) 8 + (u & 7), i.e. [n / 8][B][8]. A K step's 8
+// units of consecutive trajectories are contiguous, so the 32 B one trajectory needs per step share a 128-B line with
+// three neighbours' instead of with its own next three steps' (which L1 does not keep that long).
+__host__ __device__ __forceinline__ size_t k8(int B, int b, int u) { return ((size_t)(u >> 3) * B + b) * 8 + (u & 7); }
 
 // layer 0's window record (the x part of its cell products, fcr_wgemm.h): [hi (32) | lo (32)] halves per
 // trajectory and row, the 5 window columns first, zero after
@@ -201,7 +207,7 @@ __global__ void wide_head_kernel(WideArgs a, int j, float *rmh) {
     if (live)
         for (int u = q; u < a.H; u += kRoLanes) {
             const float v = a.fcw[u] * d[0] + a.fcw[a.H + u] * d[1] + a.fcw[2 * a.H + u] * d[2] + a.fcw[3 * a.H + u] * d[3];
-            a.dH[(size_t)b * a.H + u] = v;
+            a.dH[k8(a.B, b, u)] = v;
             m = fmaxf(m, fabsf(v));
         }
     if (!rmh) return;
