@@ -275,7 +275,7 @@ struct WideLayout {
     int Hp, ns, keep, ctrl_blocks;
     size_t fcw, fcb, cwi, cbi, cwo, fcp, fcbo, fnp, wsc, rng, xhat, tot, cmd, err, Hs, Cs, WR, HR, total;
     size_t fw[3];   // forward split weights per layer: [2][4Hp][K] (W_hi, W_lo; K = kx + Hp, wide_split_fw_kernel)
-    size_t bt[3];   // backward product A per layer: [2][NO][4Hp] (hi, lo; NO = Hp for layer 0, else 2Hp)
+    size_t bt[3];   // backward product A per layer: [NO][4Hp / 32][hi 32 | lo 32] (NO = Hp for layer 0, else 2Hp)
     size_t w0p;     // W_ih0 packed [Hp][4][kIn] (the fused layer-0 cell's window-row gradient)
     size_t Act, dH, dC, DC2, D[2], E0, RMc, RMh, RMd, rowg, dv, fnn_part;
     // kept windows (the last `keep` of N): the forward's gate pre-activations and c per cell
@@ -410,7 +410,7 @@ int wide_pack(const fcr_weights *w, int H, const WideLayout &L, bool backward, c
         const size_t nbt = (size_t)NO * 4 * Hp;
         _Float16 *bt = (_Float16 *)(base + L.bt[l]);
         hipLaunchKernelGGL(wide_split_bt_kernel, grid(nbt), dim3(256), 0, s, l == 0 ? (const float *)nullptr : w->w_ih[l],
-                           w->w_hh[l], H, Hp, NO, bt, bt + nbt);
+                           w->w_hh[l], H, Hp, NO, bt);
         if ((rc = launch_check("wide_split_bt_kernel"))) return rc;
     }
     if (backward) {
@@ -570,7 +570,7 @@ int wide_bwd_cell_hook(int B, int H, int layer0, const float *w_ih, const float 
     const size_t nbt = (size_t)NP * 4 * H;
     _Float16 *bt = (_Float16 *)(base + L.bt);
     hipLaunchKernelGGL(wide_split_bt_kernel, dim3((unsigned)((nbt + 255) / 256)), dim3(256), 0, s,
-                       layer0 ? (const float *)nullptr : w_ih, w_hh, H, H, NP, bt, bt + nbt);
+                       layer0 ? (const float *)nullptr : w_ih, w_hh, H, H, NP, bt);
     int rc = launch_check("wide_split_bt_kernel");
     if (rc) return rc;
     float *w0 = (float *)(base + L.w0);
@@ -595,8 +595,7 @@ int wide_bwd_cell_hook(int B, int H, int layer0, const float *w_ih, const float 
         return dst;
     };
     WbArgs wa{};
-    wa.Ahi = bt;
-    wa.Alo = bt + nbt;
+    wa.A = bt;
     wa.NB = B;
     wa.H = H;
     wa.act = act;
@@ -779,8 +778,7 @@ int wide_backward(const fcr_dims *d, const float *X, const float *states, const 
                 // (D rows are k8 rows of 2Hp columns: column Hp starts at + Hp B = + cell)
                 const float *dh_src = top9 ? a.dH : zero9 ? nullptr : l == 0 ? E0 : D[l - 1] + (size_t)(t + 1) * 2 * cell + cell;
                 WbArgs wa{};
-                wa.Ahi = (const _Float16 *)(base + L.bt[l]);
-                wa.Alo = wa.Ahi + (size_t)(l == 0 ? Hp : 2 * Hp) * 4 * Hp;
+                wa.A = (const _Float16 *)(base + L.bt[l]);
                 wa.NB = B;
                 wa.H = Hp;
                 wa.act = a.Act + c_off * 4;
@@ -1000,7 +998,7 @@ int surw_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, floa
         const size_t nbt = (size_t)NO * 4 * Hp;
         _Float16 *bt = (_Float16 *)(base + L.bt[l]);
         hipLaunchKernelGGL(wide_split_bt_kernel, grid(nbt), dim3(256), 0, s, l == 0 ? (const float *)nullptr : w->w_ih[l],
-                           w->w_hh[l], H, Hp, NO, bt, bt + nbt);
+                           w->w_hh[l], H, Hp, NO, bt);
         if ((rc = launch_check("wide_split_bt_kernel"))) return rc;
     }
     hipLaunchKernelGGL(wide_pack_w0_kernel, grid((size_t)4 * Hp * kIn), dim3(256), 0, s, w->w_ih[0], H, Hp,
@@ -1031,8 +1029,7 @@ int surw_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, floa
         for (int t = kL - 1; t >= 0; --t) {   // the rollout's backward cells (wide_backward), one window
             const size_t c_off = ((size_t)l * kL + t) * cell;
             WbArgs wa{};
-            wa.Ahi = (const _Float16 *)(base + L.bt[l]);
-            wa.Alo = wa.Ahi + (size_t)(l == 0 ? Hp : 2 * Hp) * 4 * Hp;
+            wa.A = (const _Float16 *)(base + L.bt[l]);
             wa.NB = B;
             wa.H = Hp;
             wa.act = Act + c_off * 4;
@@ -1639,4 +1636,13 @@ int fcr_fnn_backward(int32_t B, int32_t in_dim, int32_t hidden, const float *X, 
     return launch_check("grad_reduce_kernel");
 }
 
+#if FCR_WB_STAMP
+// diagnostic builds only (scripts/stamp_wb.py): the fused backward cell's section sums (fcr_wbwd.h), then zeroed
+int fcr_debug_wb_stamp(unsigned long long *out16) {
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(fcr_wb_stamp), 16 * sizeof(unsigned long long)) != hipSuccess)
+        return FCR_EHIP;
+    static const unsigned long long zero[16] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(fcr_wb_stamp), zero, sizeof(zero)) == hipSuccess ? FCR_OK : FCR_EHIP;
+}
+#endif
 }  // extern "C"

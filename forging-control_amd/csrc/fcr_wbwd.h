@@ -44,11 +44,9 @@ struct WbGeo {
     static constexpr int kWaves = kWbProd + CONS, kThreads = 64 * kWaves;
     static constexpr int kTM = M / CONS / 16, kTN = N / 16;   // D tiles per consumer wave
     static constexpr int kPPR = 8 / U;                          // producer threads per trajectory row
-    static constexpr int kStageA = M * kWbK * 2;                // bytes of one split half of A
-    static constexpr int kStage = 2 * kStageA;                  // hi A | lo A
+    static constexpr int kStage = M * kWbK * 4;                 // A rows of [hi (64 B) | lo (64 B)]
     static constexpr int kTileB = N * kWbK * 2;                 // one split half of the dgate tile
     static constexpr int kPieces = kStage / 1024 / CONS;        // LDS-DMA pieces per consumer wave per stage
-    static constexpr int kHalfPieces = kStageA / 1024;
     static constexpr int kOffB = 2 * kStage;                    // [A stage 0 | A stage 1 | B tile 0 hi, lo | B tile 1 ...]
     static constexpr int kOffDown = kOffB + 4 * kTileB;
     static constexpr int kOffW0 = kOffDown + N * 4;             // layer 0: W_ih0 as [unit][gate][kIn]
@@ -72,7 +70,8 @@ __host__ __device__ constexpr int wb_lds_bytes(bool l0, int H) {
 }
 
 struct WbArgs {
-    const _Float16 *Ahi, *Alo;   // [NP][4H], unit-major K
+    const _Float16 *A;           // [NP][4H / 32][hi (32) | lo (32)]: per output column and K step one 128-B line of
+                                 // the f16 split of W^T (unit-major K, wide_split_bt_kernel)
     float *out;                  // k8 rows (fcr_wide.h) of NO columns; NO = 0: no product (layer 0, t = 0)
     int NO, NB, H;
     const float *act;            // [B][H][4] gate activations (i, f, g, o of each unit) of the cell, as its forward
@@ -96,6 +95,29 @@ struct WbArgs {
     float *rowg;                 // layer 0: [B][kIn] window-row gradient row (+=), else null
 };
 
+// Diagnostic build FCR_WB_STAMP=1 (scripts/stamp_wb.py): per-wave s_memtime sums of the layer >= 1 kernel's K-step
+// sections, added into fcr_wb_stamp by lane 0 (vector atomics) — consumers: barrier wait, A DMA issue, fragment reads +
+// MFMA issue; producers: barrier wait, input load issue, dgates (including the wait for their inputs) + tile writes.
+// Read the shares, never the build's run time (each stamp drains lgkmcnt).
+#ifndef FCR_WB_STAMP
+#define FCR_WB_STAMP 0
+#endif
+#if FCR_WB_STAMP
+__device__ unsigned long long fcr_wb_stamp[16];
+#define FCR_WB_ST(t)                                                                         \
+    do {                                                                                     \
+        __builtin_amdgcn_sched_barrier(0);                                                   \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");           \
+        __builtin_amdgcn_sched_barrier(0);                                                   \
+    } while (0)
+#else
+#define FCR_WB_ST(t) ((void)0)
+#endif
+
+// byte offset of 16-B chunk c (0..3 hi, 4..7 lo) of 128-B LDS row r of an A stage: the XOR by (r >> 1) & 7 puts the 16
+// lanes of each ds_read_b128 lane group (rows r, chunk c or c + 1) on 16 distinct 16-B slots of the 256-B bank row
+__device__ __forceinline__ uint32_t wb_offa(int r, int c) { return (uint32_t)(r * 128 + ((c ^ ((r >> 1) & 7)) << 4)); }
+
 // byte offset of 16-B chunk c of 64-B LDS row r: the swizzle puts the 8 rows of a fragment read's 8-lane phase
 // on distinct 16-B slots of a 128-B bank line (fcr_wgemm.h wg_off)
 __device__ __forceinline__ uint32_t wb_off(int r, int c) { return (uint32_t)(r * 64 + ((c ^ ((r >> 1) & 3)) << 4)); }
@@ -113,7 +135,7 @@ struct WbIn {
 template <class G, bool L0, bool W0G = false>
 __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a) {
     constexpr int kWbM = G::kM, kWbN = G::kN, kWbCons = G::kCons, kWbUnits = G::kUnits, kWbTM = G::kTM,
-                  kWbTN = G::kTN, kWbThreads = G::kThreads, kWbStageA = G::kStageA, kWbStage = G::kStage,
+                  kWbTN = G::kTN, kWbThreads = G::kThreads, kWbStage = G::kStage,
                   kWbTileB = G::kTileB, kWbPieces = G::kPieces, kWbOffB = G::kOffB, kWbOffDown = G::kOffDown,
                   kWbOffW0 = G::kOffW0, kPPR = G::kPPR;
     using In = WbIn<kWbUnits>;
@@ -166,13 +188,12 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
     uint32_t ldst[kWbPieces];
 #pragma unroll
     for (int q = 0; q < kWbPieces; ++q) {
-        const int j = (producer ? 0 : cw) + kWbCons * q;
-        const bool lo = j >= G::kHalfPieces;
-        const int r = 16 * (lo ? j - G::kHalfPieces : j) + (lane >> 2);
-        const int c = (lane & 3) ^ ((r >> 1) & 3);
+        const int j = (producer ? 0 : cw) + kWbCons * q;   // piece: rows 8 j .. 8 j + 7, whole 128-B lines
+        const int r = 8 * j + (lane >> 3);
+        const int c = (lane & 7) ^ ((r >> 1) & 7);         // the chunk wb_offa puts in lane's slot
         int n = m0 + r;
         if (n >= a.NO) n = a.NO > 0 ? a.NO - 1 : 0;        // tail columns recompute the last one (not stored)
-        gsrc[q] = (lo ? a.Alo : a.Ahi) + (size_t)n * K + 8 * c;
+        gsrc[q] = a.A + (size_t)n * 2 * K + 8 * c;
         ldst[q] = (uint32_t)j * 1024;
     }
     auto dma = [&](int ks, int buf) {
@@ -180,7 +201,7 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
         for (int q = 0; q < kWbPieces; ++q) {
             const uint32_t la = __builtin_amdgcn_readfirstlane(
                 (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char *)(lds + buf * kWbStage + ldst[q]));
-            const _Float16 *g = gsrc[q] + ks * kWbK;
+            const _Float16 *g = gsrc[q] + ks * 2 * kWbK;
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
             asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" :: "s"(la), "v"(g) : "memory", "m0");
@@ -300,11 +321,23 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
             if (nk > 2) x2 = load_in(2);
             barrier();   // W_ih0 and the row scales in LDS
             dgates(0, x0, 0);
+            unsigned long long sw[4] = {0, 0, 0, 0}, tw0 = 0, tw1 = 0, tw2 = 0, tw3 = 0;
+            (void)sw, (void)tw0, (void)tw1, (void)tw2, (void)tw3;
             auto pstep = [&](auto full, int ks, const In &xuse, In &xload) {
                 constexpr bool FULL = decltype(full)::value;   // ks + 3 < nk: nothing conditional in the step
+                FCR_WB_ST(tw0);
                 pbarrier();                                    // tile ks published
+                FCR_WB_ST(tw1);
                 if (FULL || ks + 3 < nk) xload = load_in(ks + 3);
+                FCR_WB_ST(tw2);
                 if (FULL || ks + 1 < nk) dgates(ks + 1, xuse, (ks & 1) ^ 1);   // (its buffer was read at ks - 1)
+                FCR_WB_ST(tw3);
+                if (FCR_WB_STAMP) {
+                    sw[0] += tw1 - tw0;
+                    sw[1] += tw2 - tw1;
+                    sw[2] += tw3 - tw2;
+                    sw[3] += 1;
+                }
             };
             using Full = std::integral_constant<bool, true>;
             using Tail = std::integral_constant<bool, false>;
@@ -319,6 +352,10 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
             if (ks + 2 < nk) pstep(Tail{}, ks + 2, x0, x2);
             if (ks + 3 < nk) pstep(Tail{}, ks + 3, x1, x0);
             if (ks + 4 < nk) pstep(Tail{}, ks + 4, x2, x1);
+#if FCR_WB_STAMP
+            if (lane == 0)
+                for (int k = 0; k < 4; ++k) atomicAdd(&fcr_wb_stamp[4 + k], sw[k]);
+#endif
         } else {
             // layer 0 (the window-row gradient's W_ih0 reads and accumulators) has registers for one set ahead
             In xc = load_in(0);
@@ -355,19 +392,28 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
         const int fr = lane & 15, fq = lane >> 4;
         if (prod) dma(0, 0);
         barrier();
+        unsigned long long sc[4] = {0, 0, 0, 0}, tc0 = 0, tc1 = 0, tc2 = 0;
+        (void)sc, (void)tc0, (void)tc1, (void)tc2;
+        FCR_WB_ST(tc0);
         for (int ks = 0; ks < nk; ++ks) {
             const int buf = ks & 1;
             barrier();   // stage ks's A landed (each consumer waits for its own pieces), tile ks written
+            FCR_WB_ST(tc1);
             if (!prod) continue;
             if (ks + 1 < nk) dma(ks + 1, buf ^ 1);   // into the stage every consumer finished reading at ks - 1
+            FCR_WB_ST(tc2);
+            if (FCR_WB_STAMP) {
+                sc[0] += tc1 - tc0;
+                sc[1] += tc2 - tc1;
+            }
             const char *st = lds + buf * kWbStage;
             const char *bt = lds + kWbOffB + buf * 2 * kWbTileB;
             f16x8 ah[kWbTM], al[kWbTM];
 #pragma unroll
             for (int i = 0; i < kWbTM; ++i) {
                 const int r = 16 * (kWbTM * cw + i) + fr;
-                ah[i] = *reinterpret_cast<const f16x8 *>(st + wb_off(r, fq));
-                al[i] = *reinterpret_cast<const f16x8 *>(st + kWbStageA + wb_off(r, fq));
+                ah[i] = *reinterpret_cast<const f16x8 *>(st + wb_offa(r, fq));
+                al[i] = *reinterpret_cast<const f16x8 *>(st + wb_offa(r, 4 + fq));
             }
 #pragma unroll
             for (int j = 0; j < kWbTN; ++j) {   // B tile by tile; the A fragments stay in registers across them
@@ -377,7 +423,16 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
 #pragma unroll
                 for (int i = 0; i < kWbTM; ++i) acc[i][j] = mma3(ah[i], al[i], bh, bl, acc[i][j]);
             }
+            FCR_WB_ST(tc0);
+            if (FCR_WB_STAMP) {
+                sc[2] += tc0 - tc2;
+                sc[3] += 1;
+            }
         }
+#if FCR_WB_STAMP
+        if (!L0 && lane == 0)
+            for (int k = 0; k < 4; ++k) atomicAdd(&fcr_wb_stamp[k], sc[k]);
+#endif
         if (!prod) return;
         // epilogue: lane = trajectory b0 + 16 j + (lane & 15), columns m0 + 16 (TM cw + i) + 4 (lane >> 4) .. +3, in
         // true units (x the row's down); and the row maxima of the dh and input-gradient columns
@@ -430,7 +485,7 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
 // (unit-major: a K step of the fused kernel is 8 whole units) holding torch's gate row gate H + unit; zero for the
 // padding units (unit or column >= H) of the padded hidden size Hp.
 __global__ void wide_split_bt_kernel(const float *__restrict__ wih, const float *__restrict__ whh, int H, int Hp,
-                                     int NO, _Float16 *dst_hi, _Float16 *dst_lo) {
+                                     int NO, _Float16 *dst) {
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int K = 4 * Hp;
     if (idx >= (size_t)NO * K) return;
@@ -440,8 +495,9 @@ __global__ void wide_split_bt_kernel(const float *__restrict__ wih, const float 
     float v = 0.0f;
     if (unit < H && col < H) v = (wih && n < Hp) ? wih[(size_t)r * H + col] : whh[(size_t)r * H + col];
     const _Float16 hi = (_Float16)v;
-    dst_hi[idx] = hi;
-    dst_lo[idx] = (_Float16)(v - (float)hi);
+    _Float16 *d = dst + (size_t)n * 2 * K + (rp >> 5) * 64 + (rp & 31);   // K step rp / 32: [hi (32) | lo (32)]
+    d[0] = hi;
+    d[32] = (_Float16)(v - (float)hi);
 }
 
 }  // namespace fcr

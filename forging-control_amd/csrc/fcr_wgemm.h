@@ -35,10 +35,13 @@ namespace fcr {
 
 constexpr int kWgU = 64;                  // units per workgroup (the host pads H to a multiple)
 constexpr int kWgM = 4 * kWgU;            // W rows per workgroup
-constexpr int kWgN = 128;                 // trajectories per workgroup
+#ifndef FCR_WG_N
+#define FCR_WG_N 128
+#endif
+constexpr int kWgN = FCR_WG_N;            // trajectories per workgroup (FCR_WG_N = 256: 8 waves, one workgroup per CU)
 constexpr int kWgK = 32;                  // k per block (one 16x16x32 f16 MFMA k-block)
 constexpr int kWgC = kWgK / 8;            // 16-B chunks per LDS row
-constexpr int kWgWaves = 4;               // 2 x kWgWC waves; each 128 rows x kWgN / kWgWC trajectories
+constexpr int kWgWaves = kWgN / 32;       // 2 x kWgWC waves; each 128 rows x 64 trajectories
 constexpr int kWgWC = kWgWaves / 2;
 constexpr int kWgNT = kWgN / kWgWC / 16;  // D tiles per wave along the trajectories
 constexpr int kWgThreads = 64 * kWgWaves;
@@ -71,7 +74,7 @@ struct WgArgs {
 // 8-lane phase on the 8 distinct 16-B slots of a 128-B bank line
 __device__ __forceinline__ uint32_t wg_off(int r, int c) { return (uint32_t)(r * 64 + ((c ^ ((r >> 1) & 3)) << 4)); }
 
-__global__ __launch_bounds__(kWgThreads, 2) void wide_cell_fwd_kernel(WgArgs a) {
+__global__ __launch_bounds__(kWgThreads, kWgN == 128 ? 2 : 1) void wide_cell_fwd_kernel(WgArgs a) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -92,22 +95,23 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_cell_fwd_kernel(WgArgs a) 
     // that the row's swizzle puts in that slot. A stage is 16 W pieces + 8 operand pieces, 6 per wave: pieces
     // q = 0..3 of a wave are W rows, q = 4, 5 operand rows.
     constexpr int NPC = (kWgStageA + kWgStageB) / 1024 / kWgWaves;
-    static_assert(kWgC == 4 && NPC == 6 && kWgStageA / 1024 == 4 * kWgWaves, "DMA pieces");
-    const _Float16 *gw[4];
-    const _Float16 *gx[2], *gh[2];
+    constexpr int NW = kWgStageA / 1024 / kWgWaves;   // the wave's W pieces (then NPC - NW operand pieces)
+    static_assert(kWgC == 4 && (NPC == 6 || NPC == 4) && NW * kWgWaves * 1024 == kWgStageA, "DMA pieces");
+    const _Float16 *gw[NW];
+    const _Float16 *gx[NPC - NW], *gh[NPC - NW];
     const size_t wlo = (size_t)4 * H * a.K;            // W_lo after W_hi
 #pragma unroll
     for (int q = 0; q < NPC; ++q) {
         const int j = wv + kWgWaves * q;                  // piece of the stage
-        const int r = 16 * (q < 4 ? j : j - kWgStageA / 1024) + (lane >> 2);
+        const int r = 16 * (q < NW ? j : j - kWgStageA / 1024) + (lane >> 2);
         const int c = (lane & 3) ^ ((r >> 1) & 3);
-        if (q < 4) {
+        if (q < NW) {
             gw[q] = a.W + (size_t)((r & 3) * H + u0 + (r >> 2)) * a.K + 8 * c;
         } else {
             int b = b0 + r;
             if (b >= a.B) b = a.B - 1;                     // tail rows recompute the last trajectory (not stored)
-            gx[q - 4] = a.xr + (size_t)b * 2 * a.kx + 8 * c;
-            gh[q - 4] = a.hr ? a.hr + (size_t)b * 2 * H + 8 * c : gx[q - 4];
+            gx[q - NW] = a.xr + (size_t)b * 2 * a.kx + 8 * c;
+            gh[q - NW] = a.hr ? a.hr + (size_t)b * 2 * H + 8 * c : gx[q - NW];
         }
     }
     // step s: k-block kb = s / 2, split half s % 2 (0: the hi halves, 1: the lo halves)
@@ -118,8 +122,8 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_cell_fwd_kernel(WgArgs a) 
 #pragma unroll
         for (int q = 0; q < NPC; ++q) {
             const _Float16 *src;
-            if (q < 4) src = gw[q] + kb * kWgK + (lo ? wlo : 0);
-            else src = xpart ? gx[q - 4] + kb * kWgK + (lo ? a.kx : 0) : gh[q - 4] + (kb - nkx) * kWgK + (lo ? H : 0);
+            if (q < NW) src = gw[q] + kb * kWgK + (lo ? wlo : 0);
+            else src = xpart ? gx[q - NW] + kb * kWgK + (lo ? a.kx : 0) : gh[q - NW] + (kb - nkx) * kWgK + (lo ? H : 0);
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
                                              (__attribute__((address_space(3))) void *)(
                                                  (__attribute__((address_space(3))) char *)dst +
@@ -143,7 +147,10 @@ __global__ __launch_bounds__(kWgThreads, 2) void wide_cell_fwd_kernel(WgArgs a) 
     f16x8 ah[8], bh[kWgNT];   // the hi fragments of the current k-block, kept from its first step to its second
     int buf = 0;
     auto wait_stage = [&](int s) {
-        if (s + 1 < ns) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        if (s + 1 < ns) {   // the next step's NPC pieces may stay in flight
+            if constexpr (NPC == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        }
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     };
