@@ -16,7 +16,8 @@ timeout -k 10 300 $B --batch 15 --steps 100 --warmup 5 --graphed > $O/c1_b15_gra
 timeout -k 10 300 $B --batch 15 --steps 50 --warmup 5 --small-limit 0 > $O/c1_b15_fused.log 2>&1
 timeout -k 10 300 $B --batch 256 --steps 50 --warmup 5 > $O/c1_b256.log 2>&1
 timeout -k 10 300 $B --batch 256 --steps 100 --warmup 5 --graphed > $O/c1_b256_graphed.log 2>&1
-timeout -k 10 600 $B --horizon 25 --hidden 256 --steps 3 --warmup 1 > $O/c5.log 2>&1
+timeout -k 10 600 $B --horizon 25 --hidden 256 --steps 5 --warmup 2 > $O/c5.log 2>&1
+timeout -k 10 600 $B --horizon 25 --hidden 256 --steps 5 --warmup 2 --wide-keep-budget max > $O/c5max.log 2>&1
 for f in $O/*.log; do echo "== $f"; python3 -c "
 import json,sys
 d=json.loads(open('$f').read().strip().splitlines()[-1])
