@@ -15,7 +15,8 @@
 // holds one producer and one consumer: the producer's transcendental chains issue while its partner's MFMAs run
 // (with every wave doing both in turn, the step barrier lined the two waves of a SIMD up on the same phase, and the
 // dgate chains were the critical path: 247 ms of backward against 168 ms with the activations stubbed out). K in
-// steps of 32: A through a 2-stage LDS-DMA ring issued by the consumers (W^T is L2-resident); the B tile of step
+// steps of 32: A through a 2-stage LDS-DMA ring (W^T is L2-resident), in whole 128-B lines, issued by the producers
+// for layers >= 1 (by the consumers for layer 0, whose producers carry the window-row gradient); the B tile of step
 // ks + 1 is formed while the consumers multiply step ks. Producer thread (row r = tid / 2, half p = tid % 2) loads
 // units 8s + 4p .. + 3 of its trajectory (pre-activations, c_{t-1}, dh, din, dc: 16-B loads, one step ahead), forms
 // their 16 dgates and dc_{t-1} from the forward's saved activations, splits them into the two 16-B chunks of
@@ -188,7 +189,7 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
     uint32_t ldst[kWbPieces];
 #pragma unroll
     for (int q = 0; q < kWbPieces; ++q) {
-        const int j = (producer ? 0 : cw) + kWbCons * q;   // piece: rows 8 j .. 8 j + 7, whole 128-B lines
+        const int j = (producer ? wv : cw) + kWbCons * q;   // piece: rows 8 j .. 8 j + 7, whole 128-B lines
         const int r = 8 * j + (lane >> 3);
         const int c = (lane & 7) ^ ((r >> 1) & 7);         // the chunk wb_offa puts in lane's slot
         int n = m0 + r;
@@ -314,6 +315,12 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
         // compiler's own wait before their first use (exact counts: no DMA intrinsic in the kernel) is all
         auto pbarrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
         if constexpr (!L0) {
+            // Layers >= 1: the producers also stage A (the consumers then only read and multiply): step ks's pieces
+            // of stage ks + 1 go out after its barrier (the slot every consumer finished reading at ks - 1), and
+            // the step's barrier waits vmcnt(0) for them (and for the step's input loads: measured, the inputs
+            // need no more than that one step in flight, round5_c5_bwd_pdma_ab.log)
+            auto pbarrier_a = [] { asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+            if (prod) dma(0, 0);
             // inputs three steps ahead in rotating register sets (unrolled by three: a copy between sets would wait
             // for the loads)
             In x0 = load_in(0), x1, x2;
@@ -326,9 +333,10 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
             auto pstep = [&](auto full, int ks, const In &xuse, In &xload) {
                 constexpr bool FULL = decltype(full)::value;   // ks + 3 < nk: nothing conditional in the step
                 FCR_WB_ST(tw0);
-                pbarrier();                                    // tile ks published
+                pbarrier_a();                                  // tile ks published, stage ks landed
                 FCR_WB_ST(tw1);
                 if (FULL || ks + 3 < nk) xload = load_in(ks + 3);
+                if (prod && ks + 1 < nk) dma(ks + 1, (ks + 1) & 1);
                 FCR_WB_ST(tw2);
                 if (FULL || ks + 1 < nk) dgates(ks + 1, xuse, (ks & 1) ^ 1);   // (its buffer was read at ks - 1)
                 FCR_WB_ST(tw3);
@@ -390,17 +398,17 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
 #pragma unroll
             for (int j = 0; j < kWbTN; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         const int fr = lane & 15, fq = lane >> 4;
-        if (prod) dma(0, 0);
+        if (prod && L0) dma(0, 0);
         barrier();
         unsigned long long sc[4] = {0, 0, 0, 0}, tc0 = 0, tc1 = 0, tc2 = 0;
         (void)sc, (void)tc0, (void)tc1, (void)tc2;
         FCR_WB_ST(tc0);
         for (int ks = 0; ks < nk; ++ks) {
             const int buf = ks & 1;
-            barrier();   // stage ks's A landed (each consumer waits for its own pieces), tile ks written
+            barrier();   // stage ks's A landed (its issuing waves waited for their pieces), tile ks written
             FCR_WB_ST(tc1);
             if (!prod) continue;
-            if (ks + 1 < nk) dma(ks + 1, buf ^ 1);   // into the stage every consumer finished reading at ks - 1
+            if (L0 && ks + 1 < nk) dma(ks + 1, buf ^ 1);   // into the stage every consumer finished reading at ks - 1
             FCR_WB_ST(tc2);
             if (FCR_WB_STAMP) {
                 sc[0] += tc1 - tc0;
