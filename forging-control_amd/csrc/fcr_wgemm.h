@@ -11,16 +11,19 @@
 // K-concatenated form ([x_hi|x_lo|x_hi|h_hi|h_lo|h_hi] operand rows that the cells wrote in two copies, against
 // [W_hi|W_hi|W_lo|...]) this stages 4 halves per (row, k) instead of 6 and writes each h record once instead of
 // twice (3 copies each): a third less LDS-DMA per MFMA and ~270 MB less HBM per cell at config 5.
-// A workgroup owns 64 units x 128 trajectories: its 256 W rows are taken unit-major, gate-minor (LDS row 4 u +
+// A workgroup owns 64 units x kWgN (256) trajectories: its 256 W rows are taken unit-major, gate-minor (LDS row 4 u +
 // gate), so an MFMA D fragment (16 rows x 16 trajectories; lane = trajectory lane & 15, rows 4 (lane >> 4) .. +3)
 // holds the four gates i, f, g, o of ONE unit of ONE trajectory: the cell update runs on the accumulators, and the
 // 4H x B gate matrix never goes to HBM.
 //
-// Tile walk: 4 waves (2 x 2), each 128 rows (32 units) x 64 trajectories = 8 x 4 D tiles. A 32-k block is TWO ring
-// steps of 24 KB: step 2kb stages [W_hi | x_hi] and multiplies W_hi x_hi; step 2kb + 1 stages [W_lo | x_lo] and
-// multiplies W_hi x_lo + W_lo x_hi (the hi fragments stay in registers across the two steps). Stages land by LDS-DMA
-// through a 3-slot ring (two steps of prefetch, one barrier per step), 72 KB in all (the epilogue's tiles reuse it),
-// so two workgroups share a CU and one's epilogue and barriers overlap the other's MFMAs. LDS rows are 64 B; their
+// Tile walk: kWgN / 32 waves (2 x kWgN / 64), each 128 rows (32 units) x 64 trajectories = 8 x 4 D tiles. A 32-k block
+// is TWO ring steps of 32 KB (24 KB at kWgN = 128): step 2kb stages [W_hi | x_hi] and multiplies W_hi x_hi; step
+// 2kb + 1 stages [W_lo | x_lo] and multiplies W_hi x_lo + W_lo x_hi (the hi fragments stay in registers across the
+// two steps). Stages land by LDS-DMA through a 3-slot ring (two steps of prefetch, one barrier per step; the epilogue's
+// tiles reuse it); at kWgN = 128 two workgroups share a CU (one's epilogue and barriers overlap the other's MFMAs), at
+// 256 one workgroup per CU stages W once for twice the trajectories (round 5: −4.8 % forward). Round 5 also measured
+// one 64 KB ring step per k-block (hi and lo together, 2 slots, one barrier per k-block): +1 % against the split
+// steps at 256 (round5_c5_wg256_ab2_keepall.log). LDS rows are 64 B; their
 // 16-B chunks are XOR-swizzled by (row >> 1) & 3, so the 8 rows of a ds_read_b128 phase land on distinct 16-B bank
 // groups. (History, K-concatenated form: 8 waves x 128 x 32 measured the same; K steps of 64 at one workgroup per CU
 // 13 % slower; B fragments straight from global memory 22 % slower; a 3-stage ring with two steps of DMA prefetch
@@ -36,9 +39,12 @@ namespace fcr {
 constexpr int kWgU = 64;                  // units per workgroup (the host pads H to a multiple)
 constexpr int kWgM = 4 * kWgU;            // W rows per workgroup
 #ifndef FCR_WG_N
-#define FCR_WG_N 128
+#define FCR_WG_N 256
 #endif
-constexpr int kWgN = FCR_WG_N;            // trajectories per workgroup (FCR_WG_N = 256: 8 waves, one workgroup per CU)
+// trajectories per workgroup: 256 = 8 waves at one workgroup per CU (W staged once per 256 trajectories: config 5's
+// forward −4.8 % every window kept, −1.9 % step at the default budget against 128 = 4 waves at two workgroups per CU,
+// round5_c5_wg256_ab2_*.log)
+constexpr int kWgN = FCR_WG_N;
 constexpr int kWgK = 32;                  // k per block (one 16x16x32 f16 MFMA k-block)
 constexpr int kWgC = kWgK / 8;            // 16-B chunks per LDS row
 constexpr int kWgWaves = kWgN / 32;       // 2 x kWgWC waves; each 128 rows x 64 trajectories
