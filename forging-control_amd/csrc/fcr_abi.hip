@@ -863,9 +863,11 @@ struct WgSplit {
     long long n_per;
 };
 WgSplit wg_split(long long n, int R, int K) {
-    const long long tiles = (long long)((R + kWgrT - 1) / kWgrT) * ((K + kWgrT - 1) / kWgrT);
-    long long S = (512 + tiles - 1) / tiles;
-    S = S < 1 ? 1 : (S > 64 ? 64 : S);
+    // K <= kWgrSmallK (wgrad_small_kernel): one thread per row r, so many n slices for parallelism
+    const bool small = K <= kWgrSmallK;
+    const long long tiles = small ? (R + 255) / 256 : (long long)((R + kWgrT - 1) / kWgrT) * ((K + kWgrT - 1) / kWgrT);
+    long long S = ((small ? 2048 : 512) + tiles - 1) / tiles;
+    S = S < 1 ? 1 : (S > (small ? 1024 : 64) ? (small ? 1024 : 64) : S);
     long long per = (n + S - 1) / S;
     per = (per + kWgrN - 1) / kWgrN * kWgrN;
     return {(int)((n + per - 1) / per), per};
@@ -974,10 +976,18 @@ int surw_wgrad(const float *A, long long n, int Hp, int H, int K, const float *X
     g.K = K;
     g.n_per = sp.n_per;
     g.part = part;
-    hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)((4 * Hp + kWgrT - 1) / kWgrT), (unsigned)((K + kWgrT - 1) / kWgrT),
-                                          (unsigned)sp.S),
-                       dim3(kWgrThreads), 0, s, g);
-    int rc = launch_check("wgrad_kernel");
+    int rc;
+    if (K <= kWgrSmallK && X) {
+        hipLaunchKernelGGL(wgrad_small_kernel, dim3((unsigned)((4 * Hp + 255) / 256), (unsigned)sp.S), dim3(256), 0, s, g);
+        rc = launch_check("wgrad_small_kernel");
+    } else {
+        static std::atomic<unsigned long long> attr_done{0};
+        if ((rc = lds_attr((const void *)wgrad_kernel, kWgrLds, attr_done, "wgrad"))) return rc;
+        hipLaunchKernelGGL(wgrad_kernel, dim3((unsigned)((4 * Hp + kWgrT - 1) / kWgrT), (unsigned)((K + kWgrT - 1) / kWgrT),
+                                              (unsigned)sp.S),
+                           dim3(kWgrThreads), kWgrLds, s, g);
+        rc = launch_check("wgrad_kernel");
+    }
     if (rc) return rc;
     const long long e = (long long)4 * H * K;
     hipLaunchKernelGGL(wgrad_sum_pad_kernel, dim3((unsigned)((e + 255) / 256)), dim3(256), 0, s, (const float *)part, sp.S,

@@ -18,8 +18,10 @@
 namespace fcr {
 
 constexpr int kWgrT = 128;                 // C tile (r and k) per workgroup
-constexpr int kWgrN = 16;                  // n rows per staged step (4 MFMA k-steps of 4)
+constexpr int kWgrN = 32;                  // n rows per staged step (8 MFMA k-steps of 4)
 constexpr int kWgrThreads = 256;
+constexpr int kWgrLd = kWgrT + 4;          // LDS row stride (floats): consecutive rows shift by 4 banks
+constexpr int kWgrSmallK = 16;             // K up to this: wgrad_small_kernel (layer 0's 5 window columns)
 
 struct WgradArgs {
     const float *A;            // [n][lda] fp32 dgate rows
@@ -29,12 +31,16 @@ struct WgradArgs {
     int ldx, Hx;               // fp32 row stride; the records' half width
     long long n;               // rows
     int R, K;                  // C rows (padded gate rows 4 Hp) and columns (real input width)
-    long long n_per;           // rows per n slice (the split over blockIdx.z)
+    long long n_per;           // rows per n slice (the split over blockIdx.z); a multiple of kWgrN
     float *part;               // [S][R][K] partial sums (slice s at + s R K)
 };
 
-__global__ __launch_bounds__(kWgrThreads) void wgrad_kernel(WgradArgs a) {
-    __shared__ float As[kWgrN][kWgrT + 4], Xs[kWgrN][kWgrT + 4];
+// Round 5 (second session): 32 rows per step staged through two LDS buffers with ONE barrier per step, the next
+// step's rows loaded into registers (16-B loads: 4 A quads and 2 + 2 record quads per thread) while the current one
+// multiplies — the first form loaded, barriered, stored, barriered and multiplied 16 rows at a time, exposing every
+// load's latency (48 TF/s on the surrogate's H = 256 step, 68 % of it).
+__global__ __launch_bounds__(kWgrThreads, 2) void wgrad_kernel(WgradArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float wgs[];   // [2][As | Xs], each [kWgrN][kWgrLd]
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int r0 = blockIdx.x * kWgrT, k0 = blockIdx.y * kWgrT;
     const long long nb = (long long)blockIdx.z * a.n_per, ne = nb + a.n_per < a.n ? nb + a.n_per : a.n;
@@ -44,30 +50,62 @@ __global__ __launch_bounds__(kWgrThreads) void wgrad_kernel(WgradArgs a) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    // staging: thread -> row tid / 16 of the 16, 8 consecutive columns (tid % 16) * 8 of the 128
-    const int sr = tid >> 4, sc = (tid & 15) * 8;
-    for (long long n0 = nb; n0 < ne; n0 += kWgrN) {
+    // staging: thread -> row tid / 8 of the 32, 16 consecutive columns (tid % 8) * 16 of the 128
+    const int sr = tid >> 3, sc = (tid & 7) * 16;
+    f32x4 av[4], xv[4];
+    auto load = [&](long long n0) {
         const long long n = n0 + sr;
         const bool live = n < ne;
-        float av[8], xv[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int r = r0 + sc + e, k = k0 + sc + e;
-            av[e] = (live && r < a.R) ? a.A[n * a.lda + r] : 0.0f;
-            float x = 0.0f;
-            if (live && k < a.K) {
-                if (a.X) x = a.X[n * a.ldx + k];
-                else x = (float)a.XR[n * 2 * a.Hx + k] + (float)a.XR[n * 2 * a.Hx + a.Hx + k];
+        for (int q = 0; q < 4; ++q) {
+            const int r = r0 + sc + 4 * q, k = k0 + sc + 4 * q;
+            av[q] = (live && r + 3 < a.R) ? *reinterpret_cast<const f32x4 *>(a.A + n * a.lda + r) : f32x4{0, 0, 0, 0};
+            if (a.X) {
+                f32x4 v = {0, 0, 0, 0};
+                if (live)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = k + e < a.K ? a.X[n * a.ldx + k + e] : 0.0f;
+                xv[q] = v;
             }
-            xv[e] = x;
         }
-        __syncthreads();   // the previous step's fragments are read
+        if (!a.X) {   // records: 16 hi and 16 lo halves = 2 + 2 quads (halves past K are zero padding units, and
+                      // their columns are not stored)
+            typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            As[sr][sc + e] = av[e];
-            Xs[sr][sc + e] = xv[e];
+            for (int h = 0; h < 2; ++h) {
+                const int k = k0 + sc + 8 * h;
+                h8 hi = {}, lo = {};
+                if (live && k < a.K) {
+                    const _Float16 *rec = a.XR + n * 2 * a.Hx;
+                    hi = *reinterpret_cast<const h8 *>(rec + k);
+                    lo = *reinterpret_cast<const h8 *>(rec + a.Hx + k);
+                }
+#pragma unroll
+                for (int e = 0; e < 8; ++e) xv[2 * h + e / 4][e % 4] = (float)hi[e] + (float)lo[e];
+            }
         }
-        __syncthreads();
+    };
+    auto store = [&](int buf) {
+        float *As = wgs + buf * 2 * kWgrN * kWgrLd, *Xs = As + kWgrN * kWgrLd;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            *reinterpret_cast<f32x4 *>(As + sr * kWgrLd + sc + 4 * q) = av[q];
+            *reinterpret_cast<f32x4 *>(Xs + sr * kWgrLd + sc + 4 * q) = xv[q];
+        }
+    };
+    long long n0 = nb;
+    if (n0 < ne) {
+        load(n0);
+        store(0);
+        if (n0 + kWgrN < ne) load(n0 + kWgrN);
+    }
+    for (int buf = 0; n0 < ne; n0 += kWgrN, buf ^= 1) {
+        __syncthreads();   // buffer buf written; buffer buf ^ 1 no longer read (step - 1)
+        if (n0 + kWgrN < ne) {
+            store(buf ^ 1);                                   // rows of the next step, loaded during this one
+            if (n0 + 2 * kWgrN < ne) load(n0 + 2 * kWgrN);   // and the step after, in flight across it
+        }
+        const float *As = wgs + buf * 2 * kWgrN * kWgrLd, *Xs = As + kWgrN * kWgrLd;
 #pragma unroll
         for (int kk = 0; kk < kWgrN; kk += 4) {
             // 16x16x4 f32: lane l supplies A[i = l % 16][kk + l / 16] and X[kk + l / 16][j = l % 16]
@@ -75,8 +113,8 @@ __global__ __launch_bounds__(kWgrThreads) void wgrad_kernel(WgradArgs a) {
             float fa[4], fx[4];
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-                fa[t] = As[q][wr + 16 * t + i];
-                fx[t] = Xs[q][wk + 16 * t + i];
+                fa[t] = As[q * kWgrLd + wr + 16 * t + i];
+                fx[t] = Xs[q * kWgrLd + wk + 16 * t + i];
             }
 #pragma unroll
             for (int ti = 0; ti < 4; ++ti)
@@ -95,6 +133,27 @@ __global__ __launch_bounds__(kWgrThreads) void wgrad_kernel(WgradArgs a) {
                 const int r = r0 + wr + 16 * ti + 4 * (lane >> 4) + v, k = k0 + wk + 16 * tj + (lane & 15);
                 if (r < a.R && k < a.K) out[(long long)r * a.K + k] = acc[ti][tj][v];
             }
+}
+constexpr int kWgrLds = 2 * 2 * kWgrN * kWgrLd * 4;   // bytes
+
+// The same reduction for K <= kWgrSmallK fp32 columns (layer 0's W_ih: the 5 window columns), where a 128-wide k tile
+// would multiply zeros: one thread per gate row r and n slice, all K columns in registers, partials [S][R][K]
+__global__ __launch_bounds__(256) void wgrad_small_kernel(WgradArgs a) {
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= a.R) return;
+    const long long nb = (long long)blockIdx.y * a.n_per, ne = nb + a.n_per < a.n ? nb + a.n_per : a.n;
+    float s[kWgrSmallK] = {};
+#pragma unroll 8
+    for (long long n = nb; n < ne; ++n) {
+        const float g = a.A[n * a.lda + r];
+#pragma unroll
+        for (int k = 0; k < kWgrSmallK; ++k)
+            if (k < a.K) s[k] = fmaf(g, a.X[n * a.ldx + k], s[k]);
+    }
+    float *out = a.part + (long long)blockIdx.y * a.R * a.K + (long long)r * a.K;
+#pragma unroll
+    for (int k = 0; k < kWgrSmallK; ++k)
+        if (k < a.K) out[k] = s[k];
 }
 
 // dW (torch layout [4H][K], real units only) = sum over the S slices of the padded partials [S][4Hp][K], in slice
