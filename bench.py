@@ -69,16 +69,24 @@ def pmc_traffic(kernel, suffix=""):
     return d[kernel]["hbm_bytes_corrected"], os.path.basename(f)
 
 
-def load_weights(dev, H):
+WEIGHT_KEYS = ("Wih0", "Wih1", "Wih2", "Whh0", "Whh1", "Whh2", "fcW", "fcb", "W_inp", "b_inp", "W_out")
+
+
+def weight_arrays(H):
+    """The benchmark's weights as float32 arrays: the reference-trained set at H = 50 (tests/golden), seeded synthetic
+    uniform(-1/sqrt(H), 1/sqrt(H)) otherwise."""
     if H == 50:
         w = np.load(os.path.join(ROOT, "tests", "golden", "weights_ref.npz"))
-        g = lambda k: torch.as_tensor(w[k])
-    else:
-        gen = torch.Generator().manual_seed(0)
-        shapes = {"Wih0": (4 * H, 5), "Wih1": (4 * H, H), "Wih2": (4 * H, H), "Whh0": (4 * H, H), "Whh1": (4 * H, H),
-                  "Whh2": (4 * H, H), "fcW": (4, H), "fcb": (4,), "W_inp": (50, 3), "b_inp": (50,), "W_out": (1, 50)}
-        rnd = {k: (torch.rand(s, generator=gen) * 2 - 1) / np.sqrt(H) for k, s in shapes.items()}
-        g = lambda k: rnd[k]
+        return {k: np.asarray(w[k], np.float32) for k in WEIGHT_KEYS}
+    gen = torch.Generator().manual_seed(0)
+    shapes = {"Wih0": (4 * H, 5), "Wih1": (4 * H, H), "Wih2": (4 * H, H), "Whh0": (4 * H, H), "Whh1": (4 * H, H),
+              "Whh2": (4 * H, H), "fcW": (4, H), "fcb": (4,), "W_inp": (50, 3), "b_inp": (50,), "W_out": (1, 50)}
+    return {k: ((torch.rand(s, generator=gen) * 2 - 1) / np.sqrt(H)).numpy() for k, s in shapes.items()}
+
+
+def load_weights(dev, H):
+    w = weight_arrays(H)
+    g = lambda k: torch.as_tensor(w[k])
     sim = fca.LSTMModel(5, H, 4, 3).to(dev)
     ctrl = fca.FNNModel(3, 50, 1, 1).to(dev)
     with torch.no_grad():
@@ -138,24 +146,27 @@ def host_cpu_info():
     return info
 
 
-def cpu_baseline(budget_s=24.0, N=10):
+def cpu_baseline(budget_s=24.0, N=10, H=50):
     """The reference CPU path (stock torch ops in MPCLoss's order, oracle/rollout_torch.py, with the
     reference's requires_grad on the frozen LSTM) timed on the host: forward + backward + AdamW per step,
     at B = 15 (the reference's training batch, UL/Main.py:84), B = 256 (BASELINE config 1 as written) and
     B = 4 096 (stands in for config 2's B = 65 536: rollout-steps/s is per (trajectory, step), and the CPU
     path is throughput-bound from a few thousand trajectories on), each on all usable host cores and on
     one thread. The reported value is B = 256 at the faster of the two thread counts (torch's intra-op
-    threads do not pay at these small per-op sizes on a shared host)."""
+    threads do not pay at these small per-op sizes on a shared host). At H > 52 (config 5) the same path on the
+    line's own N, H and weights, at B = 15 and B = 256 (a B = 256 step is ~1 s of host work there): B = 256 on all
+    usable cores only."""
     from oracle import rollout_torch as T
     info = host_cpu_info()
-    w = np.load(os.path.join(ROOT, "tests", "golden", "weights_ref.npz"))
+    w = weight_arrays(H)
     params = {"Wih": [w[f"Wih{k}"] for k in range(3)], "Whh": [w[f"Whh{k}"] for k in range(3)], "fcW": w["fcW"],
               "fcb": w["fcb"], "W_inp": w["W_inp"], "b_inp": w["b_inp"], "W_out": w["W_out"]}
     sim, ctrl = T.build_modules(params, torch.float32)
     opt = torch.optim.AdamW(ctrl.parameters(), lr=1e-4)
     runs = []
-    share = {15: 0.15, 256: 0.35, 4096: 0.5}
-    for B in (15, 256, 4096):
+    wide = H > 52
+    share = {15: 0.3, 256: 0.7} if wide else {15: 0.15, 256: 0.35, 4096: 0.5}
+    for B in share:
         X, S = synth_batch(B, "cpu", 99)
 
         def step():
@@ -165,7 +176,7 @@ def cpu_baseline(budget_s=24.0, N=10):
             loss.backward()
             opt.step()
 
-        for threads in (info["usable"], 1):
+        for threads in ((info["usable"],) if wide and B > 15 else (info["usable"], 1)):
             torch.set_num_threads(threads)
             step()
             t0 = time.perf_counter()
@@ -179,9 +190,12 @@ def cpu_baseline(budget_s=24.0, N=10):
     main_run = max((r for r in runs if r["batch"] == 256), key=lambda r: r["rollout_steps_per_s"])
     return {"value": main_run["rollout_steps_per_s"], "unit": "rollout-steps/s", "cores": main_run["threads"],
             "kind": "port",
-            "sample": f"oracle/rollout_torch.py fwd+bwd+AdamW (reference op order, LSTM weight grads on), N={N} "
-                      f"H=50; value = B=256 at the faster of {info['usable']} threads and 1 thread; B=4096 stands in "
-                      f"for B=65536 (per rollout-step rate); torch {torch.__version__}",
+            "sample": (f"oracle/rollout_torch.py fwd+bwd+AdamW (reference op order, LSTM weight grads on), N={N} "
+                       f"H={H}; value = B=256 at the faster of {info['usable']} threads and 1 thread; B=4096 stands in "
+                       f"for B=65536 (per rollout-step rate); torch {torch.__version__}") if not wide else
+                      (f"oracle/rollout_torch.py fwd+bwd+AdamW (reference op order, LSTM weight grads on), N={N} "
+                       f"H={H}, the line's seeded weights; value = B=256 on {info['usable']} threads (B=15 also on "
+                       f"1 thread); per rollout-step rate; torch {torch.__version__}"),
             "runs": runs, "host": info}
 
 
@@ -515,7 +529,8 @@ def main():
             line["out_max_rel_err"] = gc.pop("out_max_rel_err")
             line["grad_check"] = gc
         if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_budget, N=10)
+            # the line's own workload at H > 52 (config 5); the H <= 52 lines share config 2's (per rollout-step)
+            line["cpu_baseline"] = cpu_baseline(args.cpu_budget, N=N if H > 52 else 10, H=H if H > 52 else 50)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
