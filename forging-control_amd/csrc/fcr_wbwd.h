@@ -140,6 +140,9 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
                   kWbTileB = G::kTileB, kWbPieces = G::kPieces, kWbOffB = G::kOffB, kWbOffDown = G::kOffDown,
                   kWbOffW0 = G::kOffW0, kPPR = G::kPPR;
     using In = WbIn<kWbUnits>;
+    // who stages A: the producers for layers >= 1 when they are as many waves as the consumers (the piece split
+    // assumes kWbCons issuing waves), else the consumers
+    constexpr bool kProdDma = !L0 && kWbProd == G::kCons;
     using fU = typename In::fU;
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -320,7 +323,7 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
             // the step's barrier waits vmcnt(0) for them (and for the step's input loads: measured, the inputs
             // need no more than that one step in flight, round5_c5_bwd_pdma_ab.log)
             auto pbarrier_a = [] { asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-            if (prod) dma(0, 0);
+            if (kProdDma && prod) dma(0, 0);
             // inputs three steps ahead in rotating register sets (unrolled by three: a copy between sets would wait
             // for the loads)
             In x0 = load_in(0), x1, x2;
@@ -336,7 +339,7 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
                 pbarrier_a();                                  // tile ks published, stage ks landed
                 FCR_WB_ST(tw1);
                 if (FULL || ks + 3 < nk) xload = load_in(ks + 3);
-                if (prod && ks + 1 < nk) dma(ks + 1, (ks + 1) & 1);
+                if (kProdDma && prod && ks + 1 < nk) dma(ks + 1, (ks + 1) & 1);
                 FCR_WB_ST(tw2);
                 if (FULL || ks + 1 < nk) dgates(ks + 1, xuse, (ks & 1) ^ 1);   // (its buffer was read at ks - 1)
                 FCR_WB_ST(tw3);
@@ -398,7 +401,7 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
 #pragma unroll
             for (int j = 0; j < kWbTN; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         const int fr = lane & 15, fq = lane >> 4;
-        if (prod && L0) dma(0, 0);
+        if (!kProdDma && prod) dma(0, 0);
         barrier();
         unsigned long long sc[4] = {0, 0, 0, 0}, tc0 = 0, tc1 = 0, tc2 = 0;
         (void)sc, (void)tc0, (void)tc1, (void)tc2;
@@ -408,7 +411,7 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
             barrier();   // stage ks's A landed (its issuing waves waited for their pieces), tile ks written
             FCR_WB_ST(tc1);
             if (!prod) continue;
-            if (L0 && ks + 1 < nk) dma(ks + 1, buf ^ 1);   // into the stage every consumer finished reading at ks - 1
+            if (!kProdDma && ks + 1 < nk) dma(ks + 1, buf ^ 1);   // into the stage every consumer finished reading at ks - 1
             FCR_WB_ST(tc2);
             if (FCR_WB_STAMP) {
                 sc[0] += tc1 - tc0;
