@@ -26,3 +26,18 @@ def test_every_round_pmc_summary_has_its_kernels():
         assert keys, f"{os.path.basename(path)} holds no kernel"
         if re.search(r"_c5_pmc\.json$", path):
             assert d.get("bwd_pass", {}).get("hbm_bytes_corrected"), path
+
+
+def test_config3_lines_read_their_own_pmc_summaries():
+    for prec in ("f16", "fp32"):
+        t, src = bench.pmc_traffic("fcr_bwd_kernel", f"_c3{prec}")
+        assert t and t > 1e9 and f"c3{prec}" in src, src
+
+
+def test_wide_cpu_baseline_times_the_lines_own_workload():
+    """A config-5 line's cpu_baseline runs the CPU path at its own N and H (seeded weights), not config 2's."""
+    r = bench.cpu_baseline(0.2, N=2, H=64)
+    assert r["value"] > 0 and "N=2 H=64" in r["sample"], r["sample"]
+    assert {x["batch"] for x in r["runs"]} == {15, 256}
+    r50 = bench.cpu_baseline(0.2, N=2, H=50)
+    assert "H=50" in r50["sample"] and {x["batch"] for x in r50["runs"]} == {15, 256, 4096}
