@@ -6,9 +6,9 @@
 // Product: out[b][n] = sum_r dG[b][r] W[r][n] over the 4H gate rows r, fp32-accurate from f16 halves: with dG = dG_hi
 // + dG_lo (each trajectory row's dgates times its own power of two) and W = W_hi + W_lo,
 //   out = (W_lo dG_hi + W_hi dG_lo + W_hi dG_hi) / scale_b    (three MFMAs per k-block; the dropped lo·lo <= 2^-22)
-// A = W^T split [NP][4H] (row n = output column, W_ih column n for n < H, W_hh column n - H; layer 0: W_hh only) with
-// the K index UNIT-major, r' = 4 unit + gate (wide_split_bt_kernel), so a K step of 32 is 8 whole units: the dgates
-// of one K step need only those units' inputs.
+// A = W^T split, [NP][4H / 32][hi (32) | lo (32)] (row n = output column, W_ih column n for n < H, W_hh column n - H;
+// layer 0: W_hh only; a K step's halves of one row are one 128-B line) with the K index UNIT-major, r' = 4 unit + gate
+// (wide_split_bt_kernel), so a K step of 32 is 8 whole units: the dgates of one K step need only those units' inputs.
 // Tile: a workgroup owns 256 output columns x 128 trajectories, and its 8 waves split by ROLE (round 4): waves 0-3
 // produce the B tiles (the step's dgates, hi | lo), waves 4-7 consume them (each 64 columns x all 128 trajectories =
 // 4 x 8 D tiles; lane = trajectory, 4 consecutive columns: one 16-B store). Wave w runs on SIMD w % 4, so every SIMD
@@ -18,8 +18,9 @@
 // steps of 32: A through a 2-stage LDS-DMA ring (W^T is L2-resident), in whole 128-B lines, issued by the producers
 // for layers >= 1 (by the consumers for layer 0, whose producers carry the window-row gradient); the B tile of step
 // ks + 1 is formed while the consumers multiply step ks. Producer thread (row r = tid / 2, half p = tid % 2) loads
-// units 8s + 4p .. + 3 of its trajectory (pre-activations, c_{t-1}, dh, din, dc: 16-B loads, one step ahead), forms
-// their 16 dgates and dc_{t-1} from the forward's saved activations, splits them into the two 16-B chunks of
+// units 8s + 4p .. + 3 of its trajectory — their activations (the forward's [unit][gate] rows: 64 contiguous B) and
+// c_{t-1}, dh, din, dc (k8 rows, fcr_wide.h: a step's units of consecutive trajectories contiguous), issued three
+// steps ahead in rotating register sets — forms their 16 dgates and dc_{t-1}, splits them into the two 16-B chunks of
 // its row half. With two column blocks (NO > 256) both form the same dgates; the first writes dc_{t-1}.
 // Row scale: 2^(13 - e), e the exponent of a bound on the row's |dgates|: |dgate| <= |dc_t| <= |dc| + |dh_rec| +
 // |din| (forget row: x (kL - 1) / 4, fcr_wide.h kWideDgExp). The three maxima come from the kernels that wrote those
