@@ -485,25 +485,38 @@ int launch_wgemm_cell(const WgArgs &wa, hipStream_t s) {
 
 // One backward cell of the fused path (fcr_wbwd.h): dgates formed in the product's prologue, out = dG [W_ih | W_hh]
 // (columns [0, NO), NO = 0: the dgate part only) in true units
+#ifndef FCR_WB_N256
+#define FCR_WB_N256 1   // layers >= 1 on 256 columns x 256 trajectories (WbG256w, fcr_wbwd.h): A staged once per 256
+                        // trajectories, backward −5.4 % at config 5 (round5_c5_n256_ab_*.log); 0: 256 x 128 (WbG256)
+#endif
 int launch_fb(const WbArgs &wa, bool l0, hipStream_t s) {
-    static std::atomic<unsigned long long> attr_done[4] = {{0}, {0}, {0}, {0}};
+    static std::atomic<unsigned long long> attr_done[5] = {{0}, {0}, {0}, {0}, {0}};
     const bool w0g = l0 && wa.H > kWbW0LdsUnits, wide = wb_wide(l0, wa.H);
-    const int kind = l0 ? (w0g ? 2 : 1) : (wide ? 3 : 0);
+    const int kind = l0 ? (w0g ? 2 : 1) : (wide ? 3 : (FCR_WB_N256 ? 4 : 0));
     const void *fn = kind == 0   ? (const void *)wide_bwd_fused_kernel<WbG256, false>
                      : kind == 1 ? (const void *)wide_bwd_fused_kernel<WbG256, true, false>
 #if FCR_WB512
                      : kind == 3 ? (const void *)wide_bwd_fused_kernel<WbG512, false>
 #endif
+#if FCR_WB_N256
+                     : kind == 4 ? (const void *)wide_bwd_fused_kernel<WbG256w, false>
+#endif
                                  : (const void *)wide_bwd_fused_kernel<WbG256, true, true>;
-    if (const int rc = lds_attr(fn, wide ? kWbLds512 : kWbLds256, attr_done[kind], "wbwd")) return rc;
+    if (const int rc = lds_attr(fn, wide ? kWbLds512 : kind == 4 ? kWbLds256w : kWbLds256, attr_done[kind], "wbwd"))
+        return rc;
     if (wa.NO < 0 || wa.NO > 2 * wa.H || wa.NO % 8 || wa.H % 8 || wa.NB <= 0 || (wa.rm_h && wa.nrh < 1) ||
         (wa.rm_d && wa.nrd < 1) || (l0 && (!wa.wih0 || !wa.rowg)))
         return fail(FCR_EINVAL, "wide_bwd_fused_kernel: NO %d H %d B %d off its tiling", wa.NO, wa.H, wa.NB);
-    const int M = wide ? WbG512::kM : WbG256::kM, N = wide ? WbG512::kN : WbG256::kN;
+    const int M = wide ? WbG512::kM : WbG256::kM, N = wide ? WbG512::kN : kind == 4 ? WbG256w::kN : WbG256::kN;
     const dim3 grid((unsigned)((wa.NB + N - 1) / N * (wa.NO > 0 ? (wa.NO + M - 1) / M : 1)));
 #if FCR_WB512
     if (kind == 3)
         hipLaunchKernelGGL((wide_bwd_fused_kernel<WbG512, false>), grid, dim3(WbG512::kThreads), wb_lds_bytes<WbG512>(false, wa.H), s, wa);
+    else
+#endif
+#if FCR_WB_N256
+    if (kind == 4)
+        hipLaunchKernelGGL((wide_bwd_fused_kernel<WbG256w, false>), grid, dim3(WbG256w::kThreads), wb_lds_bytes<WbG256w>(false, wa.H), s, wa);
     else
 #endif
     if (kind == 0)

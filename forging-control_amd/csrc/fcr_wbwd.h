@@ -9,9 +9,10 @@
 // A = W^T split, [NP][4H / 32][hi (32) | lo (32)] (row n = output column, W_ih column n for n < H, W_hh column n - H;
 // layer 0: W_hh only; a K step's halves of one row are one 128-B line) with the K index UNIT-major, r' = 4 unit + gate
 // (wide_split_bt_kernel), so a K step of 32 is 8 whole units: the dgates of one K step need only those units' inputs.
-// Tile: a workgroup owns 256 output columns x 128 trajectories, and its 8 waves split by ROLE (round 4): waves 0-3
-// produce the B tiles (the step's dgates, hi | lo), waves 4-7 consume them (each 64 columns x all 128 trajectories =
-// 4 x 8 D tiles; lane = trajectory, 4 consecutive columns: one 16-B store). Wave w runs on SIMD w % 4, so every SIMD
+// Tile (WbG256, layer 0): a workgroup owns 256 output columns x 128 trajectories, and its 8 waves split by ROLE
+// (round 4): waves 0-3 produce the B tiles (the step's dgates, hi | lo), waves 4-7 consume them (each 64 columns x all
+// 128 trajectories = 4 x 8 D tiles; lane = trajectory, 4 consecutive columns: one 16-B store). Layers >= 1 run
+// WbG256w (256 x 256, 4 + 8 waves, round 5). Wave w runs on SIMD w % 4, so every SIMD
 // holds one producer and one consumer: the producer's transcendental chains issue while its partner's MFMAs run
 // (with every wave doing both in turn, the step barrier lined the two waves of a SIMD up on the same phase, and the
 // dgate chains were the critical path: 247 ms of backward against 168 ms with the activations stubbed out). K in
@@ -46,6 +47,7 @@ struct WbGeo {
     static constexpr int kWaves = kWbProd + CONS, kThreads = 64 * kWaves;
     static constexpr int kTM = M / CONS / 16, kTN = N / 16;   // D tiles per consumer wave
     static constexpr int kPPR = 8 / U;                          // producer threads per trajectory row
+    static constexpr int kRPT = 8 * N / (64 * kWbProd * U);     // trajectory rows per producer thread
     static constexpr int kStage = M * kWbK * 4;                 // A rows of [hi (64 B) | lo (64 B)]
     static constexpr int kTileB = N * kWbK * 2;                 // one split half of the dgate tile
     static constexpr int kPieces = kStage / 1024 / CONS;        // LDS-DMA pieces per consumer wave per stage
@@ -53,7 +55,7 @@ struct WbGeo {
     static constexpr int kOffDown = kOffB + 4 * kTileB;
     static constexpr int kOffW0 = kOffDown + N * 4;             // layer 0: W_ih0 as [unit][gate][kIn]
     static_assert(kStage % (1024 * CONS) == 0, "DMA pieces");
-    static_assert(64 * kWbProd * U == 8 * N, "dgate mapping: a step's 8 units of every row over the producers");
+    static_assert(kRPT >= 1 && kRPT * 64 * kWbProd * U == 8 * N, "dgate mapping: a step's 8 units of every row");
     static_assert(U == 2 || U == 4, "units per producer thread");
 };
 // 256 columns x 128 trajectories, 4 + 4 waves (round 4): every layer; two column blocks at Hp = 256 form the same dgates
@@ -61,10 +63,15 @@ using WbG256 = WbGeo<256, 128, 4, 4>;
 // 512 columns x 64 trajectories, 4 + 8 waves: a layer >= 1 cell's whole [input gradient | dh_{t-1}] at Hp = 256 in one
 // workgroup, so its dgates are formed (and its rows read) once
 using WbG512 = WbGeo<512, 64, 8, 2>;
+// 256 columns x 256 trajectories, 4 + 8 waves (layers >= 1 by default, FCR_WB_N256): A staged once per 256
+// trajectories (half the A bytes per trajectory of WbG256); each producer thread forms the dgates of two rows, each
+// consumer 32 columns x 256 trajectories; 168 registers per wave (12 waves), 129 KB of LDS
+using WbG256w = WbGeo<256, 256, 8, 4>;
 constexpr int kWbW0LdsUnits = 768;                        // layer 0 with H above: W_ih0 read from global memory
 constexpr int kWbLds256 = WbG256::kOffW0 + 4 * kWbW0LdsUnits * kIn * 4;
 constexpr int kWbLds512 = WbG512::kOffW0;                 // (layers >= 1 only: no W_ih0 block)
-static_assert(kWbLds256 <= 163840 && kWbLds512 <= 163840, "LDS");
+constexpr int kWbLds256w = WbG256w::kOffW0;               // (layers >= 1 only)
+static_assert(kWbLds256 <= 163840 && kWbLds512 <= 163840 && kWbLds256w <= 163840, "LDS");
 // LDS bytes of one launch: the W_ih0 block only for layer 0 with H <= kWbW0LdsUnits
 template <class G>
 __host__ __device__ constexpr int wb_lds_bytes(bool l0, int H) {
@@ -161,21 +168,34 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
     const int m0 = cb * kWbM;                               // first output column
     const int b0 = (wg / ny) * kWbN;                        // first trajectory
 
-    // ---- producer thread: its dgate row and unit share; the row's scale from the producers' bounds ----
-    const int er = (tid / kPPR) & (kWbN - 1), ep = tid % kPPR;   // (consumers: unused)
-    const int eb = b0 + er < a.NB ? b0 + er : a.NB - 1;    // tail rows recompute the last trajectory (not stored)
-    const bool elive = b0 + er < a.NB;
-    float up = 0.0f;
+    // ---- producer thread: its dgate rows (kRPT of them) and unit share; each row's scale from the producers' bounds
+    constexpr int kRPT = G::kRPT;
+    static_assert(!L0 || kRPT == 1, "layer 0 runs the one-row producer");
+    const int er0 = (tid / kPPR) & (kWbN / kRPT - 1), ep = tid % kPPR;   // (consumers: unused)
+    int er[kRPT], eb[kRPT];
+    bool elive[kRPT];
+    float up[kRPT];
+#pragma unroll
+    for (int h = 0; h < kRPT; ++h) {
+        er[h] = er0 + h * (kWbN / kRPT);
+        eb[h] = b0 + er[h] < a.NB ? b0 + er[h] : a.NB - 1;   // tail rows recompute the last trajectory (not stored)
+        elive[h] = b0 + er[h] < a.NB;
+        up[h] = 0.0f;
+    }
     if (producer) {
-        float mh = 0.0f, md = 0.0f;
-        if (a.rm_h)
-            for (int k = 0; k < a.nrh; ++k) mh = fmaxf(mh, a.rm_h[(size_t)k * a.NB + eb]);
-        if (a.rm_d)
-            for (int k = 0; k < a.nrd; ++k) md = fmaxf(md, a.rm_d[(size_t)k * a.NB + eb]);
-        const float m = (a.rm_c ? a.rm_c[eb] : 0.0f) + mh + md;
-        const int ex = m > 0.0f ? __builtin_amdgcn_frexp_expf(m) : 0;   // every |dgate| < 2^ex (times (kL-1)/4: forget)
-        up = __builtin_amdgcn_ldexpf(1.0f, kWideDgExp - ex);
-        if (ep == 0) reinterpret_cast<float *>(lds + kWbOffDown)[er] = __builtin_amdgcn_ldexpf(1.0f, ex - kWideDgExp);
+#pragma unroll
+        for (int h = 0; h < kRPT; ++h) {
+            float mh = 0.0f, md = 0.0f;
+            if (a.rm_h)
+                for (int k = 0; k < a.nrh; ++k) mh = fmaxf(mh, a.rm_h[(size_t)k * a.NB + eb[h]]);
+            if (a.rm_d)
+                for (int k = 0; k < a.nrd; ++k) md = fmaxf(md, a.rm_d[(size_t)k * a.NB + eb[h]]);
+            const float m = (a.rm_c ? a.rm_c[eb[h]] : 0.0f) + mh + md;
+            const int ex = m > 0.0f ? __builtin_amdgcn_frexp_expf(m) : 0;   // every |dgate| < 2^ex (x (kL-1)/4: forget)
+            up[h] = __builtin_amdgcn_ldexpf(1.0f, kWideDgExp - ex);
+            if (ep == 0)
+                reinterpret_cast<float *>(lds + kWbOffDown)[er[h]] = __builtin_amdgcn_ldexpf(1.0f, ex - kWideDgExp);
+        }
     }
     float *w0s = reinterpret_cast<float *>(lds + kWbOffW0);
     if constexpr (L0 && !W0G) {   // W_ih0, packed [unit][gate][kIn] by the host, into LDS as it is (16-B copies)
@@ -215,31 +235,28 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
     };
 
     // ---- producers: inputs ahead, the tile one step ahead of the MFMAs ----
-    const float *pre = a.act + (size_t)eb * K;
     // k8 rows: this thread's U units of step s at + s * 8 NB
-    const size_t kso = (size_t)8 * a.NB, ko = (size_t)eb * 8 + kWbUnits * ep;
-    const float *cpr = a.c_prev ? a.c_prev + ko : nullptr;
-    const float *dhr = a.dh ? a.dh + ko : nullptr;
-    const float *dnr = a.din ? a.din + ko : nullptr;
-    const float *dcr = a.dC ? a.dC + ko : nullptr;
-    float *dco_r = a.dC_out + ko;
+    const size_t kso = (size_t)8 * a.NB;
     auto ldu = [](const float *p) { return *reinterpret_cast<const fU *>(p); };
-    auto load_in = [&](int s) {
+    auto load_in = [&](int h, int s) {
         In x;
         const int u = 8 * s + kWbUnits * ep;
-        const size_t so = s * kso;
+        const size_t so = s * kso + (size_t)eb[h] * 8 + kWbUnits * ep;
+        const float *pre = a.act + (size_t)eb[h] * K;
 #pragma unroll
         for (int k = 0; k < kWbUnits; ++k) x.ac[k] = *reinterpret_cast<const f32x4 *>(pre + 4 * (u + k));
-        x.cp = cpr ? ldu(cpr + so) : fU{};
-        x.dh = dhr ? ldu(dhr + so) : fU{};
-        x.dn = dnr ? ldu(dnr + so) : fU{};
-        x.dc = dcr ? ldu(dcr + so) : fU{};
+        x.cp = a.c_prev ? ldu(a.c_prev + so) : fU{};
+        x.dh = a.dh ? ldu(a.dh + so) : fU{};
+        x.dn = a.din ? ldu(a.din + so) : fU{};
+        x.dc = a.dC ? ldu(a.dC + so) : fU{};
         return x;
     };
-    const bool wr_dc = cb == 0 && elive;   // every column block forms the same dc_{t-1}: the first stores it
-    float mdc = 0.0f;                      // max |dc_{t-1}| of this thread's units
+    float mdc[kRPT];                       // max |dc_{t-1}| of this thread's units, per row
+#pragma unroll
+    for (int h = 0; h < kRPT; ++h) mdc[h] = 0.0f;
     float pc[kIn] = {};                    // layer 0: this thread's share of the window-row gradient
-    auto dgates = [&](int s, const In &x, int buf) {
+    auto dgates = [&](int h, int s, const In &x, int buf) {
+        const bool wr_dc = cb == 0 && elive[h];   // every column block forms the same dc_{t-1}: the first stores it
         float dg[4 * kWbUnits];
         fU dco;
         const int u = 8 * s + kWbUnits * ep;
@@ -256,9 +273,9 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
             dg[4 * k + 3] = dh * tc * (o - o * o);
             dco[k] = dct * f;
         }
-        if (wr_dc) *reinterpret_cast<fU *>(dco_r + s * kso) = dco;
+        if (wr_dc) *reinterpret_cast<fU *>(a.dC_out + s * kso + (size_t)eb[h] * 8 + kWbUnits * ep) = dco;
         if (a.dg && wr_dc) {   // (column block 0 writes them: every block forms the same)
-            float *d = a.dg + (size_t)eb * K + u;
+            float *d = a.dg + (size_t)eb[h] * K + u;
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 fU v;
@@ -268,7 +285,7 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
             }
         }
 #pragma unroll
-        for (int k = 0; k < kWbUnits; ++k) mdc = fmaxf(mdc, fabsf(dco[k]));
+        for (int k = 0; k < kWbUnits; ++k) mdc[h] = fmaxf(mdc[h], fabsf(dco[k]));
         if constexpr (L0) {   // sum_r dG[b][r] W_ih0[r][c] over this thread's 4 U gate rows, fp32
             const f32x4 *w4 = reinterpret_cast<const f32x4 *>(w0l + u * 4 * kIn);   // 20 U floats: units u .. u + U - 1
 #pragma unroll
@@ -288,11 +305,11 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
             constexpr int NW = 2 * kWbUnits;   // 32-bit words of halves
             unsigned hw[NW], lw[NW];
 #pragma unroll
-            for (int p = 0; p < NW; ++p) mix_pair(dg[2 * p], up, dg[2 * p + 1], up, hw[p], lw[p]);
+            for (int p = 0; p < NW; ++p) mix_pair(dg[2 * p], up[h], dg[2 * p + 1], up[h], hw[p], lw[p]);
             char *bt = lds + kWbOffB + buf * 2 * kWbTileB;
 #pragma unroll
             for (int c = 0; c < kWbUnits / 2; ++c) {
-                const uint32_t o = wb_off(er, kWbUnits / 2 * ep + c);
+                const uint32_t o = wb_off(er[h], kWbUnits / 2 * ep + c);
                 *reinterpret_cast<u32x4 *>(bt + o) = u32x4{hw[4 * c], hw[4 * c + 1], hw[4 * c + 2], hw[4 * c + 3]};
                 *reinterpret_cast<u32x4 *>(bt + kWbTileB + o) = u32x4{lw[4 * c], lw[4 * c + 1], lw[4 * c + 2], lw[4 * c + 3]};
             }
@@ -318,7 +335,29 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
         // a producer's barrier waits only for its LDS tile writes: its input loads stay in flight across it, and the
         // compiler's own wait before their first use (exact counts: no DMA intrinsic in the kernel) is all
         auto pbarrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-        if constexpr (!L0) {
+        if constexpr (!L0 && kRPT == 2) {
+            // two rows per thread (WbG256w): one register set per row, refilled for step ks + 2 right after step
+            // ks + 1's dgates consumed it (a second set per row would not fit the 12-wave register budget); A is
+            // staged by the consumers
+            In x[kRPT];
+#pragma unroll
+            for (int h = 0; h < kRPT; ++h) x[h] = load_in(h, 0);
+            barrier();   // the row scales in LDS
+#pragma unroll
+            for (int h = 0; h < kRPT; ++h) {
+                dgates(h, 0, x[h], 0);
+                if (nk > 1) x[h] = load_in(h, 1);
+            }
+            for (int ks = 0; ks < nk; ++ks) {
+                pbarrier();   // tile ks published
+                if (ks + 1 < nk)
+#pragma unroll
+                    for (int h = 0; h < kRPT; ++h) {
+                        dgates(h, ks + 1, x[h], (ks & 1) ^ 1);
+                        if (ks + 2 < nk) x[h] = load_in(h, ks + 2);
+                    }
+            }
+        } else if constexpr (!L0) {
             // Layers >= 1: the producers also stage A (the consumers then only read and multiply): step ks's pieces
             // of stage ks + 1 go out after its barrier (the slot every consumer finished reading at ks - 1), and
             // the step's barrier waits vmcnt(0) for them (and for the step's input loads: measured, the inputs
@@ -327,11 +366,11 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
             if (kProdDma && prod) dma(0, 0);
             // inputs three steps ahead in rotating register sets (unrolled by three: a copy between sets would wait
             // for the loads)
-            In x0 = load_in(0), x1, x2;
-            if (nk > 1) x1 = load_in(1);
-            if (nk > 2) x2 = load_in(2);
+            In x0 = load_in(0, 0), x1, x2;
+            if (nk > 1) x1 = load_in(0, 1);
+            if (nk > 2) x2 = load_in(0, 2);
             barrier();   // W_ih0 and the row scales in LDS
-            dgates(0, x0, 0);
+            dgates(0, 0, x0, 0);
             unsigned long long sw[4] = {0, 0, 0, 0}, tw0 = 0, tw1 = 0, tw2 = 0, tw3 = 0;
             (void)sw, (void)tw0, (void)tw1, (void)tw2, (void)tw3;
             auto pstep = [&](auto full, int ks, const In &xuse, In &xload) {
@@ -339,10 +378,10 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
                 FCR_WB_ST(tw0);
                 pbarrier_a();                                  // tile ks published, stage ks landed
                 FCR_WB_ST(tw1);
-                if (FULL || ks + 3 < nk) xload = load_in(ks + 3);
+                if (FULL || ks + 3 < nk) xload = load_in(0, ks + 3);
                 if (kProdDma && prod && ks + 1 < nk) dma(ks + 1, (ks + 1) & 1);
                 FCR_WB_ST(tw2);
-                if (FULL || ks + 1 < nk) dgates(ks + 1, xuse, (ks & 1) ^ 1);   // (its buffer was read at ks - 1)
+                if (FULL || ks + 1 < nk) dgates(0, ks + 1, xuse, (ks & 1) ^ 1);   // (its buffer was read at ks - 1)
                 FCR_WB_ST(tw3);
                 if (FCR_WB_STAMP) {
                     sw[0] += tw1 - tw0;
@@ -370,27 +409,30 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
 #endif
         } else {
             // layer 0 (the window-row gradient's W_ih0 reads and accumulators) has registers for one set ahead
-            In xc = load_in(0);
+            In xc = load_in(0, 0);
             barrier();
-            dgates(0, xc, 0);
-            if (nk > 1) xc = load_in(1);
+            dgates(0, 0, xc, 0);
+            if (nk > 1) xc = load_in(0, 1);
             for (int ks = 0; ks < nk; ++ks) {
                 pbarrier();
                 In xn;
-                if (ks + 2 < nk) xn = load_in(ks + 2);
-                if (ks + 1 < nk) dgates(ks + 1, xc, (ks & 1) ^ 1);
+                if (ks + 2 < nk) xn = load_in(0, ks + 2);
+                if (ks + 1 < nk) dgates(0, ks + 1, xc, (ks & 1) ^ 1);
                 if (ks + 2 < nk) xc = xn;
             }
         }
         // per-row results: dc_{t-1} bound, layer 0's window-row gradient
-        mdc = row_max(mdc);
-        if (a.rm_c_out && wr_dc && ep == 0) a.rm_c_out[eb] = mdc;
+#pragma unroll
+        for (int h = 0; h < kRPT; ++h) {
+            const float m = row_max(mdc[h]);
+            if (a.rm_c_out && cb == 0 && elive[h] && ep == 0) a.rm_c_out[eb[h]] = m;
+        }
         if constexpr (L0) {
 #pragma unroll
             for (int c = 0; c < kIn; ++c) pc[c] = row_sum(pc[c]);
-            if (a.rowg && elive && cb == 0 && ep == 0)
+            if (a.rowg && elive[0] && cb == 0 && ep == 0)
 #pragma unroll
-                for (int c = 0; c < kIn; ++c) a.rowg[(size_t)eb * kIn + c] += pc[c];
+                for (int c = 0; c < kIn; ++c) a.rowg[(size_t)eb[0] * kIn + c] += pc[c];
         }
         if (!prod) return;
         barrier();   // (the consumers' epilogue reuses the A stages)
