@@ -104,8 +104,8 @@ struct WbArgs {
     float *rowg;                 // layer 0: [B][kIn] window-row gradient row (+=), else null
 };
 
-// Diagnostic build FCR_WB_STAMP=1 (scripts/stamp_wb.py): per-wave s_memtime sums of the layer >= 1 kernel's K-step
-// sections, added into fcr_wb_stamp by lane 0 (vector atomics) — consumers: barrier wait, A DMA issue, fragment reads +
+// Diagnostic build FCR_WB_STAMP=1 (scripts/stamp_wb.py; with -DFCR_WB_N256=0: the stamps sit in the one-row producer
+// of WbG256, which layers >= 1 run in that build): per-wave s_memtime sums of the layer >= 1 kernel's K-step sections, added into fcr_wb_stamp by lane 0 (vector atomics) — consumers: barrier wait, A DMA issue, fragment reads +
 // MFMA issue; producers: barrier wait, input load issue, dgates (including the wait for their inputs) + tile writes.
 // Read the shares, never the build's run time (each stamp drains lgkmcnt).
 #ifndef FCR_WB_STAMP

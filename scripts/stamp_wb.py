@@ -1,4 +1,5 @@
-"""Section shares of config 5's fused backward cell (layers >= 1) from an FCR_WB_STAMP=1 build (diagnostic):
+"""Section shares of config 5's fused backward cell (layers >= 1) from an FCR_WB_STAMP=1 FCR_WB_N256=0 build
+(diagnostic; the stamps are in WbG256's one-row producer):
 
     python scripts/stamp_wb.py lib_ab/wbstamp.so [--batch 65536] [--horizon 2]
 Runs scripts/kbench.py's config-5 step with every window kept, then reads fcr_debug_wb_stamp: cycles per K step and
