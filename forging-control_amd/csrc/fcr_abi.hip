@@ -492,7 +492,11 @@ int launch_wgemm_cell(const WgArgs &wa, hipStream_t s) {
 int launch_fb(const WbArgs &wa, bool l0, hipStream_t s) {
     static std::atomic<unsigned long long> attr_done[5] = {{0}, {0}, {0}, {0}, {0}};
     const bool w0g = l0 && wa.H > kWbW0LdsUnits, wide = wb_wide(l0, wa.H);
-    const int kind = l0 ? (w0g ? 2 : 1) : (wide ? 3 : (FCR_WB_N256 ? 4 : 0));
+    // WbG256w halves the workgroups per cell: only where they still fill the chip (B >= 32 768: >= 256 of them at
+    // two column blocks); smaller batches keep WbG256's parallelism (the surrogate's B = 256 step: 3.2 vs 4.1 ms).
+    // Cells that also write their dgates (the surrogate's weight gradients) measured 2 % slower on it: WbG256
+    const bool n256 = FCR_WB_N256 && wa.NB >= 32768 && !wa.dg;
+    const int kind = l0 ? (w0g ? 2 : 1) : (wide ? 3 : (n256 ? 4 : 0));
     const void *fn = kind == 0   ? (const void *)wide_bwd_fused_kernel<WbG256, false>
                      : kind == 1 ? (const void *)wide_bwd_fused_kernel<WbG256, true, false>
 #if FCR_WB512
