@@ -485,18 +485,24 @@ int launch_wgemm_cell(const WgArgs &wa, hipStream_t s) {
 
 // One backward cell of the fused path (fcr_wbwd.h): dgates formed in the product's prologue, out = dG [W_ih | W_hh]
 // (columns [0, NO), NO = 0: the dgate part only) in true units
+#ifndef FCR_WB_L0_N256
+#define FCR_WB_L0_N256 0   // 1: layer 0 on WbG256w too (H <= kWbW0LdsUnits256w): its W_ih0 accumulation spills
+                           // ~320 registers at the 12-wave budget, backward +57 % (round5_c5_l0w_ab_keepall.log)
+#endif
 #ifndef FCR_WB_N256
 #define FCR_WB_N256 1   // layers >= 1 on 256 columns x 256 trajectories (WbG256w, fcr_wbwd.h): A staged once per 256
                         // trajectories, backward −5.4 % at config 5 (round5_c5_n256_ab_*.log); 0: 256 x 128 (WbG256)
 #endif
 int launch_fb(const WbArgs &wa, bool l0, hipStream_t s) {
-    static std::atomic<unsigned long long> attr_done[5] = {{0}, {0}, {0}, {0}, {0}};
+    static std::atomic<unsigned long long> attr_done[6] = {{0}, {0}, {0}, {0}, {0}, {0}};
     const bool w0g = l0 && wa.H > kWbW0LdsUnits, wide = wb_wide(l0, wa.H);
     // WbG256w halves the workgroups per cell: only where they still fill the chip (B >= 32 768: >= 256 of them at
     // two column blocks); smaller batches keep WbG256's parallelism (the surrogate's B = 256 step: 3.2 vs 4.1 ms).
     // Cells that also write their dgates (the surrogate's weight gradients) measured 2 % slower on it: WbG256
     const bool n256 = FCR_WB_N256 && wa.NB >= 32768 && !wa.dg;
-    const int kind = l0 ? (w0g ? 2 : 1) : (wide ? 3 : (n256 ? 4 : 0));
+    // layer 0 on it too while its W_ih0 block fits beside it in LDS (H <= kWbW0LdsUnits256w)
+    const bool l0w = FCR_WB_L0_N256 && n256 && wa.H <= kWbW0LdsUnits256w;
+    const int kind = l0 ? (l0w ? 5 : w0g ? 2 : 1) : (wide ? 3 : (n256 ? 4 : 0));
     const void *fn = kind == 0   ? (const void *)wide_bwd_fused_kernel<WbG256, false>
                      : kind == 1 ? (const void *)wide_bwd_fused_kernel<WbG256, true, false>
 #if FCR_WB512
@@ -504,14 +510,19 @@ int launch_fb(const WbArgs &wa, bool l0, hipStream_t s) {
 #endif
 #if FCR_WB_N256
                      : kind == 4 ? (const void *)wide_bwd_fused_kernel<WbG256w, false>
+#if FCR_WB_L0_N256
+                     : kind == 5 ? (const void *)wide_bwd_fused_kernel<WbG256w, true, false>
+#endif
 #endif
                                  : (const void *)wide_bwd_fused_kernel<WbG256, true, true>;
-    if (const int rc = lds_attr(fn, wide ? kWbLds512 : kind == 4 ? kWbLds256w : kWbLds256, attr_done[kind], "wbwd"))
+    const int lds_max = wide ? kWbLds512 : kind == 4 ? kWbLds256w
+                                         : kind == 5 ? wb_lds_bytes<WbG256w>(true, kWbW0LdsUnits256w) : kWbLds256;
+    if (const int rc = lds_attr(fn, lds_max, attr_done[kind], "wbwd"))
         return rc;
     if (wa.NO < 0 || wa.NO > 2 * wa.H || wa.NO % 8 || wa.H % 8 || wa.NB <= 0 || (wa.rm_h && wa.nrh < 1) ||
         (wa.rm_d && wa.nrd < 1) || (l0 && (!wa.wih0 || !wa.rowg)))
         return fail(FCR_EINVAL, "wide_bwd_fused_kernel: NO %d H %d B %d off its tiling", wa.NO, wa.H, wa.NB);
-    const int M = wide ? WbG512::kM : WbG256::kM, N = wide ? WbG512::kN : kind == 4 ? WbG256w::kN : WbG256::kN;
+    const int M = wide ? WbG512::kM : WbG256::kM, N = wide ? WbG512::kN : kind >= 4 ? WbG256w::kN : WbG256::kN;
     const dim3 grid((unsigned)((wa.NB + N - 1) / N * (wa.NO > 0 ? (wa.NO + M - 1) / M : 1)));
 #if FCR_WB512
     if (kind == 3)
@@ -522,6 +533,11 @@ int launch_fb(const WbArgs &wa, bool l0, hipStream_t s) {
     if (kind == 4)
         hipLaunchKernelGGL((wide_bwd_fused_kernel<WbG256w, false>), grid, dim3(WbG256w::kThreads), wb_lds_bytes<WbG256w>(false, wa.H), s, wa);
     else
+#if FCR_WB_L0_N256
+    if (kind == 5)
+        hipLaunchKernelGGL((wide_bwd_fused_kernel<WbG256w, true, false>), grid, dim3(WbG256w::kThreads), wb_lds_bytes<WbG256w>(true, wa.H), s, wa);
+    else
+#endif
 #endif
     if (kind == 0)
         hipLaunchKernelGGL((wide_bwd_fused_kernel<WbG256, false>), grid, dim3(WbG256::kThreads), wb_lds_bytes<WbG256>(false, wa.H), s, wa);

@@ -70,7 +70,8 @@ using WbG256w = WbGeo<256, 256, 8, 4>;
 constexpr int kWbW0LdsUnits = 768;                        // layer 0 with H above: W_ih0 read from global memory
 constexpr int kWbLds256 = WbG256::kOffW0 + 4 * kWbW0LdsUnits * kIn * 4;
 constexpr int kWbLds512 = WbG512::kOffW0;                 // (layers >= 1 only: no W_ih0 block)
-constexpr int kWbLds256w = WbG256w::kOffW0;               // (layers >= 1 only)
+constexpr int kWbLds256w = WbG256w::kOffW0;               // layers >= 1; layer 0 adds its W_ih0 block
+constexpr int kWbW0LdsUnits256w = (163840 - kWbLds256w) / (4 * kIn * 4);   // layer 0 on WbG256w up to this H
 static_assert(kWbLds256 <= 163840 && kWbLds512 <= 163840 && kWbLds256w <= 163840, "LDS");
 // LDS bytes of one launch: the W_ih0 block only for layer 0 with H <= kWbW0LdsUnits
 template <class G>
@@ -170,7 +171,6 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
 
     // ---- producer thread: its dgate rows (kRPT of them) and unit share; each row's scale from the producers' bounds
     constexpr int kRPT = G::kRPT;
-    static_assert(!L0 || kRPT == 1, "layer 0 runs the one-row producer");
     const int er0 = (tid / kPPR) & (kWbN / kRPT - 1), ep = tid % kPPR;   // (consumers: unused)
     int er[kRPT], eb[kRPT];
     bool elive[kRPT];
@@ -254,10 +254,11 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
     float mdc[kRPT];                       // max |dc_{t-1}| of this thread's units, per row
 #pragma unroll
     for (int h = 0; h < kRPT; ++h) mdc[h] = 0.0f;
-    float pc[kIn] = {};                    // layer 0: this thread's share of the window-row gradient
-    auto dgates = [&](int h, int s, const In &x, int buf) {
+    float pc[kRPT][kIn] = {};              // layer 0: this thread's share of each row's window-row gradient
+    // a row's dgates of step s: formed (and dc_{t-1}, the optional fp32 dgate rows, the dc bound), layer 0's
+    // window-row gradient accumulated, split into the B tile
+    auto form = [&](int h, int s, const In &x, float (&dg)[4 * kWbUnits]) {
         const bool wr_dc = cb == 0 && elive[h];   // every column block forms the same dc_{t-1}: the first stores it
-        float dg[4 * kWbUnits];
         fU dco;
         const int u = 8 * s + kWbUnits * ep;
 #pragma unroll
@@ -286,34 +287,61 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
         }
 #pragma unroll
         for (int k = 0; k < kWbUnits; ++k) mdc[h] = fmaxf(mdc[h], fabsf(dco[k]));
-        if constexpr (L0) {   // sum_r dG[b][r] W_ih0[r][c] over this thread's 4 U gate rows, fp32
-            const f32x4 *w4 = reinterpret_cast<const f32x4 *>(w0l + u * 4 * kIn);   // 20 U floats: units u .. u + U - 1
+    };
+    // layer 0: sum_r dG[b][r] W_ih0[r][c] over this thread's 4 U gate rows, fp32, for its kRPT rows at once: each
+    // unit's 20 W_ih0 values are read once for all rows, and unit by unit behind a scheduling fence (unrolled whole,
+    // the compiler would hold all 20 U of them in registers)
+    auto w0acc = [&](int s, const float (&dg)[kRPT][4 * kWbUnits]) {
+        const int u = 8 * s + kWbUnits * ep;
 #pragma unroll
-            for (int q = 0; q < kWbUnits * 4 * kIn / 4; ++q) {
+        for (int k = 0; k < kWbUnits; ++k) {
+            if constexpr (kRPT > 1) __builtin_amdgcn_sched_barrier(0);
+            const f32x4 *w4 = reinterpret_cast<const f32x4 *>(w0l + (u + k) * 4 * kIn);   // [gate][column] of unit u + k
+#pragma unroll
+            for (int q = 0; q < 4 * kIn / 4; ++q) {
                 const f32x4 wq = w4[q];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const int idx = 4 * q + e;   // (unit k, gate g, column c): idx / 20, idx / 5 % 4, idx % 5
-                    pc[idx % kIn] = fmaf(dg[idx / kIn], wq[e], pc[idx % kIn]);
+                    const int idx = 4 * q + e;   // (gate g, column c) = (idx / 5, idx % 5)
+#pragma unroll
+                    for (int h = 0; h < kRPT; ++h)
+                        pc[h][idx % kIn] = fmaf(dg[h][4 * k + idx / kIn], wq[e], pc[h][idx % kIn]);
                 }
             }
         }
-        if (prod) {
-            // the split (fcr_f16.h mix_pair): hi = f16(up dg), lo = f16(up dg - hi); this thread's U units of the row's 8
-            // are 16-B chunks U / 2 * ep .. of the row
-            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            constexpr int NW = 2 * kWbUnits;   // 32-bit words of halves
-            unsigned hw[NW], lw[NW];
+    };
+    auto tile = [&](int h, const float (&dg)[4 * kWbUnits], int buf) {
+        if (!prod) return;
+        // the split (fcr_f16.h mix_pair): hi = f16(up dg), lo = f16(up dg - hi); this thread's U units of the row's 8
+        // are 16-B chunks U / 2 * ep .. of the row
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        constexpr int NW = 2 * kWbUnits;   // 32-bit words of halves
+        unsigned hw[NW], lw[NW];
 #pragma unroll
-            for (int p = 0; p < NW; ++p) mix_pair(dg[2 * p], up[h], dg[2 * p + 1], up[h], hw[p], lw[p]);
-            char *bt = lds + kWbOffB + buf * 2 * kWbTileB;
+        for (int p = 0; p < NW; ++p) mix_pair(dg[2 * p], up[h], dg[2 * p + 1], up[h], hw[p], lw[p]);
+        char *bt = lds + kWbOffB + buf * 2 * kWbTileB;
 #pragma unroll
-            for (int c = 0; c < kWbUnits / 2; ++c) {
-                const uint32_t o = wb_off(er[h], kWbUnits / 2 * ep + c);
-                *reinterpret_cast<u32x4 *>(bt + o) = u32x4{hw[4 * c], hw[4 * c + 1], hw[4 * c + 2], hw[4 * c + 3]};
-                *reinterpret_cast<u32x4 *>(bt + kWbTileB + o) = u32x4{lw[4 * c], lw[4 * c + 1], lw[4 * c + 2], lw[4 * c + 3]};
-            }
+        for (int c = 0; c < kWbUnits / 2; ++c) {
+            const uint32_t o = wb_off(er[h], kWbUnits / 2 * ep + c);
+            *reinterpret_cast<u32x4 *>(bt + o) = u32x4{hw[4 * c], hw[4 * c + 1], hw[4 * c + 2], hw[4 * c + 3]};
+            *reinterpret_cast<u32x4 *>(bt + kWbTileB + o) = u32x4{lw[4 * c], lw[4 * c + 1], lw[4 * c + 2], lw[4 * c + 3]};
         }
+    };
+    // one row (the one-row producers)
+    auto dgates = [&](int h, int s, const In &x, int buf) {
+        float dg[kRPT][4 * kWbUnits];
+        form(h, s, x, dg[0]);
+        if constexpr (L0 && kRPT == 1) w0acc(s, dg);
+        tile(h, dg[0], buf);
+    };
+    // every row of the thread (the two-row producers; layer 0 reads each W_ih0 value once for both)
+    auto dgates_all = [&](int s, In (&x)[kRPT], int buf) {
+        float dg[kRPT][4 * kWbUnits];
+#pragma unroll
+        for (int h = 0; h < kRPT; ++h) form(h, s, x[h], dg[h]);
+        if constexpr (L0) w0acc(s, dg);
+#pragma unroll
+        for (int h = 0; h < kRPT; ++h) tile(h, dg[h], buf);
     };
 
     // The two roles run separate loops with the same barriers (one per K step, plus the prologue's and the
@@ -335,27 +363,26 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
         // a producer's barrier waits only for its LDS tile writes: its input loads stay in flight across it, and the
         // compiler's own wait before their first use (exact counts: no DMA intrinsic in the kernel) is all
         auto pbarrier = [] { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-        if constexpr (!L0 && kRPT == 2) {
+        if constexpr (kRPT == 2) {
             // two rows per thread (WbG256w): one register set per row, refilled for step ks + 2 right after step
             // ks + 1's dgates consumed it (a second set per row would not fit the 12-wave register budget); A is
             // staged by the consumers
             In x[kRPT];
 #pragma unroll
             for (int h = 0; h < kRPT; ++h) x[h] = load_in(h, 0);
-            barrier();   // the row scales in LDS
+            barrier();   // W_ih0 and the row scales in LDS
+            dgates_all(0, x, 0);
 #pragma unroll
-            for (int h = 0; h < kRPT; ++h) {
-                dgates(h, 0, x[h], 0);
+            for (int h = 0; h < kRPT; ++h)
                 if (nk > 1) x[h] = load_in(h, 1);
-            }
             for (int ks = 0; ks < nk; ++ks) {
                 pbarrier();   // tile ks published
-                if (ks + 1 < nk)
+                if (ks + 1 < nk) {
+                    dgates_all(ks + 1, x, (ks & 1) ^ 1);
 #pragma unroll
-                    for (int h = 0; h < kRPT; ++h) {
-                        dgates(h, ks + 1, x[h], (ks & 1) ^ 1);
+                    for (int h = 0; h < kRPT; ++h)
                         if (ks + 2 < nk) x[h] = load_in(h, ks + 2);
-                    }
+                }
             }
         } else if constexpr (!L0) {
             // Layers >= 1: the producers also stage A (the consumers then only read and multiply): step ks's pieces
@@ -429,10 +456,13 @@ __global__ __launch_bounds__(G::kThreads, 1) void wide_bwd_fused_kernel(WbArgs a
         }
         if constexpr (L0) {
 #pragma unroll
-            for (int c = 0; c < kIn; ++c) pc[c] = row_sum(pc[c]);
-            if (a.rowg && elive[0] && cb == 0 && ep == 0)
+            for (int h = 0; h < kRPT; ++h) {
 #pragma unroll
-                for (int c = 0; c < kIn; ++c) a.rowg[(size_t)eb[0] * kIn + c] += pc[c];
+                for (int c = 0; c < kIn; ++c) pc[h][c] = row_sum(pc[h][c]);
+                if (a.rowg && elive[h] && cb == 0 && ep == 0)
+#pragma unroll
+                    for (int c = 0; c < kIn; ++c) a.rowg[(size_t)eb[h] * kIn + c] += pc[h][c];
+            }
         }
         if (!prod) return;
         barrier();   // (the consumers' epilogue reuses the A stages)
