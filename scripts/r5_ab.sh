@@ -1,5 +1,7 @@
 # Same-process A/B of a candidate build against lib_ab/prod.so: its wide GPU tests first (FCR_LIB), then config 5
 # keep-all and default budget. usage: scripts/r5_ab.sh NAME [rounds]
+# (lib_ab/prod.so: a copy of the current forging-control_amd/lib/libfcr.so; lib_ab/NAME.so: the candidate, e.g. from
+# scripts/build_patch_variant.py or hipcc with a -D option)
 set -e -o pipefail
 N=$1; RND=${2:-3}
 mkdir -p gpurun_out/$N
