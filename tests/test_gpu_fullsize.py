@@ -180,3 +180,14 @@ def test_config5_full_batch(seed):
         params = {"Wih": [np.asarray(a, np.float64) for a in p["Wih"]], "Whh": [np.asarray(a, np.float64) for a in p["Whh"]],
                   **{k: np.asarray(p[k], np.float64) for k in ("fcW", "fcb", "W_inp", "b_inp", "W_out")}}
     _check(*hip_and_oracle(params, 65536, 25, seed, chunk=4096), 65536, 1e-5, 1e-5, 1e-5, 1e-5)
+
+
+@pytest.mark.parametrize("B", [32768, 32767])
+def test_wide_backward_geometries_at_their_batch_threshold(B):
+    """The wide backward's layers >= 1 run 256 x 256-trajectory workgroups from B = 32 768 on and 256 x 128 below
+    (fcr_abi.hip launch_fb): both sides of the threshold at H = 264 (Hp = 320: three 256-column blocks, three row-bound
+    slots) and N = 2, every trajectory against the fp64 oracle."""
+    p = synth_params(264, 7)
+    params = {"Wih": [np.asarray(a, np.float64) for a in p["Wih"]], "Whh": [np.asarray(a, np.float64) for a in p["Whh"]],
+              **{k: np.asarray(p[k], np.float64) for k in ("fcW", "fcb", "W_inp", "b_inp", "W_out")}}
+    _check(*hip_and_oracle(params, B, 2, ("own", 26), chunk=8192), B, 1e-5, 1e-5, 1e-5, 1e-5)
