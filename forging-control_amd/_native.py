@@ -7,16 +7,20 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 import threading
 
 _LIB_NAME = "libfcr.so"
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# FCR_LIB: another build of the same ABI (A/B timing, scripts/inject_stale_lo.sh's fault-injected build); the
-# in-tree library otherwise
-LIB_PATH = os.environ.get("FCR_LIB") or os.path.join(_HERE, "lib", _LIB_NAME)
+_IN_TREE = os.path.join(_HERE, "lib", _LIB_NAME)
+# FCR_LIB: another build of the same ABI (A/B timing, scripts/inject_stale_lo.sh's fault-injected build). A development
+# switch only: it takes effect together with FCR_DEV=1 (load() refuses FCR_LIB without it and says on stderr which
+# library it loaded when it is honoured); the in-tree library otherwise.
+LIB_PATH = os.environ.get("FCR_LIB") or _IN_TREE
 
 FCR_OK = 0
-ABI_VERSION = 5
+# 6 (round 6): kept wide windows store gate activations (not pre-activations), fcr_wide_bwd_cell[_workspace] exported
+ABI_VERSION = 6
 PRECISION_FP32, PRECISION_F16 = 0, 1
 ERRORS = {-1: "FCR_EINVAL", -2: "FCR_EWORKSPACE", -3: "FCR_EHIP", -4: "FCR_EUNSUPPORTED"}
 
@@ -98,6 +102,11 @@ def load() -> ctypes.CDLL:
     with _lock:
         if _lib is not None:
             return _lib
+        if LIB_PATH != _IN_TREE:
+            if os.environ.get("FCR_DEV") != "1":
+                raise NativeError(f"FCR_LIB={LIB_PATH} names a development build; set FCR_DEV=1 to load it "
+                                  "(unset FCR_LIB for the in-tree library)")
+            sys.stderr.write(f"forging_control_amd: FCR_LIB development build {LIB_PATH}\n")
         if not os.path.exists(LIB_PATH):
             raise NativeError(
                 f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "

@@ -252,22 +252,16 @@ int launch_sbwd_t(const BwdArgs &ba, const Layout &L, hipStream_t s) {
 // and every product they enter gains exact zeros (the H <= 52 tiers pad the same way, slot_tier). The split weights,
 // the readout's fc.W and the window-row gradient's W_ih0 are packed padded per call; the caller's tensors keep H.
 int wide_hp(int H) { return (H + kWgU - 1) / kWgU * kWgU; }
-// The fused backward cell's geometry per layer (fcr_wbwd.h): 256 columns x 128 trajectories. Built with FCR_WB512=1,
-// layers >= 1 run 512 columns x 64 trajectories where that covers the [input gradient | dh_{t-1}] columns (2 Hp) in no
-// more padded columns than 256-column blocks do: each cell's dgates formed once instead of per column block, at twice
-// the A (weight) reads per trajectory; measured 3 % slower at config 5 (DESIGN.md §4 "Round 5"), so not the default.
-#ifndef FCR_WB512
-#define FCR_WB512 0
-#endif
-bool wb_wide(bool l0, int Hp) {
-    return FCR_WB512 && !l0 &&
-           (2 * Hp + WbG512::kM - 1) / WbG512::kM * WbG512::kM <= (2 * Hp + WbG256::kM - 1) / WbG256::kM * WbG256::kM;
-}
-int wb_cols(bool l0, int Hp) { return wb_wide(l0, Hp) ? WbG512::kM : WbG256::kM; }
+// The fused backward cell's column blocks (fcr_wbwd.h): 256 output columns per workgroup in every geometry (WbG256,
+// WbG256w). (Round 5 measured 512 columns x 64 trajectories for layers >= 1 — each cell's dgates formed once instead
+// of per column block, at twice the A reads per trajectory — 3 % slower at config 5; commit e9dc1d2 builds it with
+// -DFCR_WB512=1.)
+constexpr int kWbCols = WbG256::kM;
+static_assert(WbG256w::kM == kWbCols, "every backward geometry has the same column blocks");
 // row-bound slots: one per column block of the writing launch (every block writes its slot, 0 where it has no such
 // columns). dh of layer l: its own cells' [0, 2 Hp) (layer 0: [0, Hp)); the input gradient: layer l + 1's [0, Hp)
-int wb_hslots(int l, int Hp) { return ((l ? 2 * Hp : Hp) + wb_cols(l == 0, Hp) - 1) / wb_cols(l == 0, Hp); }
-int wb_dslots(int Hp) { return (Hp + wb_cols(false, Hp) - 1) / wb_cols(false, Hp); }
+int wb_hslots(int l, int Hp) { return ((l ? 2 * Hp : Hp) + kWbCols - 1) / kWbCols; }
+int wb_dslots(int Hp) { return (Hp + kWbCols - 1) / kWbCols; }
 // the slots allocated: the most any geometry writes
 int wide_nslots(int Hp) { return (2 * Hp + WbG256::kM - 1) / WbG256::kM; }
 
@@ -484,64 +478,34 @@ int launch_wgemm_cell(const WgArgs &wa, hipStream_t s) {
 }
 
 // One backward cell of the fused path (fcr_wbwd.h): dgates formed in the product's prologue, out = dG [W_ih | W_hh]
-// (columns [0, NO), NO = 0: the dgate part only) in true units
-#ifndef FCR_WB_L0_N256
-#define FCR_WB_L0_N256 0   // 1: layer 0 on WbG256w too (H <= kWbW0LdsUnits256w): its W_ih0 accumulation spills
-                           // ~320 registers at the 12-wave budget, backward +57 % (round5_c5_l0w_ab_keepall.log)
-#endif
-#ifndef FCR_WB_N256
-#define FCR_WB_N256 1   // layers >= 1 on 256 columns x 256 trajectories (WbG256w, fcr_wbwd.h): A staged once per 256
-                        // trajectories, backward −5.4 % at config 5 (round5_c5_n256_ab_*.log); 0: 256 x 128 (WbG256)
-#endif
+// (columns [0, NO), NO = 0: the dgate part only) in true units. Geometries: layers >= 1 on 256 columns x 256
+// trajectories (WbG256w: A staged once per 256 trajectories, backward −5.4 % at config 5, round5_c5_n256_ab_*.log)
+// where its halved workgroup count still fills the chip (B >= 32 768: >= 256 workgroups at two column blocks; the
+// surrogate's B = 256 step: 3.2 ms on WbG256 against 4.1) and the cell does not also write its dgates (the surrogate's
+// B = 65 536 step 2 % slower on it); everything else, layer 0 included, on 256 x 128 (WbG256). (Layer 0 on WbG256w
+// spills ~320 registers in its W_ih0 accumulation at the 12-wave budget: backward +57 %, round5_c5_l0w_ab_keepall.log;
+// commit e9dc1d2 builds it with -DFCR_WB_L0_N256=1.)
 int launch_fb(const WbArgs &wa, bool l0, hipStream_t s) {
-    static std::atomic<unsigned long long> attr_done[6] = {{0}, {0}, {0}, {0}, {0}, {0}};
-    const bool w0g = l0 && wa.H > kWbW0LdsUnits, wide = wb_wide(l0, wa.H);
-    // WbG256w halves the workgroups per cell: only where they still fill the chip (B >= 32 768: >= 256 of them at
-    // two column blocks); smaller batches keep WbG256's parallelism (the surrogate's B = 256 step: 3.2 vs 4.1 ms).
-    // Cells that also write their dgates (the surrogate's weight gradients) measured 2 % slower on it: WbG256
-    const bool n256 = FCR_WB_N256 && wa.NB >= 32768 && !wa.dg;
-    // layer 0 on it too while its W_ih0 block fits beside it in LDS (H <= kWbW0LdsUnits256w)
-    const bool l0w = FCR_WB_L0_N256 && n256 && wa.H <= kWbW0LdsUnits256w;
-    const int kind = l0 ? (l0w ? 5 : w0g ? 2 : 1) : (wide ? 3 : (n256 ? 4 : 0));
-    const void *fn = kind == 0   ? (const void *)wide_bwd_fused_kernel<WbG256, false>
-                     : kind == 1 ? (const void *)wide_bwd_fused_kernel<WbG256, true, false>
-#if FCR_WB512
-                     : kind == 3 ? (const void *)wide_bwd_fused_kernel<WbG512, false>
-#endif
-#if FCR_WB_N256
-                     : kind == 4 ? (const void *)wide_bwd_fused_kernel<WbG256w, false>
-#if FCR_WB_L0_N256
-                     : kind == 5 ? (const void *)wide_bwd_fused_kernel<WbG256w, true, false>
-#endif
-#endif
-                                 : (const void *)wide_bwd_fused_kernel<WbG256, true, true>;
-    const int lds_max = wide ? kWbLds512 : kind == 4 ? kWbLds256w
-                                         : kind == 5 ? wb_lds_bytes<WbG256w>(true, kWbW0LdsUnits256w) : kWbLds256;
-    if (const int rc = lds_attr(fn, lds_max, attr_done[kind], "wbwd"))
-        return rc;
+    static std::atomic<unsigned long long> attr_done[4] = {{0}, {0}, {0}, {0}};
+    const bool w0g = l0 && wa.H > kWbW0LdsUnits;   // layer 0 with W_ih0 read from global memory
+    const bool n256 = !l0 && wa.NB >= 32768 && !wa.dg;
+    enum { kL1 = 0, kL0 = 1, kL0Global = 2, kL1N256 = 3 };
+    const int kind = l0 ? (w0g ? kL0Global : kL0) : (n256 ? kL1N256 : kL1);
+    const void *fn = kind == kL1       ? (const void *)wide_bwd_fused_kernel<WbG256, false>
+                     : kind == kL0     ? (const void *)wide_bwd_fused_kernel<WbG256, true, false>
+                     : kind == kL1N256 ? (const void *)wide_bwd_fused_kernel<WbG256w, false>
+                                       : (const void *)wide_bwd_fused_kernel<WbG256, true, true>;
+    if (const int rc = lds_attr(fn, kind == kL1N256 ? kWbLds256w : kWbLds256, attr_done[kind], "wbwd")) return rc;
     if (wa.NO < 0 || wa.NO > 2 * wa.H || wa.NO % 8 || wa.H % 8 || wa.NB <= 0 || (wa.rm_h && wa.nrh < 1) ||
         (wa.rm_d && wa.nrd < 1) || (l0 && (!wa.wih0 || !wa.rowg)))
         return fail(FCR_EINVAL, "wide_bwd_fused_kernel: NO %d H %d B %d off its tiling", wa.NO, wa.H, wa.NB);
-    const int M = wide ? WbG512::kM : WbG256::kM, N = wide ? WbG512::kN : kind >= 4 ? WbG256w::kN : WbG256::kN;
-    const dim3 grid((unsigned)((wa.NB + N - 1) / N * (wa.NO > 0 ? (wa.NO + M - 1) / M : 1)));
-#if FCR_WB512
-    if (kind == 3)
-        hipLaunchKernelGGL((wide_bwd_fused_kernel<WbG512, false>), grid, dim3(WbG512::kThreads), wb_lds_bytes<WbG512>(false, wa.H), s, wa);
-    else
-#endif
-#if FCR_WB_N256
-    if (kind == 4)
+    const int N = kind == kL1N256 ? WbG256w::kN : WbG256::kN;
+    const dim3 grid((unsigned)((wa.NB + N - 1) / N * (wa.NO > 0 ? (wa.NO + kWbCols - 1) / kWbCols : 1)));
+    if (kind == kL1N256)
         hipLaunchKernelGGL((wide_bwd_fused_kernel<WbG256w, false>), grid, dim3(WbG256w::kThreads), wb_lds_bytes<WbG256w>(false, wa.H), s, wa);
-    else
-#if FCR_WB_L0_N256
-    if (kind == 5)
-        hipLaunchKernelGGL((wide_bwd_fused_kernel<WbG256w, true, false>), grid, dim3(WbG256w::kThreads), wb_lds_bytes<WbG256w>(true, wa.H), s, wa);
-    else
-#endif
-#endif
-    if (kind == 0)
+    else if (kind == kL1)
         hipLaunchKernelGGL((wide_bwd_fused_kernel<WbG256, false>), grid, dim3(WbG256::kThreads), wb_lds_bytes<WbG256>(false, wa.H), s, wa);
-    else if (kind == 1)
+    else if (kind == kL0)
         hipLaunchKernelGGL((wide_bwd_fused_kernel<WbG256, true, false>), grid, dim3(WbG256::kThreads), wb_lds_bytes<WbG256>(true, wa.H), s, wa);
     else
         hipLaunchKernelGGL((wide_bwd_fused_kernel<WbG256, true, true>), grid, dim3(WbG256::kThreads), wb_lds_bytes<WbG256>(true, wa.H), s, wa);
@@ -886,7 +850,7 @@ int check_lstm_dims(const fcr_dims *d) {
 struct SurWideLayout {
     int Hp, ns;
     size_t fcw, wsc, rng, xt, WR, HR, Cs, Act, Hs, fw[3], bt[3], w0p, dH, dC, DC2, D[2], E0, RMc, RMh, RMd, rowg, dG,
-        fcpart, part, total;
+        fcpart, part, part_floats, total;
 };
 constexpr int kSurFcSlices = 64;   // batch slices of the readout's weight gradient (fixed: deterministic)
 
@@ -924,7 +888,8 @@ SurWideLayout make_surw(const fcr_dims *d, int with_backward) {
     L.WR = take(F16 * kL * B * 2 * kWgRecX0);
     L.HR = take(F16 * kLayers * kL * B * 2 * Hp);
     L.Cs = take(F * kLayers * kL * B * Hp);
-    L.Act = take(F * kLayers * kL * B * 4 * Hp);
+    // the gate activations only for the backward (the forward-only call's cells run with keep_act off)
+    L.Act = with_backward ? take(F * kLayers * kL * B * 4 * Hp) : 0;
     L.Hs = take(F * B * Hp);
     for (int l = 0; l < kLayers; ++l) {
         L.fw[l] = take(F16 * 2 * 4 * Hp * ((l == 0 ? kWgRecX0 : Hp) + Hp));
@@ -944,13 +909,18 @@ SurWideLayout make_surw(const fcr_dims *d, int with_backward) {
         L.rowg = take(F * kL * B * kIn);
         L.dG = take(F * kL * B * 4 * Hp);   // one layer's dgates, every step
         L.fcpart = take(F * kSurFcSlices * kOut * Hp);
-        size_t pf = 0;   // the largest set of weight-gradient partials
-        for (int K : {kIn, d->H}) {
-            const WgSplit w = wg_split((long long)kL * B, 4 * (int)Hp, K);
-            const size_t a = (size_t)w.S * 4 * Hp * K;
-            pf = a > pf ? a : pf;
-        }
+        // the largest set of weight-gradient partials over every reduction surw_backward runs: n = 10 B rows (W_ih)
+        // and 9 B rows (W_hh), K = kIn (layer 0's W_ih) and H. wg_split rounds each slice up to whole kWgrN steps,
+        // so the 9 B reduction can take MORE slices than the 10 B one (H = 256, B = 110: 31 against 18)
+        size_t pf = 0;
+        for (long long n : {(long long)kL * B, (long long)(kL - 1) * B})
+            for (int K : {kIn, d->H}) {
+                const WgSplit w = wg_split(n, 4 * (int)Hp, K);
+                const size_t a = (size_t)w.S * 4 * Hp * K;
+                pf = a > pf ? a : pf;
+            }
         L.part = take(F * pf);
+        L.part_floats = pf;
     }
     L.total = off;
     return L;
@@ -984,7 +954,7 @@ int surw_forward(const fcr_dims *d, const fcr_weights *w, const float *x, float 
     a.N = 1;
     a.H = Hp;
     a.Cs = (float *)(base + L.Cs);
-    a.Act = (float *)(base + L.Act);
+    a.Act = with_backward ? (float *)(base + L.Act) : nullptr;
     a.Hs = (float *)(base + L.Hs);
     a.wr = (_Float16 *)(base + L.WR);
     if ((rc = wide_cells(a, fw, (_Float16 *)(base + L.HR), Hp, kLayers, with_backward != 0, s))) return rc;
@@ -995,8 +965,10 @@ int surw_forward(const fcr_dims *d, const fcr_weights *w, const float *x, float 
 
 // one weight gradient: dW [4H][K] = sum_n A[n][.] X[n][.] (fcr_wgrad.h), X fp32 rows or split records
 int surw_wgrad(const float *A, long long n, int Hp, int H, int K, const float *X, int ldx, const _Float16 *XR,
-               float *part, float *dW, hipStream_t s) {
+               float *part, size_t part_floats, float *dW, hipStream_t s) {
     const WgSplit sp = wg_split(n, 4 * Hp, K);
+    if ((size_t)sp.S * 4 * Hp * K > part_floats)   // make_surw sizes L.part for every (n, K) this runs with
+        return fail(FCR_EWORKSPACE, "surrogate weight-gradient partials exceed their workspace slab");
     WgradArgs g{};
     g.A = A;
     g.lda = 4 * Hp;
@@ -1112,10 +1084,11 @@ int surw_backward(const fcr_dims *d, const fcr_weights *w, const float *dy, floa
         // layer below's h records; h_{t-1} = this layer's records of steps 0..8 against the dgates of steps 1..9
         const long long n10 = (long long)kL * B, n9 = (long long)(kL - 1) * B;
         if ((rc = surw_wgrad(dG, n10, Hp, H, l == 0 ? kIn : H, l == 0 ? (const float *)(base + L.xt) : nullptr, kIn,
-                             l == 0 ? nullptr : HR + (size_t)(l - 1) * kL * B * 2 * Hp, part, g_w_ih[l], s)))
+                             l == 0 ? nullptr : HR + (size_t)(l - 1) * kL * B * 2 * Hp, part, L.part_floats, g_w_ih[l],
+                             s)))
             return rc;
         if ((rc = surw_wgrad(dG + (size_t)B * 4 * Hp, n9, Hp, H, H, nullptr, 0, HR + (size_t)l * kL * B * 2 * Hp, part,
-                             g_w_hh[l], s)))
+                             L.part_floats, g_w_hh[l], s)))
             return rc;
     }
     if (g_x) {   // the window-row gradients [t][B][5] -> (B, 10, 5)

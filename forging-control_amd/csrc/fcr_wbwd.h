@@ -60,19 +60,14 @@ struct WbGeo {
 };
 // 256 columns x 128 trajectories, 4 + 4 waves (round 4): every layer; two column blocks at Hp = 256 form the same dgates
 using WbG256 = WbGeo<256, 128, 4, 4>;
-// 512 columns x 64 trajectories, 4 + 8 waves: a layer >= 1 cell's whole [input gradient | dh_{t-1}] at Hp = 256 in one
-// workgroup, so its dgates are formed (and its rows read) once
-using WbG512 = WbGeo<512, 64, 8, 2>;
-// 256 columns x 256 trajectories, 4 + 8 waves (layers >= 1 by default, FCR_WB_N256): A staged once per 256
+// 256 columns x 256 trajectories, 4 + 8 waves (layers >= 1 at B >= 32 768, fcr_abi.hip launch_fb): A staged once per 256
 // trajectories (half the A bytes per trajectory of WbG256); each producer thread forms the dgates of two rows, each
 // consumer 32 columns x 256 trajectories; 168 registers per wave (12 waves), 129 KB of LDS
 using WbG256w = WbGeo<256, 256, 8, 4>;
 constexpr int kWbW0LdsUnits = 768;                        // layer 0 with H above: W_ih0 read from global memory
 constexpr int kWbLds256 = WbG256::kOffW0 + 4 * kWbW0LdsUnits * kIn * 4;
-constexpr int kWbLds512 = WbG512::kOffW0;                 // (layers >= 1 only: no W_ih0 block)
-constexpr int kWbLds256w = WbG256w::kOffW0;               // layers >= 1; layer 0 adds its W_ih0 block
-constexpr int kWbW0LdsUnits256w = (163840 - kWbLds256w) / (4 * kIn * 4);   // layer 0 on WbG256w up to this H
-static_assert(kWbLds256 <= 163840 && kWbLds512 <= 163840 && kWbLds256w <= 163840, "LDS");
+constexpr int kWbLds256w = WbG256w::kOffW0;               // layers >= 1 only (no W_ih0 block)
+static_assert(kWbLds256 <= 163840 && kWbLds256w <= 163840, "LDS");
 // LDS bytes of one launch: the W_ih0 block only for layer 0 with H <= kWbW0LdsUnits
 template <class G>
 __host__ __device__ constexpr int wb_lds_bytes(bool l0, int H) {
@@ -105,8 +100,8 @@ struct WbArgs {
     float *rowg;                 // layer 0: [B][kIn] window-row gradient row (+=), else null
 };
 
-// Diagnostic build FCR_WB_STAMP=1 (scripts/stamp_wb.py; with -DFCR_WB_N256=0: the stamps sit in the one-row producer
-// of WbG256, which layers >= 1 run in that build): per-wave s_memtime sums of the layer >= 1 kernel's K-step sections, added into fcr_wb_stamp by lane 0 (vector atomics) — consumers: barrier wait, A DMA issue, fragment reads +
+// Diagnostic build FCR_WB_STAMP=1 (scripts/stamp_wb.py; the stamps sit in the one-row producer of WbG256, i.e. runs at
+// B < 32 768 or scripts/variants/wb_n128.json): per-wave s_memtime sums of the layer >= 1 kernel's K-step sections, added into fcr_wb_stamp by lane 0 (vector atomics) — consumers: barrier wait, A DMA issue, fragment reads +
 // MFMA issue; producers: barrier wait, input load issue, dgates (including the wait for their inputs) + tile writes.
 // Read the shares, never the build's run time (each stamp drains lgkmcnt).
 #ifndef FCR_WB_STAMP

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define FCR_ABI_VERSION 5
+#define FCR_ABI_VERSION 6   /* 6: kept wide windows hold gate activations; fcr_wide_bwd_cell */
 
 enum {
     FCR_OK = 0,

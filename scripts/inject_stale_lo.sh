@@ -28,7 +28,7 @@ fi
 mkdir -p $OUT
 cd $R
 set +e
-FCR_LIB=$R/lib_ab/inject_stale_lo.so timeout -k 10 300 python -u -m pytest tests/test_wide_cell.py -m gpu -v \
+FCR_DEV=1 FCR_LIB=$R/lib_ab/inject_stale_lo.so timeout -k 10 300 python -u -m pytest tests/test_wide_cell.py -m gpu -v \
   --timeout 120 --timeout-method thread -k layer_cell > $OUT/inject_stale_lo.log 2>&1
 rc=$?
 set -e
