@@ -38,13 +38,10 @@ namespace fcr {
 
 constexpr int kWgU = 64;                  // units per workgroup (the host pads H to a multiple)
 constexpr int kWgM = 4 * kWgU;            // W rows per workgroup
-#ifndef FCR_WG_N
-#define FCR_WG_N 256
-#endif
 // trajectories per workgroup: 256 = 8 waves at one workgroup per CU (W staged once per 256 trajectories: config 5's
 // forward −4.8 % every window kept, −1.9 % step at the default budget against 128 = 4 waves at two workgroups per CU,
-// round5_c5_wg256_ab2_*.log)
-constexpr int kWgN = FCR_WG_N;
+// round5_c5_wg256_ab2_*.log; the code is generic over 128 | 256)
+constexpr int kWgN = 256;
 constexpr int kWgK = 32;                  // k per block (one 16x16x32 f16 MFMA k-block)
 constexpr int kWgC = kWgK / 8;            // 16-B chunks per LDS row
 constexpr int kWgWaves = kWgN / 32;       // 2 x kWgWC waves; each 128 rows x 64 trajectories
@@ -53,7 +50,7 @@ constexpr int kWgNT = kWgN / kWgWC / 16;  // D tiles per wave along the trajecto
 constexpr int kWgThreads = 64 * kWgWaves;
 constexpr int kWgStageA = kWgM * kWgK * 2;   // bytes: one split half of the W block
 constexpr int kWgStageB = kWgN * kWgK * 2;   // one split half of the operand block
-constexpr int kWgEpi = kWgN * ((kWgU + 4) * 4 + 2 * (kWgU + 8) * 2);   // the epilogue's c / hi / lo tiles
+constexpr int kWgEpi = kWgN * (kWgU * 4 + 2 * kWgU * 2);   // the epilogue's c / hi / lo tiles (unpadded, swizzled rows)
 constexpr int kWgStages = 3;              // ring slots: two steps of prefetch; the stage wait is vmcnt(one step's pieces)
 constexpr int kWgLds = kWgStages * (kWgStageA + kWgStageB) > kWgEpi ? kWgStages * (kWgStageA + kWgStageB) : kWgEpi;
 constexpr int kWgRecX0 = kWideRecX0;     // layer 0's window record: [hi (32) | lo (32)] halves, 5 columns used
@@ -202,23 +199,36 @@ __global__ __launch_bounds__(kWgThreads, kWgN == 128 ? 2 : 1) void wide_cell_fwd
     __syncthreads();
     // ---- epilogue: the cell update on the accumulators, through LDS ----
     // A lane holds (trajectory, unit) pairs scattered over 16 rows; the records want whole rows. So the c_prev tile
-    // comes in by rows, each lane updates its pairs in LDS tiles [trajectory][unit] (rows padded by 16 B: 2-way
-    // bank conflicts at most, chunks stay 16-B aligned), and c and the h record go out by rows again; the activations
-    // go straight from the registers ([unit][gate] rows, WgArgs.act).
-    constexpr int CSTR = kWgU + 4;            // floats per c row
-    constexpr int HSTR = kWgU + 8;            // halves per hi / lo row
-    float *cs = reinterpret_cast<float *>(lds);                                   // [128][CSTR]
-    _Float16 *hs = reinterpret_cast<_Float16 *>(lds + kWgN * CSTR * 4);           // [128][HSTR]
-    _Float16 *ls = hs + kWgN * HSTR;                                              // [128][HSTR]
+    // comes in by rows, each lane updates its pairs in LDS tiles [trajectory][unit], and c and the h record go out by
+    // rows again; the activations go straight from the registers ([unit][gate] rows, WgArgs.act).
+    // Rows are unpadded (c: 256 B, hi / lo: 128 B) and swizzled (epi_cx / epi_sw): the 16-B chunks of row r XOR r & 7,
+    // the elements inside a chunk XOR 2 where bit 3 of r is set. A per-element access (32 lanes = 16 rows x 2 units
+    // on 32 banks) and every row-wise 16-B pass then hit distinct banks (scripts/wg_epi_banks.py: 320 -> 0 conflict
+    // cycles per wave; the round-5 rows padded by 16 B measured 16 % of the kernel's LDS cycles as conflicts).
+    constexpr int CSTR = kWgU;                // floats per c row
+    constexpr int HSTR = kWgU;                // halves per hi / lo row
+    float *cs = reinterpret_cast<float *>(lds);                                   // [kWgN][CSTR]
+    _Float16 *hs = reinterpret_cast<_Float16 *>(lds + kWgN * CSTR * 4);           // [kWgN][HSTR]
+    _Float16 *ls = hs + kWgN * HSTR;                                              // [kWgN][HSTR]
+    auto epi_cx = [](int r) { return r & 7; };              // chunk swizzle of row r
+    auto epi_sw = [](int r) { return ((r >> 3) & 1) << 1; }; // element swizzle inside a chunk of row r
+    auto c_el = [&](int r, int ul) { return r * CSTR + 4 * ((ul >> 2) ^ epi_cx(r)) + ((ul & 3) ^ epi_sw(r)); };
+    auto h_el = [&](int r, int ul) {
+        return r * HSTR + 8 * ((ul >> 3) ^ epi_cx(r)) + 2 * (((ul >> 1) & 3) ^ epi_sw(r)) + (ul & 1);
+    };
     constexpr int ERS = kWgThreads / 16;      // row-wise passes: ERS rows x 16 chunks per pass
+    static_assert(ERS % 16 == 0, "a thread's rows share r & 15 (its swizzle)");
     const int er = tid >> 4, ec = tid & 15;
+    const int ecx = ec ^ epi_cx(er), erx = (ec & 7) ^ epi_cx(er);   // the thread's physical c / h chunk
+    const bool eswap = epi_sw(er) != 0;                           // its chunks' elements are stored z w x y
     if (a.c_prev) {
 #pragma unroll
         for (int p = 0; p < kWgN / ERS; ++p) {
             const int r = er + ERS * p, b = b0 + r;
-            if (b < a.B)
-                *reinterpret_cast<f32x4 *>(cs + r * CSTR + 4 * ec) =
-                    *reinterpret_cast<const f32x4 *>(a.c_prev + k8(a.B, b, u0 + 4 * ec));
+            if (b < a.B) {
+                const f32x4 v = *reinterpret_cast<const f32x4 *>(a.c_prev + k8(a.B, b, u0 + 4 * ec));
+                *reinterpret_cast<f32x4 *>(cs + r * CSTR + 4 * ecx) = eswap ? f32x4{v[2], v[3], v[0], v[1]} : v;
+            }
         }
     }
     __syncthreads();
@@ -229,7 +239,7 @@ __global__ __launch_bounds__(kWgThreads, kWgN == 128 ? 2 : 1) void wide_cell_fwd
         for (int m = 0; m < 8; ++m) {
             const int ul = 32 * wr + 4 * m + fq;
             const f32x4 g4 = acc[m][n];
-            const float cp = a.c_prev ? cs[r * CSTR + ul] : 0.0f;
+            const float cp = a.c_prev ? cs[c_el(r, ul)] : 0.0f;
             const float i = sigm(g4[0]), f = sigm(g4[1]), g = tanhf(g4[2]), o = sigm(g4[3]);
             const int b = b0 + r;
             // the activations, [unit][gate] rows: a lane's four gates are one 16-B store, a fragment's 4 units x 16
@@ -238,9 +248,9 @@ __global__ __launch_bounds__(kWgThreads, kWgN == 128 ? 2 : 1) void wide_cell_fwd
             const float c = (a.c_prev ? f * cp : 0.0f) + i * g;
             const float h = o * tanhf(c);
             const _Float16 hi = (_Float16)h;
-            cs[r * CSTR + ul] = c;
-            hs[r * HSTR + ul] = hi;
-            ls[r * HSTR + ul] = (_Float16)(h - (float)hi);
+            cs[c_el(r, ul)] = c;
+            hs[h_el(r, ul)] = hi;
+            ls[h_el(r, ul)] = (_Float16)(h - (float)hi);
             if (a.h_out && b < a.B) a.h_out[(size_t)b * H + u0 + ul] = h;   // the readout's cell only
         }
     }
@@ -249,12 +259,13 @@ __global__ __launch_bounds__(kWgThreads, kWgN == 128 ? 2 : 1) void wide_cell_fwd
     for (int p = 0; p < kWgN / ERS; ++p) {
         const int r = er + ERS * p, b = b0 + r;
         if (b >= a.B) continue;
-        *reinterpret_cast<f32x4 *>(a.c_out + k8(a.B, b, u0 + 4 * ec)) = *reinterpret_cast<const f32x4 *>(cs + r * CSTR + 4 * ec);
+        const f32x4 cv = *reinterpret_cast<const f32x4 *>(cs + r * CSTR + 4 * ecx);
+        *reinterpret_cast<f32x4 *>(a.c_out + k8(a.B, b, u0 + 4 * ec)) = eswap ? f32x4{cv[2], cv[3], cv[0], cv[1]} : cv;
         // 8 chunks of 8 halves per row and half: the hi halves of the 64 units (ec < 8), then the lo halves
         const int e = ec & 7;
-        const _Float16 *src = (ec < 8 ? hs : ls) + r * HSTR + 8 * e;
+        const u32x4 hv = *reinterpret_cast<const u32x4 *>((ec < 8 ? hs : ls) + r * HSTR + 8 * erx);
         *reinterpret_cast<u32x4 *>(a.h_rec + (size_t)b * 2 * H + (ec < 8 ? 0 : H) + u0 + 8 * e) =
-            *reinterpret_cast<const u32x4 *>(src);
+            eswap ? u32x4{hv[2], hv[3], hv[0], hv[1]} : hv;
     }
 }
 

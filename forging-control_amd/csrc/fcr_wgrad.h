@@ -5,10 +5,14 @@
 // as ONE reduction per weight over all (window step, sample) rows n: C[r][k] = sum_n A[n][r] X[n][k], A the fp32
 // dgate rows the fused backward cells write (fcr_wbwd.h WbArgs.dg, rows of 4 Hp in the padded gate order
 // gate Hp + unit), X either fp32 rows (layer 0's window values) or the forward's split h records [hi (Hp) | lo (Hp)]
-// whose sum is h (fcr_wgemm.h). Exact fp32 products on the matrix cores (v_mfma_f32_16x16x4_f32, fp32 in and out:
-// the dgates of a reduction over 10 B rows span many powers of two, which an f16 split would have to rescale per
-// row), fp32 accumulation, deterministic: the n range is split over S workgroups into fixed partial slabs summed in
-// a fixed order (wgrad_sum_pad_kernel).
+// whose sum is h (fcr_wgemm.h). The products are exact fp32 products of their operands on the matrix cores
+// (v_mfma_f32_16x16x4_f32, fp32 in and out: the dgates of a reduction over 10 B rows span many powers of two, which an
+// f16 split would have to rescale per row), fp32 accumulation, deterministic: the n range is split over S workgroups
+// into fixed partial slabs summed in a fixed order (wgrad_sum_pad_kernel). The X operand of layers >= 1 is NOT the
+// forward's fp32 h: it is rebuilt as hi + lo from the f16 record (hi = f16(h), lo = f16(h - hi)), which carries
+// |h - (hi + lo)| <= 2^-11 |h - hi| <= 2^-22 |h| (lo rounds to 11 bits; a lo in f16's subnormal range, |h - hi| <
+// 2^-14, adds at most 2^-25 absolute) — the same split error the forward's own products see, so the gradients match
+// the fp64 oracle at the tests' 1e-5 (tests/test_surrogate.py) without an fp32 copy of every h.
 // Tile: a workgroup owns 128 r x 128 k of C, 4 waves of 64 x 64 (4 x 4 tiles of 16 x 16); the n loop stages 16 rows
 // of A and X (8 KB each) through LDS per step, so each MFMA operand element is loaded once per workgroup.
 #pragma once
