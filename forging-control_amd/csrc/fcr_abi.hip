@@ -126,9 +126,8 @@ Layout make_layout(const fcr_dims *d, int with_backward) {
     Layout L{};
     L.HS = slot_tier(d->H);
     L.nw = (d->B + kTile - 1) / kTile;
-    // covers every launch geometry of the precision mode (a launch covers ceil(nw / W) * W waves)
-    const int pad = d->precision == FCR_PRECISION_F16 ? kWavePadLP : (kFwdWaves > kBwdWaves ? kFwdWaves : kBwdWaves);
-    L.nw_pad = (L.nw + pad - 1) / pad * pad;
+    constexpr int kPad = kFwdWaves > kBwdWaves ? kFwdWaves : kBwdWaves;
+    L.nw_pad = (L.nw + kPad - 1) / kPad * kPad;  // covers both launch geometries
     size_t off = 0;
     auto take = [&](size_t bytes) {
         const size_t o = off;
@@ -186,8 +185,8 @@ int launch_fwd_t(const FwdArgs &fa, const Layout &L, hipStream_t s) {
     const int lds = LP ? Geo16<HS>::LDS_FWD_LP : Geo16<HS>::LDS_FWD;
     static std::atomic<unsigned long long> attr_done{0};
     if (const int rc = lds_attr((const void *)fcr_fwd_kernel<HS, STORE, LP>, lds, attr_done, "fwd")) return rc;
-    constexpr int W = fwd_waves<LP, STORE>();
-    hipLaunchKernelGGL((fcr_fwd_kernel<HS, STORE, LP>), dim3((L.nw + W - 1) / W), dim3(W * kWave), lds, s, fa);
+    hipLaunchKernelGGL((fcr_fwd_kernel<HS, STORE, LP>), dim3(L.nw_pad / kFwdWaves), dim3(kFwdWaves * kWave),
+                       lds, s, fa);
     return launch_check("fcr_fwd_kernel");
 }
 
@@ -202,8 +201,7 @@ int launch_bwd_t(const BwdArgs &ba, const Layout &L, hipStream_t s) {
     const int lds = BwdLds<HS, LP>::BYTES;
     static std::atomic<unsigned long long> attr_done{0};
     if (const int rc = lds_attr((const void *)fcr_bwd_kernel<HS, LP>, lds, attr_done, "bwd")) return rc;
-    constexpr int W = bwd_waves<LP>();
-    hipLaunchKernelGGL((fcr_bwd_kernel<HS, LP>), dim3((L.nw + W - 1) / W), dim3(W * kWave), lds, s, ba);
+    hipLaunchKernelGGL((fcr_bwd_kernel<HS, LP>), dim3(L.nw_pad / kBwdWaves), dim3(kBwdWaves * kWave), lds, s, ba);
     return launch_check("fcr_bwd_kernel");
 }
 
@@ -1483,9 +1481,9 @@ int fcr_forward(const fcr_dims *d, fcr_options *opts, const fcr_weights *w, cons
         }
     }
     if (rc) return rc;
-    // one partial per 16-trajectory group (wave or small-batch workgroup); the fused kernels' launch-padding waves
-    // past nw write zeros, and the workspace's padding beyond the launch is never written: the sum stops at nw
-    hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(256), 0, s, (const float *)fa.loss_part, L.nw, d->B, loss);
+    // the fused kernel writes a (zero) partial for every padded wave; the small one one per group
+    hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(256), 0, s, (const float *)fa.loss_part,
+                       small ? L.nw : L.nw_pad, d->B, loss);
     return launch_check("loss_reduce_kernel");
 }
 

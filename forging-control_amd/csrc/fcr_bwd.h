@@ -175,17 +175,10 @@ __device__ __forceinline__ void bwd_cell(uint32_t fb, uint32_t tb, int lane, con
     const unsigned long long t0 = stamp_now();
     constexpr bool OWNH = OWN, NX_OWNH = NX_OWN;
     // the two waves of a SIMD take turns at the higher issue priority, cell by cell, so neither runs
-    // ahead of the other between the phase barriers (oldest-first arbitration otherwise skews them);
-    // the f16 mode runs three waves per SIMD (bwd_waves): each has it every third cell
-    if constexpr (bwd_waves<LP>() == 12) {
-        if (sp.t[4] == 2) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-        sp.t[4] = sp.t[4] == 2 ? 0 : sp.t[4] + 1;
-    } else {
-        if (sp.t[4] & 1) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-        sp.t[4] ^= 1;
-    }
+    // ahead of the other between the phase barriers (oldest-first arbitration otherwise skews them)
+    if (sp.t[4] & 1) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+    sp.t[4] ^= 1;
     using I = Img<HS, L0>;
     using G = Geo16<HS>;
     constexpr int KB = I::KB, NB = I::NB, KBB = I::KBB;
@@ -464,8 +457,8 @@ struct BwdLds {
     static_assert(I1::HALF % 16 == 0 && I0::HALF % 16 == 0, "images must be whole 16-B chunks");
 };
 
-template <int HS, bool LP, int W = bwd_waves<LP>()>
-__global__ __launch_bounds__(W * kWave, W / 4) void fcr_bwd_kernel(BwdArgs a) {
+template <int HS, bool LP>
+__global__ __launch_bounds__(kBwdWaves * kWave, kBwdWaves / 4) void fcr_bwd_kernel(BwdArgs a) {
     using LD = BwdLds<HS, LP>;
     using I1 = Img<HS, false>;
     using I0 = Img<HS, true>;
@@ -484,7 +477,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void fcr_bwd_kernel(BwdArgs a) {
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int q = lane >> 4, sl = lane & 15;
-    const int wave = blockIdx.x * W + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wave = blockIdx.x * kBwdWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int b = wave * kTile + sl;
     const bool valid = b < a.B;
     const int bc = valid ? b : a.B - 1;
@@ -540,7 +533,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void fcr_bwd_kernel(BwdArgs a) {
         n.d = (uint32_t)((nl < 2 ? doff(nj, nl + 1, nt) : 0) * 16);
         return n;
     };
-    Stamps sp = {{0, 0, 0, 0, (unsigned long long)((threadIdx.x >> 8) % (W / 4)), 0, 0, 0}};
+    Stamps sp = {{0, 0, 0, 0, (unsigned long long)((threadIdx.x >> 8) & 1), 0, 0, 0}};
     const unsigned long long tk0 = stamp_now();
     CellIn<HS> ci;
     {
@@ -600,7 +593,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void fcr_bwd_kernel(BwdArgs a) {
         float unused0, unused1;
         const unsigned long long tw1 = stamp_now();
         if (!LP) {
-            lds_fill<I1::BYTES, W>(lw, a.p.img[2]);
+            lds_fill<I1::BYTES, kBwdWaves>(lw, a.p.img[2]);
         }
         if (FCR_STAMP) {
             const unsigned long long tw2 = stamp_now();
@@ -631,7 +624,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void fcr_bwd_kernel(BwdArgs a) {
         // ---- layer 1 ----
         const unsigned long long tw3 = stamp_now();
         if (!LP) {
-            lds_fill<I1::BYTES, W>(lw, a.p.img[1]);
+            lds_fill<I1::BYTES, kBwdWaves>(lw, a.p.img[1]);
         }
         if (FCR_STAMP) sp.t[7] += stamp_now() - tw3;
 #pragma unroll
@@ -649,7 +642,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void fcr_bwd_kernel(BwdArgs a) {
         din_store<HS, LP>(nb.rd, (uint32_t)((doff(j, 1, 0)) * 16), dxo, lane);
         // ---- layer 0: dx -> window-row gradients ----
         if (!LP) {
-            lds_fill<I0::BYTES, W>(lw, a.p.img[0]);
+            lds_fill<I0::BYTES, kBwdWaves>(lw, a.p.img[0]);
         }
 #pragma unroll
         for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;

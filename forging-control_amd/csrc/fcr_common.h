@@ -24,16 +24,6 @@ constexpr int kMS = 13;          // controller hidden slots (units 4m+q), hidden
 constexpr int kFnpStride = 8;    // floats per (m, q) controller record: W0 W1 W2 b wout 0 0 0
 constexpr int kFwdWaves = 8;     // waves per forward workgroup (2 per SIMD)
 constexpr int kBwdWaves = 8;     // waves per backward workgroup (2 per SIMD)
-// The f16 mode (config 3) at 3 waves per SIMD: its resident images leave one workgroup per CU, and its kernels fit 168
-// VGPRs, so its workgroups are 12 waves (192 trajectories). The workspace pads the wave count to a multiple of every
-// geometry of the mode (kWavePadLP); a launch covers ceil(nw / W) workgroups, its waves past nw compute the last
-// trajectory and store nothing but zero partials and slab records of their own.
-constexpr int kWavesLP = 12;
-constexpr int kWavePadLP = 24;
-template <bool LP, bool STORE = true>
-constexpr int fwd_waves() { return LP && STORE ? kWavesLP : kFwdWaves; }
-template <bool LP>
-constexpr int bwd_waves() { return LP ? kWavesLP : kBwdWaves; }
 constexpr float kP1Max = 2.122366f;  // Functions.py:1411 (32e6 / p1 max_abs_)
 constexpr float kP2Max = 1.036233f;  // Functions.py:1411 (32e6 / p2 max_abs_)
 

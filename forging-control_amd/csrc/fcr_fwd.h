@@ -8,8 +8,6 @@
 // (x_t, h_{t-1}, c_{t-1}) instead of reading stored activations (fcr_bwd.h), so the forward writes
 // 8 B per unit slot and cell instead of the 24 B of local derivatives.
 #pragma once
-#include <type_traits>
-
 #include "fcr_common.h"
 #include "fcr_f16.h"
 
@@ -42,22 +40,13 @@ __device__ __forceinline__ void pace_cell(Pace &p) {
     else __builtin_amdgcn_s_setprio(0);
     p.turn ^= 1;
 }
-// three waves per SIMD (the f16 mode's 12-wave workgroups): each has the higher priority every third cell
-struct Pace3 {
-    unsigned turn;
-};
-__device__ __forceinline__ void pace_cell(Pace3 &p) {
-    if (p.turn == 2) __builtin_amdgcn_s_setprio(1);
-    else __builtin_amdgcn_s_setprio(0);
-    p.turn = p.turn == 2 ? 0 : p.turn + 1;
-}
 
 // R0, R1: the tile (unit slot) range this wave computes — the whole cell by default; the small-batch
 // kernels (fcr_small.h) split a cell's tiles over the waves of a workgroup (R0 even).
-template <int HS, bool L0, bool FIRST, bool LP, int R0 = 0, int R1 = HS, class PC = Pace>
+template <int HS, bool L0, bool FIRST, bool LP, int R0 = 0, int R1 = HS>
 __device__ __forceinline__ void fwd16_cell(const float *__restrict__ lw, int lane, float x0, float x1,
                                            const float (&x)[HS], const float (&hp)[HS], float (&c)[HS],
-                                           float (&hout)[HS], PC &turn) {
+                                           float (&hout)[HS], Pace &turn) {
     pace_cell(turn);
     using G = Geo16<HS>;
     constexpr int KB = L0 ? G::KB0 : G::KB1;
@@ -145,8 +134,8 @@ __device__ __forceinline__ unsigned long long fstamp() {
 #endif
 }
 
-template <int HS, bool STORE, bool LP, int W = fwd_waves<LP, STORE>()>
-__global__ __launch_bounds__(W * kWave, W / 4) void fcr_fwd_kernel(FwdArgs a) {
+template <int HS, bool STORE, bool LP>
+__global__ __launch_bounds__(kFwdWaves * kWave, kFwdWaves / 4) void fcr_fwd_kernel(FwdArgs a) {
     using G = Geo16<HS>;
     extern __shared__ __attribute__((aligned(16))) float lw[];
     // fp32 mode: [layer 1|2 fragments, refilled per phase | layer 0 | misc];
@@ -168,7 +157,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void fcr_fwd_kernel(FwdArgs a) {
     const int lane = threadIdx.x & 63;
     const int q = lane >> 4, sl = lane & 15;
     // wave-uniform by construction; readfirstlane lets the compiler keep every address base in SGPRs
-    const int wave = blockIdx.x * W + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wave = blockIdx.x * kFwdWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int b = wave * kTile + sl;
     const bool valid = b < a.B;
     const int bc = valid ? b : a.B - 1;   // out-of-range lanes recompute the last trajectory
@@ -203,9 +192,8 @@ __global__ __launch_bounds__(W * kWave, W / 4) void fcr_fwd_kernel(FwdArgs a) {
     const __amdgpu_buffer_rsrc_t rx = wave_rsrc(a.xw + (size_t)wave * N * kL * kWave, (size_t)N * kL * kWave * 8);
 
     unsigned long long st_fill = 0, st_l0 = 0, st_l2 = 0, st_head = 0;
-    // waves w, w + 4 (, w + 8) share a SIMD: they start out of phase
-    std::conditional_t<W == 12, Pace3, Pace> turn;
-    turn.turn = (threadIdx.x >> 8) % (W / 4);
+    Pace turn;
+    turn.turn = (threadIdx.x >> 8) & 1;   // waves w and w+4 share a SIMD: start out of phase
     const unsigned long long st_k0 = fstamp();
     for (int j = 0; j < N; ++j) {
         const unsigned long long st_w0 = fstamp();
@@ -236,7 +224,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void fcr_fwd_kernel(FwdArgs a) {
         // the resident layer 0 for the phase, layer 2's replace them after it ----
         {
             const unsigned long long st_f0 = fstamp();
-            if (!LP) lds_fill<G::FA1 * 4, W>(lw, a.p.fa[1]);   // its first barrier also publishes the resident blocks
+            if (!LP) lds_fill<G::FA1 * 4, kFwdWaves>(lw, a.p.fa[1]);   // its first barrier also publishes the resident blocks
             else if (j == 0) __syncthreads();   // f16 mode: every layer resident, never refilled
             const unsigned long long st_f1 = fstamp();
             st_fill += st_f1 - st_f0;
@@ -299,7 +287,7 @@ __global__ __launch_bounds__(W * kWave, W / 4) void fcr_fwd_kernel(FwdArgs a) {
         if constexpr (!LP) {
             constexpr int l = 2;
             const unsigned long long st_f0 = fstamp();
-            lds_fill<G::FA1 * 4, W>(lw, a.p.fa[l]);
+            lds_fill<G::FA1 * 4, kFwdWaves>(lw, a.p.fa[l]);
             const float *lwc = lw;
             const unsigned long long st_f1 = fstamp();
             st_fill += st_f1 - st_f0;
