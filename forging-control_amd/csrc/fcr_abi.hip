@@ -21,6 +21,7 @@
 #include "fcr_img.h"
 #include "fcr_pack.h"
 #include "fcr_host.h"
+#include "fcr_pipe.h"
 #include "fcr_small.h"
 #include "fcr_sur.h"
 #include "fcr_surrogate.h"
@@ -85,6 +86,7 @@ namespace {
 struct Layout {
     int HS, nw, nw_pad;
     size_t fa[3], img[3], fcp, fcb, fnp, wsc, rng, xhat, dv, loss_part, fnn_part, hseq, cseq, xw, dseq, dxrow, stamp, total;
+    size_t pipe_flags, pipe_rows;   // the layer-pipelined small-batch kernels (fcr_pipe.h), L.nw <= kPipeMaxGroups
     int ctrl_blocks;
 };
 
@@ -121,6 +123,9 @@ int check_dims(const fcr_dims *d) {
         return fail(FCR_EUNSUPPORTED, "reduced precision is built for H <= %d (the fused kernels)", 4 * kMaxSlots);
     return FCR_OK;
 }
+
+// the layer-pipelined small-batch kernels (fcr_pipe.h) run at most this many 16-trajectory groups (3 workgroups each)
+constexpr int kPipeMaxGroups = 32;
 
 Layout make_layout(const fcr_dims *d, int with_backward) {
     Layout L{};
@@ -163,6 +168,10 @@ Layout make_layout(const fcr_dims *d, int with_backward) {
 #if FCR_STAMP
     L.stamp = take(sizeof(unsigned long long) * L.nw_pad * 16);   // [backward 8 | forward 8] per wave
 #endif
+    if (L.nw <= kPipeMaxGroups) {
+        L.pipe_flags = take(sizeof(unsigned) * (size_t)L.nw * kPipeFlags);
+        L.pipe_rows = take(sizeof(float) * (size_t)L.nw * d->N * kTile * kPipeRow);
+    }
     L.total = off;
     return L;
 }
@@ -224,6 +233,55 @@ bool use_small(const fcr_dims *d, const Layout &L, const fcr_options *o) {
 }
 void note_kernels(fcr_options *o, int family) {
     if (o) o->kernels = family;
+}
+// The small-batch family's layer-pipelined geometry (fcr_pipe.h: three workgroups per group that wait on each other)
+// for B <= g_pipe_max_batch (default 512; 0 = never): only where every workgroup of the launch is resident at once —
+// 3 per group, one per CU by LDS, within half the device's CUs (the other half for whatever else runs).
+std::atomic<int> g_pipe_max_batch{512};
+int device_cus() {
+    static std::atomic<int> cus[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    int n = cus[dev].load(std::memory_order_relaxed);
+    if (n == 0) {
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+        cus[dev].store(n, std::memory_order_relaxed);
+    }
+    return n;
+}
+bool use_pipe(const fcr_dims *d, const Layout &L, const fcr_options *o) {
+    return use_small(d, L, o) && d->B <= g_pipe_max_batch.load(std::memory_order_relaxed) && L.nw <= kPipeMaxGroups &&
+           6 * L.nw <= device_cus();
+}
+PipeArgs pipe_args(const Layout &L, char *base) {
+    PipeArgs p;
+    p.flags = (unsigned *)(base + L.pipe_flags);
+    p.rows = (float *)(base + L.pipe_rows);
+    p.groups = L.nw;
+    return p;
+}
+int pipe_clear(const PipeArgs &pa, const Layout &L, hipStream_t s) {
+    hipLaunchKernelGGL(fcr_pipe_clear_kernel, dim3(1), dim3(kWave), 0, s, pa.flags, L.nw * kPipeFlags);
+    return launch_check("fcr_pipe_clear_kernel");
+}
+template <int HS, bool STORE>
+int launch_pfwd_t(const FwdArgs &fa, const PipeArgs &pa, const Layout &L, hipStream_t s) {
+    constexpr int lds = Pipe<HS>::LDS_FWD;
+    static std::atomic<unsigned long long> attr_done{0};
+    if (const int rc = lds_attr((const void *)fcr_pfwd_kernel<HS, STORE>, lds, attr_done, "pfwd")) return rc;
+    if (const int rc = pipe_clear(pa, L, s)) return rc;
+    hipLaunchKernelGGL((fcr_pfwd_kernel<HS, STORE>), dim3(24 * ((L.nw + 7) / 8)), dim3(Small<HS>::NQ * kWave), lds, s, fa,
+                       pa);
+    return launch_check("fcr_pfwd_kernel");
+}
+template <int HS>
+int launch_pbwd_t(const BwdArgs &ba, const PipeArgs &pa, const Layout &L, hipStream_t s) {
+    constexpr int lds = Pipe<HS>::LDS_BWD;
+    static std::atomic<unsigned long long> attr_done{0};
+    if (const int rc = lds_attr((const void *)fcr_pbwd_kernel<HS>, lds, attr_done, "pbwd")) return rc;
+    if (const int rc = pipe_clear(pa, L, s)) return rc;
+    hipLaunchKernelGGL((fcr_pbwd_kernel<HS>), dim3(24 * ((L.nw + 7) / 8)), dim3(Small<HS>::NQ * kWave), lds, s, ba, pa);
+    return launch_check("fcr_pbwd_kernel");
 }
 
 template <int HS, bool STORE>
@@ -1317,6 +1375,8 @@ int fcr_set_small_batch_limit(int32_t max_batch) {
 }
 
 int fcr_get_small_batch_limit(void) { return g_small_max_batch.load(); }
+int fcr_set_small_pipe_limit(int32_t max_batch) { return g_pipe_max_batch.exchange(max_batch < 0 ? 0 : max_batch); }
+int fcr_get_small_pipe_limit(void) { return g_pipe_max_batch.load(); }
 
 int64_t fcr_set_wide_keep_budget(int64_t bytes) {
     return g_wide_keep_budget.exchange(bytes < 0 ? -1 : bytes);
@@ -1469,7 +1529,11 @@ int fcr_forward(const fcr_dims *d, fcr_options *opts, const fcr_weights *w, cons
 #endif
     const bool small = use_small(d, L, opts);
     note_kernels(opts, small ? FCR_KERNELS_SMALL : FCR_KERNELS_FUSED);
-    if (small) {
+    if (small && use_pipe(d, L, opts)) {
+        const PipeArgs pa = pipe_args(L, base);
+        if (L.HS == 8) rc = with_backward ? launch_pfwd_t<8, true>(fa, pa, L, s) : launch_pfwd_t<8, false>(fa, pa, L, s);
+        else rc = with_backward ? launch_pfwd_t<13, true>(fa, pa, L, s) : launch_pfwd_t<13, false>(fa, pa, L, s);
+    } else if (small) {
         if (L.HS == 8) rc = with_backward ? launch_sfwd_t<8, true>(fa, L, s) : launch_sfwd_t<8, false>(fa, L, s);
         else rc = with_backward ? launch_sfwd_t<13, true>(fa, L, s) : launch_sfwd_t<13, false>(fa, L, s);
     } else {
@@ -1530,7 +1594,10 @@ int fcr_backward(const fcr_dims *d, fcr_options *opts, const float *X, const flo
     ba.p = packed_ptrs(L, base);
     const bool small = use_small(d, L, opts);
     note_kernels(opts, small ? FCR_KERNELS_SMALL : FCR_KERNELS_FUSED);
-    if (small) {
+    if (small && use_pipe(d, L, opts)) {
+        const PipeArgs pa = pipe_args(L, base);
+        rc = L.HS == 8 ? launch_pbwd_t<8>(ba, pa, L, s) : launch_pbwd_t<13>(ba, pa, L, s);
+    } else if (small) {
         rc = L.HS == 8 ? launch_sbwd_t<8>(ba, L, s) : launch_sbwd_t<13>(ba, L, s);
     } else {
         switch (L.HS) {

@@ -1,0 +1,443 @@
+// fcr_pipe.h — layer-pipelined small-batch rollout (config 1: the reference trains at B = 15, UL/Main.py:84,297).
+//
+// The small-batch kernels (fcr_small.h) give a 16-trajectory group ONE workgroup that walks every cell of the rollout
+// in sequence: per window 30 dependent cells (3 layers x 10 steps) plus two weight-image refills, in both passes. Here
+// a group gets THREE workgroups, one per LSTM layer, each holding its layer's weights resident in LDS (no refills),
+// and the layers run as a wavefront across workgroups: cell (j, l, t) needs only (j, l, t - 1) of its own workgroup
+// and, from the layer below (forward) or above (backward), the same cell's input, handed over through the sequence
+// slabs (the layout fcr_small.h / the fused kernels use) and a per-(group, layer, wave) progress counter
+// (pipe_wait / pipe_publish, fcr_small.h). Windows pipeline too: in the forward only window j's last row depends on
+// window j - 1's output (x_hat_{j-1} and the controller's u_j, handed from the layer-2 workgroup to the layer-0 one),
+// so layer 0 runs window j's cells t = 0..8 while layers 1, 2 finish window j - 1; in the backward window j - 1's head
+// needs only window j's first layer-0 cell (the row gradient of row j + 9).
+// Within a workgroup, cells run exactly as fcr_small.h runs them (wave w owns the slots of record quad w; the same
+// fwd16_cell / sb_step arithmetic, the same LDS exchange and fixed-order reductions), so results are bit-identical to
+// the small-batch kernels'.
+// Co-residency: a workgroup may wait on another of its launch, so the host runs this family only when every
+// workgroup fits the device at once (3 x groups <= CUs / 2; a CU holds at least one) and bounds every wait.
+// Placement: the three workgroups of a group get block ids of one residue mod 8, i.e. one XCD (one L2).
+#pragma once
+#include "fcr_small.h"
+
+namespace fcr {
+
+template <int HS>
+struct Pipe {
+    static constexpr int NQ = Small<HS>::NQ;
+    // one progress counter per producing workgroup (the count of its cells whose outputs are signalled): forward layer
+    // 0, layer 1, the layer-2 workgroup's hand-off rows; backward layers 0, 1, 2
+    static constexpr int F0 = 0, F1 = 1, ROW = 2, BWD = 3;
+    static_assert(BWD + 3 <= kPipeAbort, "pipe counters");
+    // forward: [layer fragments (layer 0's or 1 / 2's, resident) | controller records | fc.weight | fc.bias | h exchange]
+    static constexpr int FRAG = Geo16<HS>::FA1 > Geo16<HS>::FA0 ? Geo16<HS>::FA1 : Geo16<HS>::FA0;   // floats
+    static constexpr int LDS_FWD = (FRAG + Geo16<HS>::FNP + Geo16<HS>::FCP + 4) * 4 + Small<HS>::XBUF;
+    // backward: [layer image (resident) | controller records | fc.weight | partial products]
+    static constexpr int LDS_BWD = BwdLds<HS, false>::BYTES + Small<HS>::RED;
+    static_assert(LDS_FWD <= 163840 && LDS_BWD <= 163840, "pipe LDS");   // at least one workgroup per CU
+};
+// the hand-off row of window j: x_hat_j (4 floats, lane group q's column q) and u_{j+1}, per trajectory
+constexpr int kPipeRow = 8;   // floats per trajectory and window
+
+struct PipeArgs {
+    unsigned *flags;   // [groups][kPipeFlags], zeroed before each launch
+    float *rows;       // [groups][N][16][kPipeRow]
+    int groups;
+};
+
+// zeroes the progress counters ahead of each pipelined launch, on the launch's stream. A kernel rather than
+// hipMemsetAsync: a memset captured into a HIP graph left stale counters in replays (the consumers ran ahead on the
+// previous replay's rows: profiles/round6_b15_pipe_graph.log); a kernel node has the ordering and the release / acquire
+// of any kernel boundary.
+__global__ __launch_bounds__(kWave) void fcr_pipe_clear_kernel(unsigned *flags, int n) {
+    for (int i = threadIdx.x; i < n; i += kWave) flags[i] = 0u;
+}
+
+// block id -> (group, layer): the ids of one group share their residue mod 8 (one XCD); -1: an unused id
+__device__ __forceinline__ int pipe_role(int groups, int &layer) {
+    const int id = blockIdx.x, xcd = id & 7, k = id >> 3;
+    layer = k % 3;
+    const int grp = xcd + 8 * (k / 3);
+    return grp < groups ? grp : -1;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// forward. Per cell (linear index n = j * 10 + t of the workgroup's layer): the gates of this wave's slots, the h
+// exchange through LDS (one barrier), then this wave's quad of the h record (and c) — the record write-through, as the
+// layer above reads it — and at the NEXT cell's barrier, all four waves having drained those stores, one lane signals
+// n + 1 cells done. Layers 1, 2 load their input records (sc1) two cells ahead.
+// ---------------------------------------------------------------------------------------------------
+template <int HS, bool STORE>
+__global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdArgs a, PipeArgs pa) {
+    using G = Geo16<HS>;
+    using P = Pipe<HS>;
+    int layer;
+    const int grp = pipe_role(pa.groups, layer);
+    if (grp < 0) return;   // uniform over the workgroup
+    extern __shared__ __attribute__((aligned(16))) float lw[];
+    float *lfnp = lw + P::FRAG;
+    float *lfcp = lfnp + G::FNP;
+    float *lfcb = lfcp + G::FCP;
+    f32x4 *xbuf = reinterpret_cast<f32x4 *>(lfcb + 4);
+    constexpr int RECB = Geo<HS>::QC * 16;
+    lds_copy(lw, a.p.fa[layer], layer == 0 ? G::FA0 : G::FA1);
+    if (layer == 2) {
+        lds_copy(lfnp, a.p.fnp, G::FNP);
+        lds_copy(lfcp, a.p.fcp, G::FCP);
+        lds_copy(lfcb, a.p.fcb, 4);
+    }
+    const int lane = threadIdx.x & 63;
+    const int q = lane >> 4, sl = lane & 15;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = grp * kTile + sl;
+    const bool valid = b < a.B;
+    const bool lead = w == 0;
+    const int bc = valid ? b : a.B - 1;
+    const int N = a.N;
+    const int NC = N * kL;   // cells of the workgroup's layer
+    const float alpha = a.alpha;
+    unsigned *fl = pa.flags + (size_t)grp * kPipeFlags;
+    float *rowbuf = pa.rows + (size_t)grp * N * kTile * kPipeRow;
+
+    const float ref = a.X[(size_t)bc * kCtrlIn + 2];                 // Functions.py:1392
+    const float *st = a.states + (size_t)bc * kL * kIn;
+    const float scq = a.p.wsc[q], sc4 = a.p.wsc[4];
+    const float u0 = a.u0[bc];
+
+    float c[HS], hout[HS], hp[HS];
+#pragma unroll
+    for (int r = 0; r < HS; ++r) c[r] = hout[r] = hp[r] = 0.0f;
+    const size_t qcell = (size_t)Geo<HS>::QC;
+    const size_t seq = (size_t)N * kLayers * kL * qcell;
+    f32x4 *cs_wave = a.cseq + (size_t)grp * seq;
+    const __amdgpu_buffer_rsrc_t rh = wave_rsrc(a.hseq + (size_t)grp * seq, seq * 16);
+    f32x2 *xw_wave = a.xw + (size_t)grp * N * kL * kWave;
+    auto hoff = [&](int n, int l) {   // byte offset of cell n = j * 10 + t of layer l in the group's h slab
+        return (uint32_t)((((size_t)(n / kL) * kLayers + l) * kL + n % kL) * qcell * 16);
+    };
+    Pace turn;
+    turn.turn = 0;
+    __syncthreads();
+    if (layer == 0) {
+        // ---- layer 0: the window ring (B-operand layout), its last row from the layer-2 workgroup's hand-off ----
+        float w0[kL], w1[kL];
+#pragma unroll
+        for (int t = 0; t < kL; ++t) {
+            w0[t] = st[t * kIn + q] * scq;
+            w1[t] = (q == 0) ? st[t * kIn + 4] * sc4 : 0.0f;
+        }
+        if (q == 0) w1[kL - 1] = u0 * sc4;                            // Functions.py:1396
+        for (int j = 0; j < N; ++j) {
+            if (j > 0) {   // Functions.py:1433-1434: the window slides; its new last row arrives at t = 9
+#pragma unroll
+                for (int k = 0; k < kL - 1; ++k) {
+                    w0[k] = w0[k + 1];
+                    w1[k] = w1[k + 1];
+                }
+            }
+            for (int t = 0; t < kL; ++t) {
+                if (j > 0 && t == kL - 1) {   // after 9 rotations the pending row is at the ring's head
+                    pipe_wait(fl, fl + P::ROW, (unsigned)j);
+                    const float *rw = rowbuf + ((size_t)(j - 1) * kTile + sl) * kPipeRow;
+                    const float xq = __hip_atomic_load(rw + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const float uj = __hip_atomic_load(rw + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    w0[0] = xq * scq;                                  // x_hat_{j-1}, column q
+                    w1[0] = (q == 0) ? uj * sc4 : 0.0f;                // u_j
+                }
+                const float x0 = w0[0], x1 = w1[0];
+                rot_left(w0);
+                rot_left(w1);
+                char *xb = reinterpret_cast<char *>(xbuf) + (t & 1) * RECB;
+                by_quad<HS>(w, [&](auto Wc) {
+                    constexpr int W = decltype(Wc)::v;
+                    using Q = QR<HS, W>;
+                    if (t == 0) fwd16_cell<HS, true, true, false, Q::R0, Q::R1>(lw, lane, x0, x1, hp, hp, c, hout, turn);
+                    else fwd16_cell<HS, true, false, false, Q::R0, Q::R1>(lw, lane, x0, x1, hp, hp, c, hout, turn);
+                    xrec_put<HS, W>(xb, hout, lane);
+                });
+                pipe_drain();   // this wave's record stores of the previous cell (long complete)
+                lds_barrier();
+                pipe_signal(fl + P::F0, (unsigned)(j * kL + t));
+                load_quads<HS>(hp, reinterpret_cast<const f32x4 *>(xb), lane);   // the whole split record of h_t
+                by_quad<HS>(w, [&](auto Wc) {
+                    constexpr int W = decltype(Wc)::v;
+                    st_quad_sc1<HS, W>(rh, hoff(j * kL + t, 0), hp, lane);
+                    if (STORE && t + 1 < kL) store_quad<HS, W>(cs_wave + (size_t)hoff(j * kL + t, 0) / 16, c, lane);
+                });
+                if (STORE && lead) xw_wave[((size_t)j * kL + t) * kWave + lane] = f32x2{x0, x1};
+            }
+        }
+        pipe_drain();
+        __syncthreads();
+        pipe_signal(fl + P::F0, (unsigned)NC);
+        return;
+    }
+    // ---- layers 1, 2: input records from the layer below (sc1), two cells ahead ----
+    const bool keep_h = layer == 1 || STORE;
+    unsigned *below = fl + (layer == 1 ? P::F0 : P::F1);
+    float u_prev = u0;
+    float cmd_j = alpha * sq(st[(kL - 2) * kIn + 4] - u0);            // Functions.py:1405
+    float cmd_sum = 0.0f, err_sum = 0.0f, tot_sum = 0.0f;
+    if (layer == 2 && lead && valid && q == 0) a.prediction[(size_t)b * N] = u0;   // Functions.py:1455
+    f32x4 xa[Geo<HS>::HQ], xn[Geo<HS>::HQ], xf[Geo<HS>::HQ];   // the input records of cells n, n + 1, n + 2
+#pragma unroll
+    for (int k = 0; k < Geo<HS>::HQ; ++k) xf[k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    pipe_wait(fl, below, 1);
+    ld_rec_sc1<HS>(xa, rh, hoff(0, layer - 1), lane);
+    pipe_wait(fl, below, 2);
+    ld_rec_sc1<HS>(xn, rh, hoff(1, layer - 1), lane);
+    for (int j = 0; j < N; ++j) {
+        for (int t = 0; t < kL; ++t) {
+            const int n = j * kL + t;
+            const bool last = layer == 2 && t + 1 == kL;   // h_9 of layer 2: the readout's, in fp32
+            char *xb = reinterpret_cast<char *>(xbuf) + (t & 1) * RECB;
+            float xc[HS];
+#pragma unroll
+            for (int r = 0; r < HS; ++r) xc[r] = xa[r >> 2][r & 3];
+            by_quad<HS>(w, [&](auto Wc) {
+                constexpr int W = decltype(Wc)::v;
+                using Q = QR<HS, W>;
+                if (t == 0) fwd16_cell<HS, false, true, false, Q::R0, Q::R1>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
+                else fwd16_cell<HS, false, false, false, Q::R0, Q::R1>(lw, lane, 0.0f, 0.0f, xc, hp, c, hout, turn);
+                if (last) xchg_put<HS, W>(reinterpret_cast<f32x4 *>(xb), hout, lane);
+                else xrec_put<HS, W>(xb, hout, lane);
+            });
+            pipe_drain();   // this wave's record stores of the previous cell and its load of cell n + 1's input
+            if (n + 2 < NC) {
+                pipe_wait(fl, below, (unsigned)(n + 3));
+                ld_rec_sc1<HS>(xf, rh, hoff(n + 2, layer - 1), lane);
+            }
+            lds_barrier();
+            if (layer == 1) pipe_signal(fl + P::F1, (unsigned)n);
+            if (last) {
+                xchg_get<HS>(reinterpret_cast<const f32x4 *>(xb), hout, lane);
+            } else {
+                load_quads<HS>(hp, reinterpret_cast<const f32x4 *>(xb), lane);
+                if (keep_h)
+                    by_quad<HS>(w, [&](auto Wc) { st_quad_sc1<HS, decltype(Wc)::v>(rh, hoff(n, layer), hp, lane); });
+            }
+            if (STORE && t + 1 < kL)
+                by_quad<HS>(w, [&](auto Wc) {
+                    store_quad<HS, decltype(Wc)::v>(cs_wave + (size_t)hoff(n, layer) / 16, c, lane);
+                });
+#pragma unroll
+            for (int k = 0; k < Geo<HS>::HQ; ++k) {
+                xa[k] = xn[k];
+                xn[k] = xf[k];
+            }
+        }
+        if (layer != 2) continue;
+        // ---- layer 2, end of window j: readout fc(h_9) (Functions.py:377), costs, the next command ----
+        const float *lfnp_j = opaque(lfnp), *lfcp_j = opaque(lfcp), *lfcb_j = opaque(lfcb);
+        float xo[kOut];
+#pragma unroll
+        for (int o = 0; o < kOut; ++o) {
+            float p = 0.0f;
+#pragma unroll
+            for (int r = 0; r < HS; ++r) p += lfcp_j[(o * HS + r) * 4 + q] * hout[r];
+            xo[o] = xor_sum_q(p) + lfcb_j[o];
+        }
+        if (a.noise) {                                                 // Functions.py:1400-1402
+            const float *nz = a.noise + ((size_t)bc * N + j) * kOut;
+#pragma unroll
+            for (int o = 0; o < kOut; ++o) xo[o] += nz[o];
+        }
+        const float xh0 = xo[0], xh1 = xo[1], xh2 = xo[2], xh3 = xo[3];
+        const float mine = sel4(q, xh0, xh1, xh2, xh3);
+        if (lead && valid) {
+            a.xhat_ws[((size_t)b * N + j) * kOut + q] = mine;
+            if (a.xhat_user) a.xhat_user[((size_t)b * N + j) * kOut + q] = mine;
+        }
+        const float err = sq(xh0 - ref);                              // Functions.py:1405-1414, 1443-1452
+        const float con = relu(-xh1) + relu(-xh2) + relu(xh1 - kP1Max) + relu(xh2 - kP2Max);
+        tot_sum += (err + cmd_j) + con;
+        err_sum += err;
+        cmd_sum += cmd_j;
+        if (j + 1 < N) {                                               // Functions.py:1421-1434
+            float z[kMS];
+            const float un = hardtanh(fnn_pre(lfnp_j, q, xh0, xh3, ref, z));
+            cmd_j = alpha * sq(u_prev - un);                           // Functions.py:1446
+            u_prev = un;
+            if (lead) {   // the hand-off row of window j (write-through; only this wave stores it), then its counter
+                float *rw = rowbuf + ((size_t)j * kTile + sl) * kPipeRow;
+                __hip_atomic_store(rw + q, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (q == 0) __hip_atomic_store(rw + 4, un, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (valid && q == 0) a.prediction[(size_t)b * N + j + 1] = un;   // Functions.py:1466
+                pipe_drain();
+                pipe_signal(fl + P::ROW, (unsigned)(j + 1));
+            }
+        }
+    }
+    if (layer == 1) {
+        pipe_drain();
+        __syncthreads();
+        pipe_signal(fl + P::F1, (unsigned)NC);
+        return;
+    }
+    const float cost = tot_sum / (float)N;                             // Functions.py:1458-1460
+    if (lead && valid && q == 0) {
+        a.cost[b] = cost;
+        a.command[b] = cmd_sum / (float)N;
+        a.error[b] = err_sum / (float)N;
+    }
+    float part = (valid && q == 0) ? cost : 0.0f;
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) part += __shfl_xor(part, m);
+    if (lead && lane == 0) a.loss_part[grp] = part;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// backward: each layer's workgroup runs fcr_sbwd_kernel's per-layer phases (sb_phase, PIPE) over every window; layer
+// 2's also the window heads (cost gradients, the controller backward, dh_9), layer 0's the window-row gradients
+// (each wave its own copy, fcr_small.h) and g_u0
+// ---------------------------------------------------------------------------------------------------
+template <int HS>
+__global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pbwd_kernel(BwdArgs a, PipeArgs pa) {
+    using LD = BwdLds<HS, false>;
+    using I1 = Img<HS, false>;
+    using I0 = Img<HS, true>;
+    using P = Pipe<HS>;
+    constexpr int NQ = P::NQ;
+    int layer;
+    const int grp = pipe_role(pa.groups, layer);
+    if (grp < 0) return;
+    extern __shared__ __attribute__((aligned(16))) float lw[];
+    float *lfnp = lw + LD::REGION / 4;
+    float *lfcp = lfnp + LD::FNP;
+    if (layer == 0) lds_copy(lw, a.p.img[0], I0::BYTES / 4);
+    else lds_copy(lw, a.p.img[layer], I1::BYTES / 4);
+    if (layer == 2) {
+        lds_copy(lfnp, a.p.fnp, LD::FNP);
+        lds_copy(lfcp, a.p.fcp, LD::FCP);
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int q = lane >> 4, sl = lane & 15;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int b = grp * kTile + sl;
+    const bool valid = b < a.B;
+    const bool lead = w == 0;
+    const int bc = valid ? b : a.B - 1;
+    const int N = a.N;
+    const float alpha = a.alpha;
+    const float wgt = valid ? a.dloss[0] / ((float)a.B * (float)N) : 0.0f;   // Functions.py:1458, 1463
+    const float ref = a.X[(size_t)bc * kCtrlIn + 2];
+    const float s84 = a.states[(size_t)bc * kL * kIn + (kL - 2) * kIn + 4];
+    const float *pred = a.prediction + (size_t)bc * N;
+    const float *xh = a.xhat + (size_t)bc * N * kOut;
+
+    SbCtx<HS, true> x;
+    {
+        const ImgLane<I1::U> L1 = img_lane<I1::U>(lds_offset(lw), lane);
+        const ImgLane<I0::U> L0 = img_lane<I0::U>(lds_offset(lw), lane);
+        x.fb1 = L1.fb;
+        x.tb1 = L1.tb;
+        x.fb0 = L0.fb;
+        x.tb0 = L0.tb;
+    }
+    x.lane = lane;
+    x.N = N;
+    Stamps sp = {{0, 0, 0, 0, 0, 0, 0, 0}};
+    x.sp = &sp;
+    x.scq = a.p.wsc[q];
+    x.sc4 = a.p.wsc[4];
+    x.red = reinterpret_cast<f32x4 *>(lw + LD::BYTES / 4);
+    x.rr = wave_rsrc(a.dxrow + ((size_t)grp * NQ + w) * N * kL * kWave, (size_t)N * kL * kWave * 8);
+    const size_t qcell = (size_t)Geo<HS>::QC;
+    const size_t seq_sz = (size_t)N * kLayers * kL * qcell;
+    const size_t dseq_sz = (size_t)N * 2 * kL * qcell;
+    x.nb.rh = wave_rsrc(a.hseq + (size_t)grp * seq_sz, seq_sz * 16);
+    x.nb.rc = wave_rsrc(a.cseq + (size_t)grp * seq_sz, seq_sz * 16);
+    x.nb.rx = wave_rsrc(a.xw + (size_t)grp * N * kL * kWave, (size_t)N * kL * kWave * 8);
+    x.nb.rd = wave_rsrc(a.dseq + (size_t)grp * dseq_sz, dseq_sz * 16);
+    x.dseq_w = a.dseq + (size_t)grp * dseq_sz;
+    unsigned *fl = pa.flags + (size_t)grp * kPipeFlags;
+    x.flags = fl;
+    x.fl_own = P::BWD + layer;
+    x.fl_above = layer < 2 ? P::BWD + layer + 1 : -1;
+    auto row_grad = [&](int rho) {   // sum over windows v = max(0, rho-9) .. min(N-1, rho) of dx(v, rho-v)
+        f32x2 acc2 = {0.0f, 0.0f};
+        const int w_hi = rho < N - 1 ? rho : N - 1;
+        const int w_lo = rho - (kL - 1) > 0 ? rho - (kL - 1) : 0;
+        // another workgroup's (layer 0's) write-through rows: sc1 loads
+        for (int v = w_hi; v >= w_lo; --v) acc2 += buf_ld2_sc1(x.rr, lane * 8, (uint32_t)((v * kL + (rho - v)) * kWave * 8));
+        return acc2;
+    };
+    float dh[HS], dc[HS];
+#pragma unroll
+    for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
+    CellIn<HS> ci;
+    {   // the first cell (N - 1, layer, 9): its x, h (forward records), c and din (the layer above's first cell)
+        if (layer < 2) pipe_wait(fl, fl + x.fl_above, x.done_after(N - 1, kL - 1));
+        const NextIn f = x.next_of(N, layer, 0);   // the cell after (N, layer, 0) = (N - 1, layer, 9)
+        by_quad<HS>(w, [&](auto Wc) {
+            constexpr int W = decltype(Wc)::v;
+            if (layer == 0) sb_load_a<HS, true, true>(ci, f, lane);
+            else sb_load_a<HS, false, true>(ci, f, lane);
+            if (layer < 2) sb_load_b<HS, W, true, true, true>(ci, f, lane);   // din: the layer above's (sc1)
+            else sb_load_b<HS, W, true, false>(ci, f, lane);
+        });
+    }
+    float dh_out[HS];
+#pragma unroll
+    for (int r = 0; r < HS; ++r) dh_out[r] = 0.0f;
+    for (int j = N - 1; j >= 0; --j) {
+        if (layer == 2) {   // ---- window head (Functions.py:1443-1452, 1424-1430, 377) ----
+            const float *lfnp_j = opaque(lfnp), *lfcp_j = opaque(lfcp);
+            const float x0 = xh[j * kOut + 0], x1 = xh[j * kOut + 1], x2 = xh[j * kOut + 2], x3 = xh[j * kOut + 3];
+            const float uj = pred[j], uj1 = pred[j + 1 < N ? j + 1 : j], uj2 = pred[j + 2 < N ? j + 2 : j];
+            float d0 = wgt * 2.0f * (x0 - ref);
+            float d1 = wgt * ((-x1 > 0.0f ? -1.0f : 0.0f) + (x1 - kP1Max > 0.0f ? 1.0f : 0.0f));
+            float d2 = wgt * ((-x2 > 0.0f ? -1.0f : 0.0f) + (x2 - kP2Max > 0.0f ? 1.0f : 0.0f));
+            float d3 = 0.0f;
+            if (j <= N - 2) {
+                // row 10 + j is complete once layer 0 has done window j + 1's first cell (t = 9)
+                pipe_wait(fl, fl + P::BWD, x.done_after(j + 1, kL - 1));
+                const f32x2 Gr = row_grad(kL + j);
+                d0 += __shfl(Gr[0], sl);
+                d1 += __shfl(Gr[0], sl + 16);
+                d2 += __shfl(Gr[0], sl + 32);
+                d3 += __shfl(Gr[0], sl + 48);
+                const float g4 = __shfl(Gr[1], sl);
+                float du = 2.0f * alpha * wgt * (uj1 - uj);
+                if (j + 2 < N) du += 2.0f * alpha * wgt * (uj1 - uj2);
+                du += g4;
+                float z[kMS];
+                const float v = fnn_pre(lfnp_j, q, x0, x3, ref, z);
+                const float dv = (v > -1.0f && v < 1.0f) ? du : 0.0f;
+                float dca = 0.0f, dcb = 0.0f;
+#pragma unroll
+                for (int m = 0; m < kMS; ++m) {
+                    const float *p = lfnp_j + (m * 4 + q) * kFnpStride;
+                    const float dz = (z[m] > 0.0f) ? dv * p[4] : 0.0f;
+                    dca += dz * p[0];
+                    dcb += dz * p[1];
+                }
+                if (lead && valid && q == 0) a.dv[(size_t)b * N + j] = dv;
+                d0 += xor_sum_q(dca);
+                d3 += xor_sum_q(dcb);
+            } else if (lead && valid && q == 0) {
+                a.dv[(size_t)b * N + j] = 0.0f;
+            }
+#pragma unroll
+            for (int r = 0; r < HS; ++r) {
+                const float *fp = lfcp_j + r * 4 + q;
+                dh_out[r] = fp[0] * d0 + fp[HS * 4] * d1 + fp[2 * HS * 4] * d2 + fp[3 * HS * 4] * d3;
+            }
+            by_quad<HS>(w, [&](auto Wc) { sb_phase<HS, 2, decltype(Wc)::v>(x, j, dh_out, ci, dh, dc); });
+        } else if (layer == 1) {
+            by_quad<HS>(w, [&](auto Wc) { sb_phase<HS, 1, decltype(Wc)::v>(x, j, dh_out, ci, dh, dc); });
+        } else {
+            by_quad<HS>(w, [&](auto Wc) { sb_phase<HS, 0, decltype(Wc)::v>(x, j, dh_out, ci, dh, dc); });
+        }
+    }
+    pipe_drain();   // the last cell's outputs, signalled once every wave has drained them
+    __syncthreads();
+    pipe_signal(fl + x.fl_own, x.done_after(0, 0));
+    if (layer != 0) return;
+    const float g_u0_rows = row_grad(kL - 1)[1];   // row 9, col 4 = u0 (Functions.py:1396)
+    float du0 = 2.0f * alpha * wgt * (pred[0] - s84);
+    if (N > 1) du0 += 2.0f * alpha * wgt * (pred[0] - pred[1]);
+    if (lead && valid && q == 0) a.g_u0[b] = g_u0_rows + du0;
+}
+
+}  // namespace fcr

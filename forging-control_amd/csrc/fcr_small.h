@@ -22,6 +22,92 @@
 
 namespace fcr {
 
+// Cross-workgroup hand-off of the layer-pipelined kernels (fcr_pipe.h), the R1 form of cdna_hip_programming.md Guideline 16
+// (MI355X_MICROARCH.md § visibility, table row 1): every handed-off byte is stored write-through (sc1) by the wave that
+// owns it; every storing wave drains its stores (s_waitcnt vmcnt(0)) before a workgroup barrier, after which ONE lane
+// raises the workgroup's progress counter (an sc1 store); a consumer polls that one word relaxed and reads the payload
+// with sc1 loads only, so no release or acquire fence (an L2 write-back / L1 invalidate, 1.7-6.5 us each) is needed.
+// Polls are bounded (kPipeSpin, ~0.3 s): a partner that never arrives cannot hang the kernel — the first wait that gives
+// up raises the group's abort word, after which every wait of the group returns at once, so the launch drains in about
+// one bound (its outputs are then wrong, which the parity tests see).
+constexpr int kPipeFlags = 32;     // words per group (128 B): progress counters, the abort word last
+constexpr int kPipeAbort = kPipeFlags - 1;
+constexpr int kPipeSpin = 1 << 20;
+constexpr int kSc1 = 16;           // aux cache bits of a raw buffer access: sc1 (write-through store / L1-bypassing load)
+__device__ __forceinline__ void pipe_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void pipe_signal(unsigned *f, unsigned v) {   // after the barrier that follows every drain
+    if (threadIdx.x == 0) __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void pipe_wait(unsigned *blk, const unsigned *f, unsigned need) {
+    for (int s = 0;; ++s) {
+        if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >= need) break;
+        if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(blk + kPipeAbort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+            break;
+        if (s == kPipeSpin) {
+            if ((threadIdx.x & 63) == 0) __hip_atomic_store(blk + kPipeAbort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // no instruction: keeps the payload loads below the poll
+}
+// sc1 record accesses in the compact record layout (store_quads): quad k of the record, or all of it
+template <int HS, int k>
+__device__ __forceinline__ void st_quad_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off, const float (&v)[HS], int lane) {
+    constexpr int n = quad_n<HS, k>();
+    const uint32_t vo = quad_voff<HS, k>(lane), so = off + quad_soff<HS, k>();
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    if constexpr (n == 4) {
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{__builtin_bit_cast(unsigned, v[4 * k]), __builtin_bit_cast(unsigned, v[4 * k + 1]),
+                                                     __builtin_bit_cast(unsigned, v[4 * k + 2]), __builtin_bit_cast(unsigned, v[4 * k + 3])},
+                                               r, (int)vo, (int)so, kSc1);
+    } else if constexpr (n == 2) {
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{__builtin_bit_cast(unsigned, v[4 * k]), __builtin_bit_cast(unsigned, v[4 * k + 1])},
+                                              r, (int)vo, (int)so, kSc1);
+    } else {
+        static_assert(n == 1, "the pipelined tiers: HS = 8, 13 (tail of 0 or 1 slot)");
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v[4 * k]), r, (int)vo, (int)so, kSc1);
+    }
+}
+template <int HS, int k = 0>
+__device__ __forceinline__ void ld_rec_sc1(f32x4 (&dst)[Geo<HS>::HQ], __amdgpu_buffer_rsrc_t r, uint32_t off, int lane) {
+    if constexpr (k < Geo<HS>::HQ) {
+        constexpr int n = quad_n<HS, k>();
+        const uint32_t vo = quad_voff<HS, k>(lane), so = off + quad_soff<HS, k>();
+        if constexpr (n == 4) {
+            dst[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)vo, (int)so, kSc1));
+        } else {
+            static_assert(n == 1, "the pipelined tiers: HS = 8, 13 (tail of 0 or 1 slot)");
+            f32x4 q = {0.0f, 0.0f, 0.0f, 0.0f};
+            q[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)vo, (int)so, kSc1));
+            dst[k] = q;
+        }
+        ld_rec_sc1<HS, k + 1>(dst, r, off, lane);
+    }
+}
+template <int HS, int k>
+__device__ __forceinline__ void ld_quad_sc1(f32x4 (&dst)[Geo<HS>::HQ], __amdgpu_buffer_rsrc_t r, uint32_t off, int lane) {
+    constexpr int n = quad_n<HS, k>();
+    const uint32_t vo = quad_voff<HS, k>(lane), so = off + quad_soff<HS, k>();
+    if constexpr (n == 4) {
+        dst[k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)vo, (int)so, kSc1));
+    } else {
+        static_assert(n == 1, "the pipelined tiers: HS = 8, 13 (tail of 0 or 1 slot)");
+        f32x4 q = {0.0f, 0.0f, 0.0f, 0.0f};
+        q[0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)vo, (int)so, kSc1));
+        dst[k] = q;
+    }
+}
+__device__ __forceinline__ void buf_st2_sc1(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, f32x2 v) {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, (int)voff, (int)soff, kSc1);
+}
+__device__ __forceinline__ f32x2 buf_ld2_sc1(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, (int)soff, kSc1));
+}
+
+
 template <int HS>
 struct Small {
     static constexpr int NQ = (HS + 3) / 4;                       // waves per workgroup = record quads
@@ -355,13 +441,17 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
 // Partial products of one cell -> the sums this wave needs: dh_prev of its slots (L0: combined slots σ =
 // s; else σ = HS + s), dx of its slots (layers >= 1: σ = s, into its dseq quad) and, for L0, the window
 // columns σ = HS, HS+1 (every wave: the row gradients feed each wave's window head).
-template <int HS, bool L0, int W>
+// PUB (the layer-pipelined backward): after the first barrier — which every wave reached after draining its stores of
+// the previous cell (wait_din_after) — one lane signals that cell's outputs: *pub = pub_v
+template <int HS, bool L0, int W, bool PUB = false>
 __device__ __forceinline__ void small_reduce(f32x4 *red, const f32x4 (&part)[Small<HS>::NB], int lane, float (&dh)[HS],
-                                             float (&dxo)[HS], float &dxq, float &dx4) {
+                                             float (&dxo)[HS], float &dxq, float &dx4, unsigned *pub = nullptr,
+                                             unsigned pub_v = 0) {
     using Q = QR<HS, W>;
     constexpr int NQ = Small<HS>::NQ, NB = Small<HS>::NB;
     constexpr int NBL = Img<HS, L0>::NB;
     asm volatile("s_barrier" ::: "memory");   // every wave has read the previous cell's partials
+    if constexpr (PUB) pipe_signal(pub, pub_v);
 #pragma unroll
     for (int tau = 0; tau < NBL; ++tau) red[(W * NB + tau) * kWave + lane] = part[tau];
     lds_barrier();
@@ -569,7 +659,9 @@ __device__ __forceinline__ f32x4 sb_ttile(const TFrag<HS, L0, R0, R1> &f, const 
     return acc;
 }
 
-template <int HS>
+// PIPE (fcr_pipe.h): one workgroup per (group, layer), so the cell after (j, l, 0) is (j - 1, l, 9), the din of a cell
+// is waited for on the layer above's counters, and each cell's outputs are published on this wave's counter
+template <int HS, bool PIPE = false>
 struct SbCtx {
     NextIn nb;                        // this group's slab descriptors
     f32x4 *dseq_w;                    // this group's dseq
@@ -583,20 +675,34 @@ struct SbCtx {
         return (uint32_t)(((size_t)(j * kLayers + l) * kL + t) * Geo<HS>::QC * 16);
     }
     __device__ size_t doff(int j, int lfrom, int t) const { return ((size_t)(j * 2 + (2 - lfrom)) * kL + t) * Geo<HS>::QC; }
+    unsigned *flags;                  // PIPE: this group's counters (kPipeFlags)
+    int fl_own, fl_above;             // PIPE: index of this workgroup's counter, of the layer above's (or -1)
     __device__ NextIn next_of(int j, int l, int t) const {   // the cell processed after (j, l, t)
         NextIn n = nb;
         int nj = j, nl = l, nt = t - 1;
         if (t == 0) {
             nt = kL - 1;
-            nl = l - 1;
-            if (l == 0) { nl = 2; nj = j - 1; }
+            nl = PIPE ? l : l - 1;
+            if (PIPE || l == 0) { nl = PIPE ? l : 2; nj = j - 1; }
         }
-        if (nj < 0) { nj = 0; nl = 2; nt = 9; }   // past the last cell: a valid one (harmless)
+        if (nj < 0) { nj = 0; nl = PIPE ? l : 2; nt = 9; }   // past the last cell: a valid one (harmless)
         n.x = nl == 0 ? (uint32_t)((nj * kL + nt) * kWave * 8) : hoff(nj, nl > 0 ? nl - 1 : 0, nt);
         n.h = hoff(nj, nl, nt > 0 ? nt - 1 : 0);
         n.c = n.h;
         n.d = (uint32_t)((nl < 2 ? doff(nj, nl + 1, nt) : 0) * 16);
         return n;
+    }
+    // PIPE: a layer workgroup's progress counter after cell (j, t) (windows N-1 .. 0, t = 9 .. 0)
+    __device__ unsigned done_after(int j, int t) const { return (unsigned)((N - 1 - j) * kL + (kL - 1 - t) + 1); }
+    // PIPE, in cell (j, t) before loading the din of the cell after it: this wave's stores of the previous cell are
+    // drained (they are signalled at this cell's first reduction barrier), and the layer above has published that din
+    __device__ void wait_din_after(int j, int t) const {
+        if constexpr (PIPE) {
+            pipe_drain();
+            int nj = j, nt = t - 1;
+            if (t == 0) { nj = j - 1; nt = kL - 1; }
+            if (nj >= 0 && fl_above >= 0) pipe_wait(flags, flags + fl_above, done_after(nj, nt));
+        }
     }
 };
 
@@ -605,10 +711,13 @@ template <int HS, bool NX_L0, bool NX_HC>
 __device__ __forceinline__ void sb_load_a(CellIn<HS> &ci, const NextIn &n, int lane) {
     load_xhd<HS, NX_L0, NX_HC, false>(ci, n, lane);
 }
-template <int HS, int W, bool NX_HC, bool NX_DIN>
+template <int HS, int W, bool NX_HC, bool NX_DIN, bool PIPE = false>
 __device__ __forceinline__ void sb_load_b(CellIn<HS> &ci, const NextIn &n, int lane) {
     if (NX_HC) ld_quad<HS, W>(ci.c, n.rc, n.c, lane);
-    if (NX_DIN) ld_quad<HS, W>(ci.d, n.rd, n.d, lane);
+    if (NX_DIN) {   // PIPE: another workgroup's record (sc1 load, the hand-off above)
+        if constexpr (PIPE) ld_quad_sc1<HS, W>(ci.d, n.rd, n.d, lane);
+        else ld_quad<HS, W>(ci.d, n.rd, n.d, lane);
+    }
 }
 
 // One pipeline step of layer LAYER at cell t (t = 9 .. 0), in chunks that pair independent work so the
@@ -620,8 +729,8 @@ __device__ __forceinline__ void sb_load_b(CellIn<HS> &ci, const NextIn &n, int l
 //   then the reduction of cell t and this wave's stores. Loads: B's next inputs (c, din of the cell after
 //   t) after region 1, A's (x, h of the cell after t-2) after region 2 — a step ahead of their use.
 template <int HS, int LAYER, int W, bool FB, bool DO_A, bool FA, bool DO_S, bool FS, bool S_NX_L0, bool S_NX_HC,
-          bool B_NX_HC, bool B_NX_DIN>
-__device__ __forceinline__ void sb_step(const SbCtx<HS> &x, int j, int t, const float (&ext)[HS], CellIn<HS> &ci,
+          bool B_NX_HC, bool B_NX_DIN, bool PIPE>
+__device__ __forceinline__ void sb_step(const SbCtx<HS, PIPE> &x, int j, int t, const float (&ext)[HS], CellIn<HS> &ci,
                                         f32x4 (&G)[4], AOps<HS, LAYER == 0> &ops, float (&dh)[HS], float (&dc)[HS]) {
     using Q = QR<HS, W>;
     constexpr int R0 = Q::R0, R1 = Q::R1, NS = R1 - R0;
@@ -654,7 +763,8 @@ __device__ __forceinline__ void sb_step(const SbCtx<HS> &x, int j, int t, const 
         }
     }
     sched_fence();
-    sb_load_b<HS, W, B_NX_HC, B_NX_DIN>(ci, x.next_of(j, LAYER, t), x.lane);
+    x.wait_din_after(j, t);   // (PIPE only; the drain also for a cell with no din to wait for)
+    sb_load_b<HS, W, B_NX_HC, B_NX_DIN, PIPE>(ci, x.next_of(j, LAYER, t), x.lane);
     const unsigned long long s1 = stamp_now();
     // ---- region 2 ----
     TFrag<HS, L0, R0, R1> tf[2];
@@ -696,7 +806,9 @@ __device__ __forceinline__ void sb_step(const SbCtx<HS> &x, int j, int t, const 
 #pragma unroll
     for (int tau = 0; tau < NB; ++tau) part[tau] = acc[tau] * sc.down;
     float dxo[HS], dxq = 0.0f, dx4 = 0.0f;
-    small_reduce<HS, L0, W>(x.red, part, x.lane, dh, dxo, dxq, dx4);
+    // PIPE: signal the previous cell (done_after(j, t) - 1, this workgroup's order) at the first reduction barrier
+    small_reduce<HS, L0, W, PIPE>(x.red, part, x.lane, dh, dxo, dxq, dx4, PIPE ? x.flags + x.fl_own : nullptr,
+                                  PIPE ? x.done_after(j, t) - 1 : 0u);
     if (FCR_STAMP) {
         const unsigned long long s3 = stamp_now();
         x.sp->t[0] += s1 - s0;
@@ -704,16 +816,24 @@ __device__ __forceinline__ void sb_step(const SbCtx<HS> &x, int j, int t, const 
         x.sp->t[2] += s3 - s2;
         x.sp->t[3] += 1;
     }
-    if (L0) buf_st2(x.rr, x.lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{dxq * x.scq, dx4 * x.sc4});   // row j+t
-    else store_quad<HS, W>(x.dseq_w + x.doff(j, LAYER, t), dxo, x.lane);
+    // this cell's outputs: the window-row gradients (layer 0) or the din of the layer below; PIPE: write-through, they
+    // are another workgroup's inputs (signalled at the next cell's first reduction barrier)
+    if constexpr (PIPE) {
+        if (L0) buf_st2_sc1(x.rr, x.lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{dxq * x.scq, dx4 * x.sc4});
+        else st_quad_sc1<HS, W>(x.nb.rd, (uint32_t)(x.doff(j, LAYER, t) * 16), dxo, x.lane);
+    } else {
+        if (L0) buf_st2(x.rr, x.lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{dxq * x.scq, dx4 * x.sc4});   // row j+t
+        else store_quad<HS, W>(x.dseq_w + x.doff(j, LAYER, t), dxo, x.lane);
+    }
 }
 
-template <int HS, int LAYER, int W>
-__device__ __forceinline__ void sb_phase(const SbCtx<HS> &x, int j, const float (&dh_out)[HS], CellIn<HS> &ci,
+template <int HS, int LAYER, int W, bool PIPE = false>
+__device__ __forceinline__ void sb_phase(const SbCtx<HS, PIPE> &x, int j, const float (&dh_out)[HS], CellIn<HS> &ci,
                                          float (&dh)[HS], float (&dc)[HS]) {
     using Q = QR<HS, W>;
     constexpr bool L0 = LAYER == 0, DIN = LAYER < 2;
-    constexpr bool NEXT_L0 = LAYER == 1, NEXT_DIN = LAYER >= 1;   // the next phase's first cell
+    // the next phase's first cell: (j, LAYER - 1, 9), or (j - 1, 2, 9) after layer 0; PIPE: (j - 1, LAYER, 9)
+    constexpr bool NEXT_L0 = PIPE ? L0 : LAYER == 1, NEXT_DIN = PIPE ? DIN : LAYER >= 1;
     float zero[HS];
 #pragma unroll
     for (int r = 0; r < HS; ++r) zero[r] = 0.0f;
@@ -734,15 +854,16 @@ __device__ __forceinline__ void sb_phase(const SbCtx<HS> &x, int j, const float 
     sb_split<HS, L0, false>(ci, ops);
     sb_load_a<HS, L0, true>(ci, x.next_of(j, LAYER, kL - 2), x.lane);
     if (FCR_STAMP) x.sp->t[6] += stamp_now() - p0;
-    //      <HS, LAYER, W, FB,   DO_A, FA,   DO_S, FS,   S_NX_L0, S_NX_HC, B_NX_HC, B_NX_DIN>
-    sb_step<HS, LAYER, W, false, true, false, true, false, L0, true, true, DIN>(x, j, kL - 1, LAYER == 2 ? dh_out : zero, ci,
-                                                                             G, ops, dh, dc);
+    //      <HS, LAYER, W, FB,   DO_A, FA,   DO_S, FS,   S_NX_L0, S_NX_HC, B_NX_HC, B_NX_DIN, PIPE>
+    sb_step<HS, LAYER, W, false, true, false, true, false, L0, true, true, DIN, PIPE>(x, j, kL - 1, LAYER == 2 ? dh_out : zero,
+                                                                                   ci, G, ops, dh, dc);
     for (int t = kL - 2; t >= 4; --t)
-        sb_step<HS, LAYER, W, false, true, false, true, false, L0, true, true, DIN>(x, j, t, zero, ci, G, ops, dh, dc);
-    sb_step<HS, LAYER, W, false, true, false, true, false, L0, false, true, DIN>(x, j, 3, zero, ci, G, ops, dh, dc);
-    sb_step<HS, LAYER, W, false, true, false, true, true, NEXT_L0, true, true, DIN>(x, j, 2, zero, ci, G, ops, dh, dc);
-    sb_step<HS, LAYER, W, false, true, true, false, false, false, false, false, DIN>(x, j, 1, zero, ci, G, ops, dh, dc);
-    sb_step<HS, LAYER, W, true, false, false, false, false, false, false, true, NEXT_DIN>(x, j, 0, zero, ci, G, ops, dh, dc);
+        sb_step<HS, LAYER, W, false, true, false, true, false, L0, true, true, DIN, PIPE>(x, j, t, zero, ci, G, ops, dh, dc);
+    sb_step<HS, LAYER, W, false, true, false, true, false, L0, false, true, DIN, PIPE>(x, j, 3, zero, ci, G, ops, dh, dc);
+    sb_step<HS, LAYER, W, false, true, false, true, true, NEXT_L0, true, true, DIN, PIPE>(x, j, 2, zero, ci, G, ops, dh, dc);
+    sb_step<HS, LAYER, W, false, true, true, false, false, false, false, false, DIN, PIPE>(x, j, 1, zero, ci, G, ops, dh, dc);
+    sb_step<HS, LAYER, W, true, false, false, false, false, false, false, true, NEXT_DIN, PIPE>(x, j, 0, zero, ci, G, ops, dh,
+                                                                                              dc);
 }
 
 template <int HS>

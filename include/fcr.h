@@ -257,6 +257,13 @@ int fcr_lstm_backward(const fcr_dims *dims, const fcr_weights *w, const float *d
 int fcr_set_small_batch_limit(int32_t max_batch);
 int fcr_get_small_batch_limit(void);
 
+/* Within the small-batch family, B <= max_batch (and at most 32 groups of 16 trajectories, 3 workgroups each within
+ * half the device's CUs) runs the layer-pipelined geometry (csrc/fcr_pipe.h: one workgroup per LSTM layer, the layers
+ * and windows as a wavefront; results bit-identical to the one-workgroup-per-group kernels). Default 512; 0 = never.
+ * Process-wide; returns the previous value; fcr_get_small_pipe_limit reads it. */
+int fcr_set_small_pipe_limit(int32_t max_batch);
+int fcr_get_small_pipe_limit(void);
+
 /*
  * H > 52 (the batch-wide GEMM path): how many bytes of "kept windows" fcr_workspace_size(with_backward = 1)
  * may add. The backward recomputes each window's cells from a per-window checkpoint (the rollout's memory

@@ -10,5 +10,5 @@ mkdir -p "$out"
 for f in fcr_abi fcr_rows; do
   /opt/rocm/bin/hipcc -O3 -fno-slp-vectorize --offload-arch=gfx950 -std=c++17 --cuda-device-only -S \
     -I "$root/include" -I "$src" "$@" "$src/$f.hip" -o "$out/$f.s"
-  grep -v -E '^\s*(;|//)|\.ident|^\s*$|__hip_cuid_' "$out/$f.s" | sed -e 's/\s*;.*$//' > "$out/$f.clean.s"
+  grep -v -E '^\s*(;|//)|\.ident|^\s*$|__hip_cuid_' "$out/$f.s" | sed -e 's/\s*;.*$//' -e 's/\.LBB[0-9]*_/.LBB_/g' -e 's/post_getpc[0-9]*/post_getpc/g' > "$out/$f.clean.s"
 done
