@@ -48,6 +48,21 @@ for name in KERNELS:
     ins = rows("inst")
     for cnt in ("SQ_INSTS_VALU_MFMA_F16", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_WAVES", "GRBM_GUI_ACTIVE"):
         d[cnt + "_per_launch"] = per_launch(ins, name, cnt)[0]
+    wt = rows("wait")   # the issue / wait split (MI355X_MICROARCH.md PMC: the three SQ_*ANY buckets are disjoint)
+    for cnt in ("SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY",
+                "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VMEM"):
+        d[cnt + "_per_launch"] = per_launch(wt, name, cnt)[0]
+    wc = d["SQ_WAVE_CYCLES_per_launch"]
+    if wc:
+        for cnt, key in (("SQ_ACTIVE_INST_ANY", "issue"), ("SQ_ACTIVE_INST_VALU", "issue_valu"),
+                         ("SQ_WAIT_INST_ANY", "issue_wait"), ("SQ_WAIT_ANY", "waitcnt_barrier")):
+            d["share_" + key] = d[cnt + "_per_launch"] / wc
+        # two waves per SIMD (8-wave workgroups, one per CU): the SIMD's vector issue busy = 2 x a wave's share
+        d["simd_valu_issue_busy"] = 2 * d["share_issue_valu"]
+    g = per_launch(wt, name, "GRBM_GUI_ACTIVE")[0]
+    if g and d.get("SQ_VALU_MFMA_BUSY_CYCLES_per_launch"):
+        # cycles the matrix pipe of a SIMD is busy over the kernel's cycles (GRBM_GUI_ACTIVE sums the 8 XCDs)
+        d["simd_mfma_busy"] = d["SQ_VALU_MFMA_BUSY_CYCLES_per_launch"] / (1024 * g / 8)
     m = d["SQ_INSTS_VALU_MFMA_F16_per_launch"]
     if m:
         d["mfma_per_wave_cell"] = m / (WAVES * N * L * LAYERS)
@@ -68,11 +83,16 @@ for name in KERNELS:
     if d.get("GRBM_GUI_ACTIVE_per_launch") and d.get("rocprof_avg_ms"):
         # MI355X_MICROARCH.md DVFS: clock ~ GRBM_GUI_ACTIVE / 8 XCDs / kernel time
         d["clock_ghz_est"] = d["GRBM_GUI_ACTIVE_per_launch"] / 8 / (d["rocprof_avg_ms"] * 1e-3) / 1e9
+    if d.get("hbm_bytes_corrected") and d.get("rocprof_avg_ms"):
+        d["hbm_tb_per_s"] = d["hbm_bytes_corrected"] / (d["rocprof_avg_ms"] * 1e-3) / 1e12
     if d.get("mfma_flop_per_launch") and d.get("rocprof_avg_ms"):
         d["mfma_tflops_executed"] = d["mfma_flop_per_launch"] / (d["rocprof_avg_ms"] * 1e-3) / 1e12
 out["_note"] = (f"rocprofv3 PMC passes of bench.py B={B} N={N} H=50 {args.precision} (scripts/profile.sh): FETCH_SIZE and "
                 "WRITE_SIZE in separate passes, KB; hbm_bytes_corrected = 2*FETCH (gfx950 reports half of wide "
                 "coalesced reads, MI355X_MICROARCH.md HBM) + WRITE. Instruction counts are wave-instructions per "
-                "launch; per wave-cell = / (B/16 waves * N windows * 10 steps * 3 layers).")
+                "launch; per wave-cell = / (B/16 waves * N windows * 10 steps * 3 layers). share_* = SQ_ACTIVE_INST_ANY / "
+                "SQ_ACTIVE_INST_VALU / SQ_WAIT_INST_ANY / SQ_WAIT_ANY over SQ_WAVE_CYCLES (per wave); simd_valu_issue_busy = "
+                "2 waves per SIMD x share_issue_valu; simd_mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x "
+                "GRBM_GUI_ACTIVE / 8).")
 json.dump(out, open(f"profiles/{tag}_pmc.json", "w"), indent=1)
 print(json.dumps(out, indent=1))

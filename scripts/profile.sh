@@ -38,7 +38,8 @@ timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o $TAG -- $SHORT > $O/write.log 2>&1
 case $CFG in
   c5*) timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_F16 SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE --output-format csv -d $O/inst -o $TAG -- $SHORT > $O/inst.log 2>&1 ;;
-  *) timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_F16 SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $O/inst -o $TAG -- $SHORT > $O/inst.log 2>&1 ;;
+  *) timeout -s KILL 200 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_F16 SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $O/inst -o $TAG -- $SHORT > $O/inst.log 2>&1
+     timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VMEM GRBM_GUI_ACTIVE --output-format csv -d $O/wait -o $TAG -- $SHORT > $O/wait.log 2>&1 ;;
 esac
 echo pmc ok
 cd $R
