@@ -273,7 +273,8 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
         pipe_signal(fl + P::F1, (unsigned)NC);
         return;
     }
-    const float cost = tot_sum / (float)N;                             // Functions.py:1458-1460
+    // every wait of the chain ends at this workgroup: a timed-out one anywhere shows as NaN cost and loss
+    const float cost = pipe_aborted(fl) ? __builtin_nanf("") : tot_sum / (float)N;   // Functions.py:1458-1460
     if (lead && valid && q == 0) {
         a.cost[b] = cost;
         a.command[b] = cmd_sum / (float)N;
@@ -437,7 +438,8 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pbwd_kernel(BwdA
     const float g_u0_rows = row_grad(kL - 1)[1];   // row 9, col 4 = u0 (Functions.py:1396)
     float du0 = 2.0f * alpha * wgt * (pred[0] - s84);
     if (N > 1) du0 += 2.0f * alpha * wgt * (pred[0] - pred[1]);
-    if (lead && valid && q == 0) a.g_u0[b] = g_u0_rows + du0;
+    // layer 0 ends the chain: a timed-out wait anywhere shows as NaN gradients
+    if (lead && valid && q == 0) a.g_u0[b] = pipe_aborted(fl) ? __builtin_nanf("") : g_u0_rows + du0;
 }
 
 }  // namespace fcr

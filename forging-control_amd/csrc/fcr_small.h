@@ -38,6 +38,10 @@ __device__ __forceinline__ void pipe_drain() { asm volatile("s_waitcnt vmcnt(0)"
 __device__ __forceinline__ void pipe_signal(unsigned *f, unsigned v) {   // after the barrier that follows every drain
     if (threadIdx.x == 0) __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// a wait of this launch timed out (its partner workgroup was not resident): the outputs are then poisoned with NaN
+__device__ __forceinline__ bool pipe_aborted(const unsigned *blk) {
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(blk + kPipeAbort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u;
+}
 __device__ __forceinline__ void pipe_wait(unsigned *blk, const unsigned *f, unsigned need) {
     for (int s = 0;; ++s) {
         if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >= need) break;
