@@ -34,7 +34,8 @@ def _with_pipe_limit(lim, fn):
         native.set_small_pipe_limit(prev)
 
 
-@pytest.mark.parametrize("H,B,N", [(50, 15, 10), (50, 1, 5), (32, 45, 4), (50, 256, 10), (50, 512, 3), (40, 37, 25)])
+@pytest.mark.parametrize("H,B,N", [(50, 15, 10), (50, 1, 5), (32, 45, 4), (50, 256, 10), (50, 512, 3), (40, 37, 25),
+                                   (50, 7, 1), (50, 16, 2), (50, 17, 2), (24, 100, 3)])
 def test_layer_pipelined_small_kernels_meet_oracle_and_match_one_workgroup(H, B, N):
     from tests.golden.make_golden import synth_params
     params = load_case("ref_b15_n10")[1] if H == 50 else synth_params(H, 700 + H)
