@@ -28,7 +28,8 @@ ERRORS = {-1: "FCR_EINVAL", -2: "FCR_EWORKSPACE", -3: "FCR_EHIP", -4: "FCR_EUNSU
 EXPORTS = ("fcr_workspace_size", "fcr_wide_kept_windows", "fcr_forward", "fcr_backward", "fcr_lstm_workspace_size",
            "fcr_lstm_forward", "fcr_lstm_backward", "fcr_plant_rk4", "fcr_closed_loop_run", "fcr_window_gather",
            "fcr_fnn_workspace_size", "fcr_fnn_forward", "fcr_fnn_backward", "fcr_set_small_batch_limit",
-           "fcr_get_small_batch_limit", "fcr_set_small_pipe_limit", "fcr_get_small_pipe_limit", "fcr_set_wide_keep_budget", "fcr_get_wide_keep_budget", "fcr_last_error",
+           "fcr_get_small_batch_limit", "fcr_set_small_pipe_limit", "fcr_get_small_pipe_limit", "fcr_set_small_pipe_sets",
+           "fcr_get_small_pipe_sets", "fcr_set_wide_keep_budget", "fcr_get_wide_keep_budget", "fcr_last_error",
            "fcr_abi_version", "fcr_wide_bwd_cell_workspace", "fcr_wide_bwd_cell")
 OPT_INHERIT, KEEP_AUTO = -2, -1
 INT32_MAX, INT64_MAX = 2**31 - 1, 2**63 - 1
@@ -150,6 +151,10 @@ def load() -> ctypes.CDLL:
         lib.fcr_set_small_pipe_limit.restype = i32
         lib.fcr_get_small_pipe_limit.argtypes = []
         lib.fcr_get_small_pipe_limit.restype = i32
+        lib.fcr_set_small_pipe_sets.argtypes = [i32]
+        lib.fcr_set_small_pipe_sets.restype = i32
+        lib.fcr_get_small_pipe_sets.argtypes = []
+        lib.fcr_get_small_pipe_sets.restype = i32
         lib.fcr_set_wide_keep_budget.argtypes = [ctypes.c_int64]
         lib.fcr_set_wide_keep_budget.restype = ctypes.c_int64
         lib.fcr_get_wide_keep_budget.argtypes = []
@@ -194,6 +199,17 @@ def set_small_pipe_limit(max_batch: int) -> int:
 def small_pipe_limit() -> int:
     """The process-wide layer-pipelined small-batch limit (fcr_get_small_pipe_limit: read-only)."""
     return int(load().fcr_get_small_pipe_limit())
+
+
+def set_small_pipe_sets(sets: int) -> int:
+    """fcr_set_small_pipe_sets: the pipelined geometry's window sets (1..3; 0 = the most that fit); process-wide;
+    returns the old value. Results are bit-identical for every value."""
+    return int(load().fcr_set_small_pipe_sets(int(sets)))
+
+
+def small_pipe_sets() -> int:
+    """The process-wide window-set setting (fcr_get_small_pipe_sets: read-only; 0 = automatic)."""
+    return int(load().fcr_get_small_pipe_sets())
 
 
 def set_wide_keep_budget(nbytes: int) -> int:

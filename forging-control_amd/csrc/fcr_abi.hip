@@ -253,6 +253,16 @@ bool use_pipe(const fcr_dims *d, const Layout &L, const fcr_options *o) {
     return use_small(d, L, o) && d->B <= g_pipe_max_batch.load(std::memory_order_relaxed) && L.nw <= kPipeMaxGroups &&
            6 * L.nw <= device_cus();
 }
+// window sets per group (fcr_pipe.h): up to 3, as many as fit 3 S workgroups per group within half the CUs and
+// S <= N; g_pipe_sets > 0 fixes it (tests: every S gives the same bits)
+std::atomic<int> g_pipe_sets{0};
+int pipe_sets(const fcr_dims *d, const Layout &L) {
+    const int fixed = g_pipe_sets.load(std::memory_order_relaxed);
+    int S = fixed > 0 ? fixed : Pipe<13>::MAX_SETS;
+    const int cus = device_cus();
+    while (S > 1 && (6 * S * L.nw > cus || S > d->N)) --S;
+    return S;
+}
 PipeArgs pipe_args(const Layout &L, char *base) {
     PipeArgs p;
     p.flags = (unsigned *)(base + L.pipe_flags);
@@ -264,24 +274,38 @@ int pipe_clear(const PipeArgs &pa, const Layout &L, hipStream_t s) {
     hipLaunchKernelGGL(fcr_pipe_clear_kernel, dim3(1), dim3(kWave), 0, s, pa.flags, L.nw * kPipeFlags);
     return launch_check("fcr_pipe_clear_kernel");
 }
-template <int HS, bool STORE>
+// grid: 3 S workgroups per group, the ids of a group one residue mod 8 apart (pipe_role)
+template <int HS, bool STORE, int S>
 int launch_pfwd_t(const FwdArgs &fa, const PipeArgs &pa, const Layout &L, hipStream_t s) {
     constexpr int lds = Pipe<HS>::LDS_FWD;
     static std::atomic<unsigned long long> attr_done{0};
-    if (const int rc = lds_attr((const void *)fcr_pfwd_kernel<HS, STORE>, lds, attr_done, "pfwd")) return rc;
+    if (const int rc = lds_attr((const void *)fcr_pfwd_kernel<HS, STORE, S>, lds, attr_done, "pfwd")) return rc;
     if (const int rc = pipe_clear(pa, L, s)) return rc;
-    hipLaunchKernelGGL((fcr_pfwd_kernel<HS, STORE>), dim3(24 * ((L.nw + 7) / 8)), dim3(Small<HS>::NQ * kWave), lds, s, fa,
-                       pa);
+    hipLaunchKernelGGL((fcr_pfwd_kernel<HS, STORE, S>), dim3(24 * S * ((L.nw + 7) / 8)), dim3(Small<HS>::NQ * kWave), lds,
+                       s, fa, pa);
     return launch_check("fcr_pfwd_kernel");
 }
-template <int HS>
+template <int HS, bool STORE>
+int launch_pfwd_s(const FwdArgs &fa, const PipeArgs &pa, const Layout &L, int S, hipStream_t s) {
+    if (S == 3) return launch_pfwd_t<HS, STORE, 3>(fa, pa, L, s);
+    if (S == 2) return launch_pfwd_t<HS, STORE, 2>(fa, pa, L, s);
+    return launch_pfwd_t<HS, STORE, 1>(fa, pa, L, s);
+}
+template <int HS, int S>
 int launch_pbwd_t(const BwdArgs &ba, const PipeArgs &pa, const Layout &L, hipStream_t s) {
     constexpr int lds = Pipe<HS>::LDS_BWD;
     static std::atomic<unsigned long long> attr_done{0};
-    if (const int rc = lds_attr((const void *)fcr_pbwd_kernel<HS>, lds, attr_done, "pbwd")) return rc;
+    if (const int rc = lds_attr((const void *)fcr_pbwd_kernel<HS, S>, lds, attr_done, "pbwd")) return rc;
     if (const int rc = pipe_clear(pa, L, s)) return rc;
-    hipLaunchKernelGGL((fcr_pbwd_kernel<HS>), dim3(24 * ((L.nw + 7) / 8)), dim3(Small<HS>::NQ * kWave), lds, s, ba, pa);
+    hipLaunchKernelGGL((fcr_pbwd_kernel<HS, S>), dim3(24 * S * ((L.nw + 7) / 8)), dim3(Small<HS>::NQ * kWave), lds, s, ba,
+                       pa);
     return launch_check("fcr_pbwd_kernel");
+}
+template <int HS>
+int launch_pbwd_s(const BwdArgs &ba, const PipeArgs &pa, const Layout &L, int S, hipStream_t s) {
+    if (S == 3) return launch_pbwd_t<HS, 3>(ba, pa, L, s);
+    if (S == 2) return launch_pbwd_t<HS, 2>(ba, pa, L, s);
+    return launch_pbwd_t<HS, 1>(ba, pa, L, s);
 }
 
 template <int HS, bool STORE>
@@ -1377,6 +1401,10 @@ int fcr_set_small_batch_limit(int32_t max_batch) {
 int fcr_get_small_batch_limit(void) { return g_small_max_batch.load(); }
 int fcr_set_small_pipe_limit(int32_t max_batch) { return g_pipe_max_batch.exchange(max_batch < 0 ? 0 : max_batch); }
 int fcr_get_small_pipe_limit(void) { return g_pipe_max_batch.load(); }
+int fcr_set_small_pipe_sets(int32_t sets) {
+    return g_pipe_sets.exchange(sets < 0 ? 0 : (sets > Pipe<13>::MAX_SETS ? Pipe<13>::MAX_SETS : sets));
+}
+int fcr_get_small_pipe_sets(void) { return g_pipe_sets.load(); }
 
 int64_t fcr_set_wide_keep_budget(int64_t bytes) {
     return g_wide_keep_budget.exchange(bytes < 0 ? -1 : bytes);
@@ -1531,8 +1559,9 @@ int fcr_forward(const fcr_dims *d, fcr_options *opts, const fcr_weights *w, cons
     note_kernels(opts, small ? FCR_KERNELS_SMALL : FCR_KERNELS_FUSED);
     if (small && use_pipe(d, L, opts)) {
         const PipeArgs pa = pipe_args(L, base);
-        if (L.HS == 8) rc = with_backward ? launch_pfwd_t<8, true>(fa, pa, L, s) : launch_pfwd_t<8, false>(fa, pa, L, s);
-        else rc = with_backward ? launch_pfwd_t<13, true>(fa, pa, L, s) : launch_pfwd_t<13, false>(fa, pa, L, s);
+        const int S = pipe_sets(d, L);
+        if (L.HS == 8) rc = with_backward ? launch_pfwd_s<8, true>(fa, pa, L, S, s) : launch_pfwd_s<8, false>(fa, pa, L, S, s);
+        else rc = with_backward ? launch_pfwd_s<13, true>(fa, pa, L, S, s) : launch_pfwd_s<13, false>(fa, pa, L, S, s);
     } else if (small) {
         if (L.HS == 8) rc = with_backward ? launch_sfwd_t<8, true>(fa, L, s) : launch_sfwd_t<8, false>(fa, L, s);
         else rc = with_backward ? launch_sfwd_t<13, true>(fa, L, s) : launch_sfwd_t<13, false>(fa, L, s);
@@ -1596,7 +1625,8 @@ int fcr_backward(const fcr_dims *d, fcr_options *opts, const float *X, const flo
     note_kernels(opts, small ? FCR_KERNELS_SMALL : FCR_KERNELS_FUSED);
     if (small && use_pipe(d, L, opts)) {
         const PipeArgs pa = pipe_args(L, base);
-        rc = L.HS == 8 ? launch_pbwd_t<8>(ba, pa, L, s) : launch_pbwd_t<13>(ba, pa, L, s);
+        const int S = pipe_sets(d, L);
+        rc = L.HS == 8 ? launch_pbwd_s<8>(ba, pa, L, S, s) : launch_pbwd_s<13>(ba, pa, L, S, s);
     } else if (small) {
         rc = L.HS == 8 ? launch_sbwd_t<8>(ba, L, s) : launch_sbwd_t<13>(ba, L, s);
     } else {

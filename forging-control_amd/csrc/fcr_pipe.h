@@ -1,21 +1,24 @@
-// fcr_pipe.h — layer-pipelined small-batch rollout (config 1: the reference trains at B = 15, UL/Main.py:84,297).
+// fcr_pipe.h — layer- and window-pipelined small-batch rollout (config 1: the reference trains at B = 15,
+// UL/Main.py:84,297).
 //
 // The small-batch kernels (fcr_small.h) give a 16-trajectory group ONE workgroup that walks every cell of the rollout
 // in sequence: per window 30 dependent cells (3 layers x 10 steps) plus two weight-image refills, in both passes. Here
-// a group gets THREE workgroups, one per LSTM layer, each holding its layer's weights resident in LDS (no refills),
-// and the layers run as a wavefront across workgroups: cell (j, l, t) needs only (j, l, t - 1) of its own workgroup
-// and, from the layer below (forward) or above (backward), the same cell's input, handed over through the sequence
-// slabs (the layout fcr_small.h / the fused kernels use) and a per-(group, layer, wave) progress counter
-// (pipe_wait / pipe_publish, fcr_small.h). Windows pipeline too: in the forward only window j's last row depends on
-// window j - 1's output (x_hat_{j-1} and the controller's u_j, handed from the layer-2 workgroup to the layer-0 one),
-// so layer 0 runs window j's cells t = 0..8 while layers 1, 2 finish window j - 1; in the backward window j - 1's head
-// needs only window j's first layer-0 cell (the row gradient of row j + 9).
+// a group gets 3 S workgroups: one per (LSTM layer, window set), each holding its layer's weights resident in LDS (no
+// refills). Set s of S takes the windows j = s, s + S, ... (forward; backward N-1-s, N-1-s-S, ...): every window is an
+// LSTM run from zero state, so the windows of different sets run at once and the layers run as a wavefront across
+// workgroups — cell (j, l, t) needs (j, l, t - 1) of its own workgroup and, from the layer below (forward) or above
+// (backward), the same cell's input, handed over through the sequence slabs (the layout fcr_small.h / the fused
+// kernels use) and a per-workgroup progress counter (pipe_wait / pipe_signal, fcr_small.h).
+// What remains serial is the prediction feedback. Forward: window j's row t is row j + t of the extended sequence,
+// for j + t >= 10 the output (x_hat, u) of window j + t - 10, handed from that window's layer-2 workgroup as a row;
+// so the chain is one cell per layer per window (j, t = 9) -> the head -> (j + 1, 9). Backward: window j's head needs
+// the row gradient of row j + 10, i.e. the first layer-0 cells of windows j + 1 .. j + S.
 // Within a workgroup, cells run exactly as fcr_small.h runs them (wave w owns the slots of record quad w; the same
-// fwd16_cell / sb_step arithmetic, the same LDS exchange and fixed-order reductions), so results are bit-identical to
-// the small-batch kernels'.
+// fwd16_cell / sb_step arithmetic, the same LDS exchange and fixed-order reductions), and the cost sums are formed
+// in window order from the rows at the end, so results are bit-identical to the small-batch kernels' for every S.
 // Co-residency: a workgroup may wait on another of its launch, so the host runs this family only when every
-// workgroup fits the device at once (3 x groups <= CUs / 2; a CU holds at least one) and bounds every wait.
-// Placement: the three workgroups of a group get block ids of one residue mod 8, i.e. one XCD (one L2).
+// workgroup fits the device at once (3 S x groups <= CUs / 2; a CU holds at least one) and bounds every wait.
+// Placement: the 3 S workgroups of a group get block ids of one residue mod 8, i.e. one XCD (one L2).
 #pragma once
 #include "fcr_small.h"
 
@@ -24,10 +27,11 @@ namespace fcr {
 template <int HS>
 struct Pipe {
     static constexpr int NQ = Small<HS>::NQ;
-    // one progress counter per producing workgroup (the count of its cells whose outputs are signalled): forward layer
-    // 0, layer 1, the layer-2 workgroup's hand-off rows; backward layers 0, 1, 2
-    static constexpr int F0 = 0, F1 = 1, ROW = 2, BWD = 3;
-    static_assert(BWD + 3 <= kPipeAbort, "pipe counters");
+    // per window set, one progress counter per producing workgroup (the count of its cells whose outputs are
+    // signalled): forward layer 0, layer 1, the layer-2 workgroup's hand-off rows; backward layers 0, 1, 2
+    static constexpr int F0 = 0, F1 = 1, ROW = 2, BWD = 3, PER_SET = 6;
+    static constexpr int MAX_SETS = 3;
+    static_assert(MAX_SETS * PER_SET <= kPipeAbort, "pipe counters");
     // forward: [layer fragments (layer 0's or 1 / 2's, resident) | controller records | fc.weight | fc.bias | h exchange]
     static constexpr int FRAG = Geo16<HS>::FA1 > Geo16<HS>::FA0 ? Geo16<HS>::FA1 : Geo16<HS>::FA0;   // floats
     static constexpr int LDS_FWD = (FRAG + Geo16<HS>::FNP + Geo16<HS>::FCP + 4) * 4 + Small<HS>::XBUF;
@@ -35,7 +39,8 @@ struct Pipe {
     static constexpr int LDS_BWD = BwdLds<HS, false>::BYTES + Small<HS>::RED;
     static_assert(LDS_FWD <= 163840 && LDS_BWD <= 163840, "pipe LDS");   // at least one workgroup per CU
 };
-// the hand-off row of window j: x_hat_j (4 floats, lane group q's column q) and u_{j+1}, per trajectory
+// the hand-off row of window j, per trajectory: x_hat_j (floats 0..3, lane group q's column q), u_{j+1} (4), and the
+// step's cost terms err_j (5), con_j (6) for the in-order sums at the end
 constexpr int kPipeRow = 8;   // floats per trajectory and window
 
 struct PipeArgs {
@@ -52,26 +57,33 @@ __global__ __launch_bounds__(kWave) void fcr_pipe_clear_kernel(unsigned *flags, 
     for (int i = threadIdx.x; i < n; i += kWave) flags[i] = 0u;
 }
 
-// block id -> (group, layer): the ids of one group share their residue mod 8 (one XCD); -1: an unused id
-__device__ __forceinline__ int pipe_role(int groups, int &layer) {
+// block id -> (group, layer, window set): the ids of one group share their residue mod 8 (one XCD); -1: unused id
+template <int S>
+__device__ __forceinline__ int pipe_role(int groups, int &layer, int &set) {
     const int id = blockIdx.x, xcd = id & 7, k = id >> 3;
-    layer = k % 3;
-    const int grp = xcd + 8 * (k / 3);
+    const int role = k % (3 * S);
+    layer = role % 3;
+    set = role / 3;
+    const int grp = xcd + 8 * (k / (3 * S));
     return grp < groups ? grp : -1;
 }
+// windows of set s: ceil((N - s) / S) (the host keeps S <= N, so every set has one)
+template <int S>
+__device__ __forceinline__ int pipe_windows(int N, int s) { return (N - s + S - 1) / S; }
 
 // ---------------------------------------------------------------------------------------------------
-// forward. Per cell (linear index n = j * 10 + t of the workgroup's layer): the gates of this wave's slots, the h
-// exchange through LDS (one barrier), then this wave's quad of the h record (and c) — the record write-through, as the
-// layer above reads it — and at the NEXT cell's barrier, all four waves having drained those stores, one lane signals
-// n + 1 cells done. Layers 1, 2 load their input records (sc1) two cells ahead.
+// forward. Per cell (local index m = i * 10 + t over the workgroup's windows j = s + S i): the gates of this wave's
+// slots, the h exchange through LDS (one barrier), then this wave's quad of the h record (and c) — the record
+// write-through, as the layer above reads it — and at the NEXT cell's barrier, all four waves having drained those
+// stores, one lane signals m + 1 cells done; a window's last cell (on the cross-window chain) is published at once.
+// Layers 1, 2 prefetch their input records (sc1) up to two cells ahead, as far as the layer below has published them.
 // ---------------------------------------------------------------------------------------------------
-template <int HS, bool STORE>
+template <int HS, bool STORE, int S>
 __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdArgs a, PipeArgs pa) {
     using G = Geo16<HS>;
     using P = Pipe<HS>;
-    int layer;
-    const int grp = pipe_role(pa.groups, layer);
+    int layer, set;
+    const int grp = pipe_role<S>(pa.groups, layer, set);
     if (grp < 0) return;   // uniform over the workgroup
     extern __shared__ __attribute__((aligned(16))) float lw[];
     float *lfnp = lw + P::FRAG;
@@ -93,10 +105,14 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
     const bool lead = w == 0;
     const int bc = valid ? b : a.B - 1;
     const int N = a.N;
-    const int NC = N * kL;   // cells of the workgroup's layer
+    const int nwin = pipe_windows<S>(N, set);
+    const int NC = nwin * kL;   // cells of the workgroup (its layer, its windows)
     const float alpha = a.alpha;
     unsigned *fl = pa.flags + (size_t)grp * kPipeFlags;
+    unsigned *fs = fl + set * P::PER_SET;   // this window set's counters
     float *rowbuf = pa.rows + (size_t)grp * N * kTile * kPipeRow;
+    auto row_of = [&](int j) { return rowbuf + ((size_t)j * kTile + sl) * kPipeRow; };   // window j's hand-off row
+    auto row_ready = [&](int j) { pipe_wait(fl, fl + (j % S) * P::PER_SET + P::ROW, (unsigned)(j / S + 1)); };
 
     const float ref = a.X[(size_t)bc * kCtrlIn + 2];                 // Functions.py:1392
     const float *st = a.states + (size_t)bc * kL * kIn;
@@ -114,34 +130,38 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
     auto hoff = [&](int n, int l) {   // byte offset of cell n = j * 10 + t of layer l in the group's h slab
         return (uint32_t)((((size_t)(n / kL) * kLayers + l) * kL + n % kL) * qcell * 16);
     };
+    auto nglob = [&](int m) { return (set + S * (m / kL)) * kL + m % kL; };   // local cell m -> cell index j * 10 + t
     Pace turn;
     turn.turn = 0;
     __syncthreads();
     if (layer == 0) {
-        // ---- layer 0: the window ring (B-operand layout), its last row from the layer-2 workgroup's hand-off ----
+        // ---- layer 0: the window's rows (B-operand layout), rotated so the current cell's row is at [0]; a row of the
+        // extended sequence past row 9 is a hand-off row, loaded when its cell comes (the last S rows of a window) ----
         float w0[kL], w1[kL];
 #pragma unroll
         for (int t = 0; t < kL; ++t) {
-            w0[t] = st[t * kIn + q] * scq;
-            w1[t] = (q == 0) ? st[t * kIn + 4] * sc4 : 0.0f;
+            const int r = set + t;   // the first window's rows below 10: the states, u0 in row 9 (Functions.py:1395-1396)
+            w0[t] = r < kL ? st[(r < kL ? r : 0) * kIn + q] * scq : 0.0f;
+            w1[t] = (q == 0 && r < kL) ? (r == kL - 1 ? u0 : st[(r < kL ? r : 0) * kIn + 4]) * sc4 : 0.0f;
         }
-        if (q == 0) w1[kL - 1] = u0 * sc4;                            // Functions.py:1396
-        for (int j = 0; j < N; ++j) {
-            if (j > 0) {   // Functions.py:1433-1434: the window slides; its new last row arrives at t = 9
+        for (int i = 0; i < nwin; ++i) {
+            const int j = set + S * i;
+            if (i > 0) {   // Functions.py:1433-1434: the window slides by S rows between this workgroup's windows
 #pragma unroll
-                for (int k = 0; k < kL - 1; ++k) {
-                    w0[k] = w0[k + 1];
-                    w1[k] = w1[k + 1];
+                for (int k = 0; k + S < kL; ++k) {
+                    w0[k] = w0[k + S];
+                    w1[k] = w1[k + S];
                 }
             }
             for (int t = 0; t < kL; ++t) {
-                if (j > 0 && t == kL - 1) {   // after 9 rotations the pending row is at the ring's head
-                    pipe_wait(fl, fl + P::ROW, (unsigned)j);
-                    const float *rw = rowbuf + ((size_t)(j - 1) * kTile + sl) * kPipeRow;
+                if (t >= kL - S && j + t >= kL) {   // row j + t = (x_hat, u) of window j + t - 10
+                    const int src = j + t - kL;
+                    row_ready(src);
+                    const float *rw = row_of(src);
                     const float xq = __hip_atomic_load(rw + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     const float uj = __hip_atomic_load(rw + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    w0[0] = xq * scq;                                  // x_hat_{j-1}, column q
-                    w1[0] = (q == 0) ? uj * sc4 : 0.0f;                // u_j
+                    w0[0] = xq * scq;                                  // x_hat, column q
+                    w1[0] = (q == 0) ? uj * sc4 : 0.0f;                // u
                 }
                 const float x0 = w0[0], x1 = w1[0];
                 rot_left(w0);
@@ -156,7 +176,7 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
                 });
                 pipe_drain();   // this wave's record stores of the previous cell (long complete)
                 lds_barrier();
-                pipe_signal(fl + P::F0, (unsigned)(j * kL + t));
+                pipe_signal(fs + P::F0, (unsigned)(i * kL + t));
                 load_quads<HS>(hp, reinterpret_cast<const f32x4 *>(xb), lane);   // the whole split record of h_t
                 by_quad<HS>(w, [&](auto Wc) {
                     constexpr int W = decltype(Wc)::v;
@@ -164,30 +184,36 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
                     if (STORE && t + 1 < kL) store_quad<HS, W>(cs_wave + (size_t)hoff(j * kL + t, 0) / 16, c, lane);
                 });
                 if (STORE && lead) xw_wave[((size_t)j * kL + t) * kWave + lane] = f32x2{x0, x1};
+                if (t == kL - 1) {   // the window's last cell is on the cross-window chain: published at once
+                    pipe_drain();
+                    lds_barrier();
+                    pipe_signal(fs + P::F0, (unsigned)(i * kL + t + 1));
+                }
             }
         }
         pipe_drain();
         __syncthreads();
-        pipe_signal(fl + P::F0, (unsigned)NC);
+        pipe_signal(fs + P::F0, (unsigned)NC);
         return;
     }
     // ---- layers 1, 2: input records from the layer below (sc1), two cells ahead ----
     const bool keep_h = layer == 1 || STORE;
-    unsigned *below = fl + (layer == 1 ? P::F0 : P::F1);
-    float u_prev = u0;
-    float cmd_j = alpha * sq(st[(kL - 2) * kIn + 4] - u0);            // Functions.py:1405
-    float cmd_sum = 0.0f, err_sum = 0.0f, tot_sum = 0.0f;
-    if (layer == 2 && lead && valid && q == 0) a.prediction[(size_t)b * N] = u0;   // Functions.py:1455
-    f32x4 xa[Geo<HS>::HQ], xn[Geo<HS>::HQ], xf[Geo<HS>::HQ];   // the input records of cells n, n + 1, n + 2
+    unsigned *below = fs + (layer == 1 ? P::F0 : P::F1);
+    if (layer == 2 && set == 0 && lead && valid && q == 0) a.prediction[(size_t)b * N] = u0;   // Functions.py:1455
+    // the input records of cells m, m + 1, m + 2, prefetched as far as the layer below has published them (a record
+    // that was late is waited for at its cell: a late input never stalls the cell before it)
+    f32x4 xa[Geo<HS>::HQ], xn[Geo<HS>::HQ], xf[Geo<HS>::HQ];
 #pragma unroll
-    for (int k = 0; k < Geo<HS>::HQ; ++k) xf[k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    pipe_wait(fl, below, 1);
-    ld_rec_sc1<HS>(xa, rh, hoff(0, layer - 1), lane);
-    pipe_wait(fl, below, 2);
-    ld_rec_sc1<HS>(xn, rh, hoff(1, layer - 1), lane);
-    for (int j = 0; j < N; ++j) {
+    for (int k = 0; k < Geo<HS>::HQ; ++k) xn[k] = xf[k] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    bool have_a = false, have_n = false;
+    for (int i = 0; i < nwin; ++i) {
+        const int j = set + S * i;
         for (int t = 0; t < kL; ++t) {
-            const int n = j * kL + t;
+            const int m = i * kL + t, n = j * kL + t;
+            if (!have_a) {
+                pipe_wait(fl, below, (unsigned)(m + 1));
+                ld_rec_sc1<HS>(xa, rh, hoff(nglob(m), layer - 1), lane);
+            }
             const bool last = layer == 2 && t + 1 == kL;   // h_9 of layer 2: the readout's, in fp32
             char *xb = reinterpret_cast<char *>(xbuf) + (t & 1) * RECB;
             float xc[HS];
@@ -201,13 +227,21 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
                 if (last) xchg_put<HS, W>(reinterpret_cast<f32x4 *>(xb), hout, lane);
                 else xrec_put<HS, W>(xb, hout, lane);
             });
-            pipe_drain();   // this wave's record stores of the previous cell and its load of cell n + 1's input
-            if (n + 2 < NC) {
-                pipe_wait(fl, below, (unsigned)(n + 3));
-                ld_rec_sc1<HS>(xf, rh, hoff(n + 2, layer - 1), lane);
+            pipe_drain();   // this wave's record stores of the previous cell and its prefetches
+            bool have_f = false;
+            {
+                const unsigned avail = pipe_count(below);
+                if (!have_n && m + 1 < NC && avail >= (unsigned)(m + 2)) {
+                    ld_rec_sc1<HS>(xn, rh, hoff(nglob(m + 1), layer - 1), lane);
+                    have_n = true;
+                }
+                if (have_n && m + 2 < NC && avail >= (unsigned)(m + 3)) {
+                    ld_rec_sc1<HS>(xf, rh, hoff(nglob(m + 2), layer - 1), lane);
+                    have_f = true;
+                }
             }
             lds_barrier();
-            if (layer == 1) pipe_signal(fl + P::F1, (unsigned)n);
+            if (layer == 1) pipe_signal(fs + P::F1, (unsigned)m);
             if (last) {
                 xchg_get<HS>(reinterpret_cast<const f32x4 *>(xb), hout, lane);
             } else {
@@ -219,14 +253,21 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
                 by_quad<HS>(w, [&](auto Wc) {
                     store_quad<HS, decltype(Wc)::v>(cs_wave + (size_t)hoff(n, layer) / 16, c, lane);
                 });
+            if (layer == 1 && t == kL - 1) {   // the window's last cell is on the cross-window chain: published at once
+                pipe_drain();
+                lds_barrier();
+                pipe_signal(fs + P::F1, (unsigned)(m + 1));
+            }
 #pragma unroll
             for (int k = 0; k < Geo<HS>::HQ; ++k) {
                 xa[k] = xn[k];
                 xn[k] = xf[k];
             }
+            have_a = have_n;
+            have_n = have_f;
         }
         if (layer != 2) continue;
-        // ---- layer 2, end of window j: readout fc(h_9) (Functions.py:377), costs, the next command ----
+        // ---- layer 2, end of window j: readout fc(h_9) (Functions.py:377), its cost terms, the next command ----
         const float *lfnp_j = opaque(lfnp), *lfcp_j = opaque(lfcp), *lfcb_j = opaque(lfcb);
         float xo[kOut];
 #pragma unroll
@@ -249,33 +290,52 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
         }
         const float err = sq(xh0 - ref);                              // Functions.py:1405-1414, 1443-1452
         const float con = relu(-xh1) + relu(-xh2) + relu(xh1 - kP1Max) + relu(xh2 - kP2Max);
-        tot_sum += (err + cmd_j) + con;
-        err_sum += err;
-        cmd_sum += cmd_j;
+        float un = 0.0f;
         if (j + 1 < N) {                                               // Functions.py:1421-1434
             float z[kMS];
-            const float un = hardtanh(fnn_pre(lfnp_j, q, xh0, xh3, ref, z));
-            cmd_j = alpha * sq(u_prev - un);                           // Functions.py:1446
-            u_prev = un;
-            if (lead) {   // the hand-off row of window j (write-through; only this wave stores it), then its counter
-                float *rw = rowbuf + ((size_t)j * kTile + sl) * kPipeRow;
-                __hip_atomic_store(rw + q, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (q == 0) __hip_atomic_store(rw + 4, un, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (valid && q == 0) a.prediction[(size_t)b * N + j + 1] = un;   // Functions.py:1466
-                pipe_drain();
-                pipe_signal(fl + P::ROW, (unsigned)(j + 1));
+            un = hardtanh(fnn_pre(lfnp_j, q, xh0, xh3, ref, z));
+            if (lead && valid && q == 0) a.prediction[(size_t)b * N + j + 1] = un;   // Functions.py:1466
+        }
+        if (lead) {   // the hand-off row of window j (write-through; only this wave stores it), then its counter
+            float *rw = row_of(j);
+            __hip_atomic_store(rw + q, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (q == 0) {
+                __hip_atomic_store(rw + 4, un, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(rw + 5, err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(rw + 6, con, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            pipe_drain();
+            pipe_signal(fs + P::ROW, (unsigned)(i + 1));
         }
     }
     if (layer == 1) {
         pipe_drain();
         __syncthreads();
-        pipe_signal(fl + P::F1, (unsigned)NC);
+        pipe_signal(fs + P::F1, (unsigned)NC);
         return;
     }
-    // every wait of the chain ends at this workgroup: a timed-out one anywhere shows as NaN cost and loss
+    // ---- the sums over the steps, in window order (Functions.py:1441-1460), by the workgroup of window N - 1 ----
+    if (set != (N - 1) % S || !lead) return;
+    for (int k = 0; k < S; ++k) pipe_wait(fl, fl + k * P::PER_SET + P::ROW, (unsigned)pipe_windows<S>(N, k));
+    float u_prev = u0;
+    float cmd_j = alpha * sq(st[(kL - 2) * kIn + 4] - u0);            // Functions.py:1405
+    float cmd_sum = 0.0f, err_sum = 0.0f, tot_sum = 0.0f;
+    for (int j = 0; j < N; ++j) {
+        const float *rw = row_of(j);
+        const float err = __hip_atomic_load(rw + 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float con = __hip_atomic_load(rw + 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        tot_sum += (err + cmd_j) + con;
+        err_sum += err;
+        cmd_sum += cmd_j;
+        if (j + 1 < N) {
+            const float un = __hip_atomic_load(rw + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            cmd_j = alpha * sq(u_prev - un);                           // Functions.py:1446
+            u_prev = un;
+        }
+    }
+    // every wait of the chains ends before this one: a timed-out one anywhere shows as NaN cost and loss
     const float cost = pipe_aborted(fl) ? __builtin_nanf("") : tot_sum / (float)N;   // Functions.py:1458-1460
-    if (lead && valid && q == 0) {
+    if (valid && q == 0) {
         a.cost[b] = cost;
         a.command[b] = cmd_sum / (float)N;
         a.error[b] = err_sum / (float)N;
@@ -283,23 +343,23 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
     float part = (valid && q == 0) ? cost : 0.0f;
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) part += __shfl_xor(part, m);
-    if (lead && lane == 0) a.loss_part[grp] = part;
+    if (lane == 0) a.loss_part[grp] = part;
 }
 
 // ---------------------------------------------------------------------------------------------------
-// backward: each layer's workgroup runs fcr_sbwd_kernel's per-layer phases (sb_phase, PIPE) over every window; layer
-// 2's also the window heads (cost gradients, the controller backward, dh_9), layer 0's the window-row gradients
-// (each wave its own copy, fcr_small.h) and g_u0
+// backward: each (layer, window set) workgroup runs fcr_sbwd_kernel's per-layer phases (sb_phase, PIPE) over its
+// windows j = N-1-s, N-1-s-S, ...; layer 2's also their heads (cost gradients, the controller backward, dh_9), layer
+// 0's the window-row gradients (each wave its own copy, fcr_small.h), and the layer-0 workgroup of window 0 g_u0
 // ---------------------------------------------------------------------------------------------------
-template <int HS>
+template <int HS, int S>
 __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pbwd_kernel(BwdArgs a, PipeArgs pa) {
     using LD = BwdLds<HS, false>;
     using I1 = Img<HS, false>;
     using I0 = Img<HS, true>;
     using P = Pipe<HS>;
     constexpr int NQ = P::NQ;
-    int layer;
-    const int grp = pipe_role(pa.groups, layer);
+    int layer, set;
+    const int grp = pipe_role<S>(pa.groups, layer, set);
     if (grp < 0) return;
     extern __shared__ __attribute__((aligned(16))) float lw[];
     float *lfnp = lw + LD::REGION / 4;
@@ -353,8 +413,16 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pbwd_kernel(BwdA
     x.dseq_w = a.dseq + (size_t)grp * dseq_sz;
     unsigned *fl = pa.flags + (size_t)grp * kPipeFlags;
     x.flags = fl;
-    x.fl_own = P::BWD + layer;
-    x.fl_above = layer < 2 ? P::BWD + layer + 1 : -1;
+    x.S = S;
+    x.din_pending = false;
+    x.fl_own = set * P::PER_SET + P::BWD + layer;
+    x.fl_above = layer < 2 ? set * P::PER_SET + P::BWD + layer + 1 : -1;
+    const int nwin = pipe_windows<S>(N, set);
+    const int j0 = N - 1 - set;   // this workgroup's first window (then j0 - S, ...)
+    // the layer-0 counter of window v's set, and its count once v's cell t is done (x.done_after in that set's order)
+    auto l0_done = [&](int v, int t) {
+        pipe_wait(fl, fl + ((N - 1 - v) % S) * P::PER_SET + P::BWD, (unsigned)((N - 1 - v) / S * kL + (kL - 1 - t) + 1));
+    };
     auto row_grad = [&](int rho) {   // sum over windows v = max(0, rho-9) .. min(N-1, rho) of dx(v, rho-v)
         f32x2 acc2 = {0.0f, 0.0f};
         const int w_hi = rho < N - 1 ? rho : N - 1;
@@ -367,9 +435,9 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pbwd_kernel(BwdA
 #pragma unroll
     for (int r = 0; r < HS; ++r) dh[r] = dc[r] = 0.0f;
     CellIn<HS> ci;
-    {   // the first cell (N - 1, layer, 9): its x, h (forward records), c and din (the layer above's first cell)
-        if (layer < 2) pipe_wait(fl, fl + x.fl_above, x.done_after(N - 1, kL - 1));
-        const NextIn f = x.next_of(N, layer, 0);   // the cell after (N, layer, 0) = (N - 1, layer, 9)
+    {   // the first cell (j0, layer, 9): its x, h (forward records), c and din (the layer above's first cell)
+        if (layer < 2) pipe_wait(fl, fl + x.fl_above, x.done_after(j0, kL - 1));
+        const NextIn f = x.next_of(j0 + S, layer, 0);   // the cell after (j0 + S, layer, 0) = (j0, layer, 9)
         by_quad<HS>(w, [&](auto Wc) {
             constexpr int W = decltype(Wc)::v;
             if (layer == 0) sb_load_a<HS, true, true>(ci, f, lane);
@@ -381,7 +449,7 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pbwd_kernel(BwdA
     float dh_out[HS];
 #pragma unroll
     for (int r = 0; r < HS; ++r) dh_out[r] = 0.0f;
-    for (int j = N - 1; j >= 0; --j) {
+    for (int j = j0; j >= 0; j -= S) {
         if (layer == 2) {   // ---- window head (Functions.py:1443-1452, 1424-1430, 377) ----
             const float *lfnp_j = opaque(lfnp), *lfcp_j = opaque(lfcp);
             const float x0 = xh[j * kOut + 0], x1 = xh[j * kOut + 1], x2 = xh[j * kOut + 2], x3 = xh[j * kOut + 3];
@@ -391,8 +459,9 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pbwd_kernel(BwdA
             float d2 = wgt * ((-x2 > 0.0f ? -1.0f : 0.0f) + (x2 - kP2Max > 0.0f ? 1.0f : 0.0f));
             float d3 = 0.0f;
             if (j <= N - 2) {
-                // row 10 + j is complete once layer 0 has done window j + 1's first cell (t = 9)
-                pipe_wait(fl, fl + P::BWD, x.done_after(j + 1, kL - 1));
+                // row 10 + j sums dx(v, 10 + j - v) over windows v = j + 1 .. j + 10: each set's latest is among
+                // v = j + 1 .. j + S (its cell t = 10 + j - v), the rest came before it in that set's order
+                for (int v = j + 1; v <= j + S && v < N; ++v) l0_done(v, kL + j - v);
                 const f32x2 Gr = row_grad(kL + j);
                 d0 += __shfl(Gr[0], sl);
                 d1 += __shfl(Gr[0], sl + 16);
@@ -433,9 +502,11 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pbwd_kernel(BwdA
     }
     pipe_drain();   // the last cell's outputs, signalled once every wave has drained them
     __syncthreads();
-    pipe_signal(fl + x.fl_own, x.done_after(0, 0));
-    if (layer != 0) return;
-    const float g_u0_rows = row_grad(kL - 1)[1];   // row 9, col 4 = u0 (Functions.py:1396)
+    pipe_signal(fl + x.fl_own, (unsigned)(nwin * kL));
+    if (layer != 0 || set != (N - 1) % S) return;
+    // row 9 (its col 4 = u0, Functions.py:1396) sums dx(v, 9 - v) over windows 0 .. 9: every set's layer 0 done
+    for (int k = 0; k < S; ++k) pipe_wait(fl, fl + k * P::PER_SET + P::BWD, (unsigned)(pipe_windows<S>(N, k) * kL));
+    const float g_u0_rows = row_grad(kL - 1)[1];
     float du0 = 2.0f * alpha * wgt * (pred[0] - s84);
     if (N > 1) du0 += 2.0f * alpha * wgt * (pred[0] - pred[1]);
     // layer 0 ends the chain: a timed-out wait anywhere shows as NaN gradients

@@ -38,6 +38,10 @@ __device__ __forceinline__ void pipe_drain() { asm volatile("s_waitcnt vmcnt(0)"
 __device__ __forceinline__ void pipe_signal(unsigned *f, unsigned v) {   // after the barrier that follows every drain
     if (threadIdx.x == 0) __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// a producer's progress counter as it stands (no wait): prefetches take what is published and leave the rest
+__device__ __forceinline__ unsigned pipe_count(const unsigned *f) {
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
 // a wait of this launch timed out (its partner workgroup was not resident): the outputs are then poisoned with NaN
 __device__ __forceinline__ bool pipe_aborted(const unsigned *blk) {
     return __builtin_amdgcn_readfirstlane(__hip_atomic_load(blk + kPipeAbort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u;
@@ -446,7 +450,7 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_sfwd_kernel(FwdA
 // s; else σ = HS + s), dx of its slots (layers >= 1: σ = s, into its dseq quad) and, for L0, the window
 // columns σ = HS, HS+1 (every wave: the row gradients feed each wave's window head).
 // PUB (the layer-pipelined backward): after the first barrier — which every wave reached after draining its stores of
-// the previous cell (wait_din_after) — one lane signals that cell's outputs: *pub = pub_v
+// the previous cell (din_ready_after) — one lane signals that cell's outputs: *pub = pub_v
 template <int HS, bool L0, int W, bool PUB = false>
 __device__ __forceinline__ void small_reduce(f32x4 *red, const f32x4 (&part)[Small<HS>::NB], int lane, float (&dh)[HS],
                                              float (&dxo)[HS], float &dxq, float &dx4, unsigned *pub = nullptr,
@@ -663,8 +667,9 @@ __device__ __forceinline__ f32x4 sb_ttile(const TFrag<HS, L0, R0, R1> &f, const 
     return acc;
 }
 
-// PIPE (fcr_pipe.h): one workgroup per (group, layer), so the cell after (j, l, 0) is (j - 1, l, 9), the din of a cell
-// is waited for on the layer above's counters, and each cell's outputs are published on this wave's counter
+// PIPE (fcr_pipe.h): one workgroup per (group, layer, window set) — set s of S takes windows N-1-s, N-1-s-S, ... — so
+// the cell after (j, l, 0) is (j - S, l, 9), the din of a cell is waited for on the layer above's counters (same set),
+// and each cell's outputs are published on this workgroup's counter
 template <int HS, bool PIPE = false>
 struct SbCtx {
     NextIn nb;                        // this group's slab descriptors
@@ -681,13 +686,15 @@ struct SbCtx {
     __device__ size_t doff(int j, int lfrom, int t) const { return ((size_t)(j * 2 + (2 - lfrom)) * kL + t) * Geo<HS>::QC; }
     unsigned *flags;                  // PIPE: this group's counters (kPipeFlags)
     int fl_own, fl_above;             // PIPE: index of this workgroup's counter, of the layer above's (or -1)
+    int S;                            // PIPE: window sets (the stride between this workgroup's windows)
+    mutable bool din_pending;         // PIPE: the next cell's din was not yet published when it would have been prefetched
     __device__ NextIn next_of(int j, int l, int t) const {   // the cell processed after (j, l, t)
         NextIn n = nb;
         int nj = j, nl = l, nt = t - 1;
         if (t == 0) {
             nt = kL - 1;
             nl = PIPE ? l : l - 1;
-            if (PIPE || l == 0) { nl = PIPE ? l : 2; nj = j - 1; }
+            if (PIPE || l == 0) { nl = PIPE ? l : 2; nj = j - (PIPE ? S : 1); }
         }
         if (nj < 0) { nj = 0; nl = PIPE ? l : 2; nt = 9; }   // past the last cell: a valid one (harmless)
         n.x = nl == 0 ? (uint32_t)((nj * kL + nt) * kWave * 8) : hoff(nj, nl > 0 ? nl - 1 : 0, nt);
@@ -696,17 +703,16 @@ struct SbCtx {
         n.d = (uint32_t)((nl < 2 ? doff(nj, nl + 1, nt) : 0) * 16);
         return n;
     }
-    // PIPE: a layer workgroup's progress counter after cell (j, t) (windows N-1 .. 0, t = 9 .. 0)
-    __device__ unsigned done_after(int j, int t) const { return (unsigned)((N - 1 - j) * kL + (kL - 1 - t) + 1); }
-    // PIPE, in cell (j, t) before loading the din of the cell after it: this wave's stores of the previous cell are
-    // drained (they are signalled at this cell's first reduction barrier), and the layer above has published that din
-    __device__ void wait_din_after(int j, int t) const {
-        if constexpr (PIPE) {
-            pipe_drain();
-            int nj = j, nt = t - 1;
-            if (t == 0) { nj = j - 1; nt = kL - 1; }
-            if (nj >= 0 && fl_above >= 0) pipe_wait(flags, flags + fl_above, done_after(nj, nt));
-        }
+    // PIPE: a layer workgroup's progress counter after cell (j, t) (its windows N-1-s, N-1-s-S, ..., t = 9 .. 0)
+    __device__ unsigned done_after(int j, int t) const { return (unsigned)((N - 1 - j) / S * kL + (kL - 1 - t) + 1); }
+    // PIPE, in cell (j, t) before prefetching the din of the cell after it: this wave's stores of the previous cell
+    // are drained (they are signalled at this cell's first reduction barrier); true if the layer above has already
+    // published that din (else the next cell waits for it at its start: a late din never stalls this cell)
+    __device__ bool din_ready_after(int j, int t) const {
+        pipe_drain();
+        int nj = j, nt = t - 1;
+        if (t == 0) { nj = j - S; nt = kL - 1; }
+        return nj < 0 || fl_above < 0 || pipe_count(flags + fl_above) >= done_after(nj, nt);
     }
 };
 
@@ -741,6 +747,13 @@ __device__ __forceinline__ void sb_step(const SbCtx<HS, PIPE> &x, int j, int t, 
     constexpr bool L0 = LAYER == 0, DIN = LAYER < 2;
     constexpr int NB = Img<HS, L0>::NB;
     const uint32_t fb = L0 ? x.fb0 : x.fb1, tb = L0 ? x.tb0 : x.tb1;
+    if constexpr (PIPE && DIN) {
+        if (x.din_pending) {   // this cell's din was late at the prefetch: wait for it now
+            pipe_wait(x.flags, x.flags + x.fl_above, x.done_after(j, t));
+            ld_quad_sc1<HS, W>(ci.d, x.nb.rd, (uint32_t)(x.doff(j, LAYER + 1, t) * 16), x.lane);
+            x.din_pending = false;
+        }
+    }
     const unsigned long long s0 = stamp_now();
     // ---- region 1 ----
     sched_fence();
@@ -767,8 +780,17 @@ __device__ __forceinline__ void sb_step(const SbCtx<HS, PIPE> &x, int j, int t, 
         }
     }
     sched_fence();
-    x.wait_din_after(j, t);   // (PIPE only; the drain also for a cell with no din to wait for)
-    sb_load_b<HS, W, B_NX_HC, B_NX_DIN, PIPE>(ci, x.next_of(j, LAYER, t), x.lane);
+    if constexpr (PIPE) {   // the drain also for a cell with no din to prefetch
+        const bool now = x.din_ready_after(j, t);
+        const NextIn nx = x.next_of(j, LAYER, t);
+        sb_load_b<HS, W, B_NX_HC, false, PIPE>(ci, nx, x.lane);
+        if constexpr (B_NX_DIN) {
+            if (now) ld_quad_sc1<HS, W>(ci.d, nx.rd, nx.d, x.lane);
+            x.din_pending = !now;
+        }
+    } else {
+        sb_load_b<HS, W, B_NX_HC, B_NX_DIN, PIPE>(ci, x.next_of(j, LAYER, t), x.lane);
+    }
     const unsigned long long s1 = stamp_now();
     // ---- region 2 ----
     TFrag<HS, L0, R0, R1> tf[2];
@@ -825,6 +847,11 @@ __device__ __forceinline__ void sb_step(const SbCtx<HS, PIPE> &x, int j, int t, 
     if constexpr (PIPE) {
         if (L0) buf_st2_sc1(x.rr, x.lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{dxq * x.scq, dx4 * x.sc4});
         else st_quad_sc1<HS, W>(x.nb.rd, (uint32_t)(x.doff(j, LAYER, t) * 16), dxo, x.lane);
+        if (t == kL - 1) {   // a window's first cell is on the cross-window chain (Pipe): published at once
+            pipe_drain();
+            lds_barrier();
+            pipe_signal(x.flags + x.fl_own, x.done_after(j, t));
+        }
     } else {
         if (L0) buf_st2(x.rr, x.lane * 8, (uint32_t)((j * kL + t) * kWave * 8), f32x2{dxq * x.scq, dx4 * x.sc4});   // row j+t
         else store_quad<HS, W>(x.dseq_w + x.doff(j, LAYER, t), dxo, x.lane);

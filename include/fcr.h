@@ -258,11 +258,19 @@ int fcr_set_small_batch_limit(int32_t max_batch);
 int fcr_get_small_batch_limit(void);
 
 /* Within the small-batch family, B <= max_batch (and at most 32 groups of 16 trajectories, 3 workgroups each within
- * half the device's CUs) runs the layer-pipelined geometry (csrc/fcr_pipe.h: one workgroup per LSTM layer, the layers
- * and windows as a wavefront; results bit-identical to the one-workgroup-per-group kernels). Default 512; 0 = never.
+ * half the device's CUs) runs the layer-pipelined geometry (csrc/fcr_pipe.h: one workgroup per LSTM layer and window
+ * set, the layers and windows as a wavefront; results bit-identical to the one-workgroup-per-group kernels). Default
+ * 512; 0 = never.
  * Process-wide; returns the previous value; fcr_get_small_pipe_limit reads it. */
 int fcr_set_small_pipe_limit(int32_t max_batch);
 int fcr_get_small_pipe_limit(void);
+
+/* The pipelined geometry's window sets S (1..3): 3 S workgroups per group, set s taking windows s, s + S, ... so
+ * windows run concurrently (every window is an LSTM run from zero state; only the prediction feedback is serial).
+ * 0 (default) = the most that fit (3 S workgroups per group within half the CUs, S <= N); results are bit-identical
+ * for every S. Process-wide; returns the previous value; fcr_get_small_pipe_sets reads it. */
+int fcr_set_small_pipe_sets(int32_t sets);
+int fcr_get_small_pipe_sets(void);
 
 /*
  * H > 52 (the batch-wide GEMM path): how many bytes of "kept windows" fcr_workspace_size(with_backward = 1)

@@ -55,6 +55,34 @@ def test_layer_pipelined_small_kernels_meet_oracle_and_match_one_workgroup(H, B,
         assert relerr(pipe[k], one[k]) <= 1e-6, (H, B, N, k, relerr(pipe[k], one[k]))
 
 
+def _with_pipe_sets(sets, fn):
+    prev = native.set_small_pipe_sets(sets)
+    try:
+        return fn()
+    finally:
+        native.set_small_pipe_sets(prev)
+
+
+@pytest.mark.parametrize("H,B,N", [(50, 15, 10), (50, 40, 25), (32, 17, 2), (50, 9, 1), (50, 3, 4)])
+def test_window_sets_meet_oracle_and_agree(H, B, N):
+    """S = 1, 2, 3 window sets (3 S workgroups per group; set s takes windows s, s + S, ...): the same cells, the cost
+    sums in window order, so the same bits for every S; and the fp64 oracle at 1e-5."""
+    from tests.golden.make_golden import synth_params
+    params = load_case("ref_b15_n10")[1] if H == 50 else synth_params(H, 900 + H)
+    X, S, _ = _synth(B, N, 1000 + H + B + N)
+    u0 = _u0(params, X)
+    assert native.small_pipe_sets() == 0
+    outs = {k: _with_pipe_sets(k, lambda: run(params, X, u0, S, N, 20.0, small_batch_limit=BIG)) for k in (1, 2, 3)}
+    f, g = _oracle(params, X, u0, S, N)
+    for k in FEATS + ("xhat",):
+        assert relerr(outs[3][k], f[k]) <= TOL, (H, B, N, k, relerr(outs[3][k], f[k]))
+    for k, _ in GRADS:
+        assert relerr(outs[3][k], g[k]) <= TOL, (H, B, N, k, relerr(outs[3][k], g[k]))
+    for sets in (2, 3):
+        for k in FEATS + ("xhat",) + tuple(k for k, _ in GRADS):
+            assert np.array_equal(outs[sets][k], outs[1][k]), (sets, H, B, N, k, relerr(outs[sets][k], outs[1][k]))
+
+
 def test_layer_pipelined_golden_reference_batch():
     """The reference's own batch (B = 15, N = 10, its trained weights) against the committed fp64 fixture."""
     c, params = load_case("ref_b15_n10")
