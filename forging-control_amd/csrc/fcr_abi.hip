@@ -270,17 +270,13 @@ PipeArgs pipe_args(const Layout &L, char *base) {
     p.groups = L.nw;
     return p;
 }
-int pipe_clear(const PipeArgs &pa, const Layout &L, hipStream_t s) {
-    hipLaunchKernelGGL(fcr_pipe_clear_kernel, dim3(1), dim3(kWave), 0, s, pa.flags, L.nw * kPipeFlags);
-    return launch_check("fcr_pipe_clear_kernel");
-}
 // grid: 3 S workgroups per group, the ids of a group one residue mod 8 apart (pipe_role)
 template <int HS, bool STORE, int S>
 int launch_pfwd_t(const FwdArgs &fa, const PipeArgs &pa, const Layout &L, hipStream_t s) {
     constexpr int lds = Pipe<HS>::LDS_FWD;
     static std::atomic<unsigned long long> attr_done{0};
     if (const int rc = lds_attr((const void *)fcr_pfwd_kernel<HS, STORE, S>, lds, attr_done, "pfwd")) return rc;
-    if (const int rc = pipe_clear(pa, L, s)) return rc;
+    // (the counters were zeroed by this call's pack_all_kernel)
     hipLaunchKernelGGL((fcr_pfwd_kernel<HS, STORE, S>), dim3(24 * S * ((L.nw + 7) / 8)), dim3(Small<HS>::NQ * kWave), lds,
                        s, fa, pa);
     return launch_check("fcr_pfwd_kernel");
@@ -296,7 +292,7 @@ int launch_pbwd_t(const BwdArgs &ba, const PipeArgs &pa, const Layout &L, hipStr
     constexpr int lds = Pipe<HS>::LDS_BWD;
     static std::atomic<unsigned long long> attr_done{0};
     if (const int rc = lds_attr((const void *)fcr_pbwd_kernel<HS, S>, lds, attr_done, "pbwd")) return rc;
-    if (const int rc = pipe_clear(pa, L, s)) return rc;
+    // (the counters were zeroed by the forward's pack_all_kernel; each backward leaves its own zeroed, fcr_pipe.h)
     hipLaunchKernelGGL((fcr_pbwd_kernel<HS, S>), dim3(24 * S * ((L.nw + 7) / 8)), dim3(Small<HS>::NQ * kWave), lds, s, ba,
                        pa);
     return launch_check("fcr_pbwd_kernel");
@@ -537,8 +533,12 @@ struct PackAllArgs {
     PackArgs a;
     int njobs;
     PackJob job[2 * kLayers + 1];
+    unsigned *clear;   // or null: the pipelined kernels' progress counters, zeroed by block 0 (fcr_pipe.h)
+    int nclear;
 };
 __global__ __launch_bounds__(256) void pack_all_kernel(PackAllArgs p) {
+    if (p.clear && blockIdx.x == 0)
+        for (int i = (int)threadIdx.x; i < p.nclear; i += 256) p.clear[i] = 0u;
     int b = blockIdx.x, j = 0;
     while (j + 1 < p.njobs && b >= p.job[j].blocks) b -= p.job[j++].blocks;
     const int idx = b * 256 + (int)threadIdx.x;
@@ -1517,9 +1517,13 @@ int fcr_forward(const fcr_dims *d, fcr_options *opts, const fcr_weights *w, cons
     if ((rc = launch_range(d, states, u0, noise, w->fc_w, w->fc_b, (float *)(base + L.rng), (float *)(base + L.wsc), s)))
         return rc;
     {   // every weight pack of the call in ONE launch (seven launches of ~4 us each were a step's overhead
-        // at the reference's B = 15)
+        // at the reference's B = 15), and the pipelined kernels' counters zeroed for this forward and its backward
         PackAllArgs pk{};
         pk.a = pa;
+        if (L.nw <= kPipeMaxGroups) {
+            pk.clear = (unsigned *)(base + L.pipe_flags);
+            pk.nclear = L.nw * kPipeFlags;
+        }
         for (int l = 0; l < kLayers; ++l) {
             const int nf = L.HS * (l == 0 ? (L.HS + 2 + 7) / 8 : (2 * L.HS + 7) / 8) * kWave * 8;   // per (tile, block, lane, k)
             pk.job[pk.njobs++] = PackJob{kPackFwd16, l, (nf + 255) / 256, (_Float16 *)(base + L.fa[l])};

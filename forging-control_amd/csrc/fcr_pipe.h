@@ -31,7 +31,7 @@ struct Pipe {
     // signalled): forward layer 0, layer 1, the layer-2 workgroup's hand-off rows; backward layers 0, 1, 2
     static constexpr int F0 = 0, F1 = 1, ROW = 2, BWD = 3, PER_SET = 6;
     static constexpr int MAX_SETS = 3;
-    static_assert(MAX_SETS * PER_SET <= kPipeAbort, "pipe counters");
+    static_assert(MAX_SETS * PER_SET <= kPipeAbort - 1, "pipe counters");
     // forward: [layer fragments (layer 0's or 1 / 2's, resident) | controller records | fc.weight | fc.bias | h exchange]
     static constexpr int FRAG = Geo16<HS>::FA1 > Geo16<HS>::FA0 ? Geo16<HS>::FA1 : Geo16<HS>::FA0;   // floats
     static constexpr int LDS_FWD = (FRAG + Geo16<HS>::FNP + Geo16<HS>::FCP + 4) * 4 + Small<HS>::XBUF;
@@ -49,13 +49,12 @@ struct PipeArgs {
     int groups;
 };
 
-// zeroes the progress counters ahead of each pipelined launch, on the launch's stream. A kernel rather than
-// hipMemsetAsync: a memset captured into a HIP graph left stale counters in replays (the consumers ran ahead on the
-// previous replay's rows: profiles/round6_b15_pipe_graph.log); a kernel node has the ordering and the release / acquire
-// of any kernel boundary.
-__global__ __launch_bounds__(kWave) void fcr_pipe_clear_kernel(unsigned *flags, int n) {
-    for (int i = threadIdx.x; i < n; i += kWave) flags[i] = 0u;
-}
+// The counters are zeroed by each forward call's pack_all_kernel (fcr_abi.hip), ahead of the forward and its backward
+// on the call's stream, by a kernel rather than hipMemsetAsync: a memset captured into a HIP graph left stale counters
+// in replays (the consumers ran ahead on the previous replay's rows: profiles/round6_b15_pipe_graph.log); a kernel node
+// has the ordering and the release / acquire of any kernel boundary. A backward leaves its own counters zeroed (the
+// last of a group's workgroups to arrive resets them), so a second backward of the same forward starts clean.
+constexpr int kPipeArrive = kPipeAbort - 1;   // backward: the group's workgroups that have finished
 
 // block id -> (group, layer, window set): the ids of one group share their residue mod 8 (one XCD); -1: unused id
 template <int S>
@@ -503,14 +502,27 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pbwd_kernel(BwdA
     pipe_drain();   // the last cell's outputs, signalled once every wave has drained them
     __syncthreads();
     pipe_signal(fl + x.fl_own, (unsigned)(nwin * kL));
-    if (layer != 0 || set != (N - 1) % S) return;
-    // row 9 (its col 4 = u0, Functions.py:1396) sums dx(v, 9 - v) over windows 0 .. 9: every set's layer 0 done
-    for (int k = 0; k < S; ++k) pipe_wait(fl, fl + k * P::PER_SET + P::BWD, (unsigned)(pipe_windows<S>(N, k) * kL));
-    const float g_u0_rows = row_grad(kL - 1)[1];
-    float du0 = 2.0f * alpha * wgt * (pred[0] - s84);
-    if (N > 1) du0 += 2.0f * alpha * wgt * (pred[0] - pred[1]);
-    // layer 0 ends the chain: a timed-out wait anywhere shows as NaN gradients
-    if (lead && valid && q == 0) a.g_u0[b] = pipe_aborted(fl) ? __builtin_nanf("") : g_u0_rows + du0;
+    if (layer == 0 && set == (N - 1) % S) {
+        // row 9 (its col 4 = u0, Functions.py:1396) sums dx(v, 9 - v) over windows 0 .. 9: every set's layer 0 done
+        for (int k = 0; k < S; ++k) pipe_wait(fl, fl + k * P::PER_SET + P::BWD, (unsigned)(pipe_windows<S>(N, k) * kL));
+        const float g_u0_rows = row_grad(kL - 1)[1];
+        float du0 = 2.0f * alpha * wgt * (pred[0] - s84);
+        if (N > 1) du0 += 2.0f * alpha * wgt * (pred[0] - pred[1]);
+        // layer 0 ends the chain: a timed-out wait anywhere shows as NaN gradients
+        if (lead && valid && q == 0) a.g_u0[b] = pipe_aborted(fl) ? __builtin_nanf("") : g_u0_rows + du0;
+    }
+    // every wave of this workgroup is past its last counter read: arrive; the group's last arrival zeroes the backward
+    // counters for a later backward of the same forward
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(fl + kPipeArrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == (unsigned)(3 * S - 1)) {
+            for (int k = 0; k < S; ++k)
+                for (int l = 0; l < 3; ++l)
+                    __hip_atomic_store(fl + k * P::PER_SET + P::BWD + l, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(fl + kPipeArrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 }  // namespace fcr

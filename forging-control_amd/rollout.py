@@ -121,6 +121,9 @@ class RolloutFn(torch.autograd.Function):
         if g_loss is None:   # (materialize_grads off) nothing flowed into loss
             ctx.ws = None
             return (None,) * 19
+        if ctx.ws is None:
+            raise RuntimeError("MPCLoss: trying to backward through the same rollout a second time; its workspace (the "
+                               "saved sequence slabs) was released by the first backward: recompute the loss")
         lib = _native.load()
         Xc, stc, prediction = ctx.saved_tensors
         dev = Xc.device

@@ -169,3 +169,38 @@ def test_layer_pipelined_graph_replay_on_new_inputs():
         torch.cuda.synchronize()
         for a, b in zip(got, want):
             assert torch.equal(a, b)
+
+
+def _rollout_node(loss):
+    node, seen = loss.grad_fn, []
+    while node is not None and not hasattr(node, "ws"):
+        seen.extend(f for f, _ in node.next_functions if f is not None)
+        node = seen.pop(0) if seen else None
+    assert node is not None
+    return node
+
+
+def test_layer_pipelined_second_backward_of_one_forward():
+    """Two fcr_backward calls on one forward's workspace (as the C ABI allows): the second starts from counters the
+    first left zeroed (its last workgroup resets them), so the accumulated gradients are exactly twice the first.
+    Through autograd a second backward is refused (the first releases the workspace); the test hands it back."""
+    c, params = load_case("ref_b15_n10")
+    sim, ctrl = modules(params)
+    d = lambda v: torch.as_tensor(np.asarray(v, np.float32), device=DEV)
+    fn = fca.MPCLoss(prediction_horizon=c["N"], alpha=20.0, small_batch_limit=BIG)
+    u0 = ctrl(d(c["X"]))
+    loss, _ = fn(sim, ctrl, d(c["X"]), u0, d(c["states"]), DEV)
+    node = _rollout_node(loss)
+    ws = node.ws
+    loss.backward(retain_graph=True)
+    params_g = [p for p in ctrl.parameters() if p.grad is not None]
+    assert params_g
+    first = [p.grad.clone() for p in params_g]
+    with pytest.raises(RuntimeError, match="second time"):
+        loss.backward(retain_graph=True)
+    node.ws = ws
+    loss.backward()
+    torch.cuda.synchronize()
+    for g1, p in zip(first, params_g):
+        assert torch.isfinite(g1).all()
+        assert torch.equal(p.grad, 2 * g1)
