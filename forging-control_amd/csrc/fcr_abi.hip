@@ -268,6 +268,7 @@ PipeArgs pipe_args(const Layout &L, char *base) {
     p.flags = (unsigned *)(base + L.pipe_flags);
     p.rows = (float *)(base + L.pipe_rows);
     p.groups = L.nw;
+    p.loss = nullptr;
     return p;
 }
 // grid: 3 S workgroups per group, the ids of a group one residue mod 8 apart (pipe_role)
@@ -1561,8 +1562,10 @@ int fcr_forward(const fcr_dims *d, fcr_options *opts, const fcr_weights *w, cons
 #endif
     const bool small = use_small(d, L, opts);
     note_kernels(opts, small ? FCR_KERNELS_SMALL : FCR_KERNELS_FUSED);
-    if (small && use_pipe(d, L, opts)) {
-        const PipeArgs pa = pipe_args(L, base);
+    const bool piped = small && use_pipe(d, L, opts);
+    if (piped) {
+        PipeArgs pa = pipe_args(L, base);
+        pa.loss = loss;
         const int S = pipe_sets(d, L);
         if (L.HS == 8) rc = with_backward ? launch_pfwd_s<8, true>(fa, pa, L, S, s) : launch_pfwd_s<8, false>(fa, pa, L, S, s);
         else rc = with_backward ? launch_pfwd_s<13, true>(fa, pa, L, S, s) : launch_pfwd_s<13, false>(fa, pa, L, S, s);
@@ -1578,6 +1581,7 @@ int fcr_forward(const fcr_dims *d, fcr_options *opts, const fcr_weights *w, cons
         }
     }
     if (rc) return rc;
+    if (piped) return FCR_OK;   // the pipelined forward wrote the loss itself
     // the fused kernel writes a (zero) partial for every padded wave; the small one one per group
     hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(256), 0, s, (const float *)fa.loss_part,
                        small ? L.nw : L.nw_pad, d->B, loss);

@@ -31,7 +31,7 @@ struct Pipe {
     // signalled): forward layer 0, layer 1, the layer-2 workgroup's hand-off rows; backward layers 0, 1, 2
     static constexpr int F0 = 0, F1 = 1, ROW = 2, BWD = 3, PER_SET = 6;
     static constexpr int MAX_SETS = 3;
-    static_assert(MAX_SETS * PER_SET <= kPipeAbort - 1, "pipe counters");
+    static_assert(MAX_SETS * PER_SET <= kPipeAbort - 2, "pipe counters");
     // forward: [layer fragments (layer 0's or 1 / 2's, resident) | controller records | fc.weight | fc.bias | h exchange]
     static constexpr int FRAG = Geo16<HS>::FA1 > Geo16<HS>::FA0 ? Geo16<HS>::FA1 : Geo16<HS>::FA0;   // floats
     static constexpr int LDS_FWD = (FRAG + Geo16<HS>::FNP + Geo16<HS>::FCP + 4) * 4 + Small<HS>::XBUF;
@@ -47,6 +47,7 @@ struct PipeArgs {
     unsigned *flags;   // [groups][kPipeFlags], zeroed before each launch
     float *rows;       // [groups][N][16][kPipeRow]
     int groups;
+    float *loss;       // forward: the batch mean (the last group to finish reduces the per-group sums)
 };
 
 // The counters are zeroed by each forward call's pack_all_kernel (fcr_abi.hip), ahead of the forward and its backward
@@ -55,6 +56,7 @@ struct PipeArgs {
 // has the ordering and the release / acquire of any kernel boundary. A backward leaves its own counters zeroed (the
 // last of a group's workgroups to arrive resets them), so a second backward of the same forward starts clean.
 constexpr int kPipeArrive = kPipeAbort - 1;   // backward: the group's workgroups that have finished
+constexpr int kPipeLossArrive = kPipeAbort - 2;   // forward, group 0's word: the groups whose cost sums are stored
 
 // block id -> (group, layer, window set): the ids of one group share their residue mod 8 (one XCD); -1: unused id
 template <int S>
@@ -342,7 +344,22 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
     float part = (valid && q == 0) ? cost : 0.0f;
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) part += __shfl_xor(part, m);
-    if (lane == 0) a.loss_part[grp] = part;
+    // the loss (no loss_reduce_kernel launch): each group's sum goes out write-through, then an arrival; the last group
+    // to arrive sums them in loss_reduce_kernel's order (fcr_pack.h: its tree over 256 slots, of which the first
+    // groups <= 32 are non-zero) and divides by B
+    if (lane == 0) __hip_atomic_store(a.loss_part + grp, part, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pipe_drain();
+    unsigned prev = 0u;
+    if (lane == 0) prev = __hip_atomic_fetch_add(pa.flags + kPipeLossArrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    prev = __builtin_amdgcn_readfirstlane(prev);
+    if (prev + 1u != (unsigned)pa.groups) return;
+    float v = lane < pa.groups ? __hip_atomic_load(a.loss_part + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0f;
+#pragma unroll
+    for (int wd = 16; wd > 0; wd >>= 1) {
+        const float o = __shfl_down(v, wd);
+        if (lane < wd) v = v + o;
+    }
+    if (lane == 0) pa.loss[0] = v / (float)a.B;
 }
 
 // ---------------------------------------------------------------------------------------------------
