@@ -202,8 +202,8 @@ def small_pipe_limit() -> int:
 
 
 def set_small_pipe_sets(sets: int) -> int:
-    """fcr_set_small_pipe_sets: the pipelined geometry's window sets (1..3; 0 = the most that fit); process-wide;
-    returns the old value. Results are bit-identical for every value."""
+    """fcr_set_small_pipe_sets: caps the pipelined geometry's window sets (forward <= 4, backward <= 3; 0 = the most
+    that fit); process-wide; returns the old value. Results are bit-identical for every value."""
     return int(load().fcr_set_small_pipe_sets(int(sets)))
 
 

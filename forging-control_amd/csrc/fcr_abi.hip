@@ -253,14 +253,14 @@ bool use_pipe(const fcr_dims *d, const Layout &L, const fcr_options *o) {
     return use_small(d, L, o) && d->B <= g_pipe_max_batch.load(std::memory_order_relaxed) && L.nw <= kPipeMaxGroups &&
            6 * L.nw <= device_cus();
 }
-// window sets per group (fcr_pipe.h): up to 3, as many as fit 3 S workgroups per group within half the CUs and
-// S <= N; g_pipe_sets > 0 fixes it (tests: every S gives the same bits)
+// window sets per group (fcr_pipe.h): up to `most` (forward 4, backward 3), as many as fit `per` S workgroups per group
+// within half the CUs and S <= N; g_pipe_sets > 0 caps it (tests: every S gives the same bits)
 std::atomic<int> g_pipe_sets{0};
-int pipe_sets(const fcr_dims *d, const Layout &L) {
+int pipe_sets(const fcr_dims *d, const Layout &L, int most, int per) {
     const int fixed = g_pipe_sets.load(std::memory_order_relaxed);
-    int S = fixed > 0 ? fixed : Pipe<13>::MAX_SETS;
+    int S = fixed > 0 && fixed < most ? fixed : most;
     const int cus = device_cus();
-    while (S > 1 && (6 * S * L.nw > cus || S > d->N)) --S;
+    while (S > 1 && (2 * per * S * L.nw > cus || S > d->N)) --S;
     return S;
 }
 PipeArgs pipe_args(const Layout &L, char *base) {
@@ -271,19 +271,20 @@ PipeArgs pipe_args(const Layout &L, char *base) {
     p.loss = nullptr;
     return p;
 }
-// grid: 3 S workgroups per group, the ids of a group one residue mod 8 apart (pipe_role)
+// grid: 2 S (forward) / 3 S (backward) workgroups per group, the ids of a group one residue mod 8 apart (pipe_role)
 template <int HS, bool STORE, int S>
 int launch_pfwd_t(const FwdArgs &fa, const PipeArgs &pa, const Layout &L, hipStream_t s) {
     constexpr int lds = Pipe<HS>::LDS_FWD;
     static std::atomic<unsigned long long> attr_done{0};
     if (const int rc = lds_attr((const void *)fcr_pfwd_kernel<HS, STORE, S>, lds, attr_done, "pfwd")) return rc;
     // (the counters were zeroed by this call's pack_all_kernel)
-    hipLaunchKernelGGL((fcr_pfwd_kernel<HS, STORE, S>), dim3(24 * S * ((L.nw + 7) / 8)), dim3(Small<HS>::NQ * kWave), lds,
+    hipLaunchKernelGGL((fcr_pfwd_kernel<HS, STORE, S>), dim3(16 * S * ((L.nw + 7) / 8)), dim3(Small<HS>::NQ * kWave), lds,
                        s, fa, pa);
     return launch_check("fcr_pfwd_kernel");
 }
 template <int HS, bool STORE>
 int launch_pfwd_s(const FwdArgs &fa, const PipeArgs &pa, const Layout &L, int S, hipStream_t s) {
+    if (S == 4) return launch_pfwd_t<HS, STORE, 4>(fa, pa, L, s);
     if (S == 3) return launch_pfwd_t<HS, STORE, 3>(fa, pa, L, s);
     if (S == 2) return launch_pfwd_t<HS, STORE, 2>(fa, pa, L, s);
     return launch_pfwd_t<HS, STORE, 1>(fa, pa, L, s);
@@ -1566,7 +1567,7 @@ int fcr_forward(const fcr_dims *d, fcr_options *opts, const fcr_weights *w, cons
     if (piped) {
         PipeArgs pa = pipe_args(L, base);
         pa.loss = loss;
-        const int S = pipe_sets(d, L);
+        const int S = pipe_sets(d, L, Pipe<13>::MAX_SETS, 2);
         if (L.HS == 8) rc = with_backward ? launch_pfwd_s<8, true>(fa, pa, L, S, s) : launch_pfwd_s<8, false>(fa, pa, L, S, s);
         else rc = with_backward ? launch_pfwd_s<13, true>(fa, pa, L, S, s) : launch_pfwd_s<13, false>(fa, pa, L, S, s);
     } else if (small) {
@@ -1633,7 +1634,7 @@ int fcr_backward(const fcr_dims *d, fcr_options *opts, const float *X, const flo
     note_kernels(opts, small ? FCR_KERNELS_SMALL : FCR_KERNELS_FUSED);
     if (small && use_pipe(d, L, opts)) {
         const PipeArgs pa = pipe_args(L, base);
-        const int S = pipe_sets(d, L);
+        const int S = pipe_sets(d, L, Pipe<13>::MAX_SETS_BWD, 3);
         rc = L.HS == 8 ? launch_pbwd_s<8>(ba, pa, L, S, s) : launch_pbwd_s<13>(ba, pa, L, S, s);
     } else if (small) {
         rc = L.HS == 8 ? launch_sbwd_t<8>(ba, L, s) : launch_sbwd_t<13>(ba, L, s);

@@ -3,22 +3,24 @@
 //
 // The small-batch kernels (fcr_small.h) give a 16-trajectory group ONE workgroup that walks every cell of the rollout
 // in sequence: per window 30 dependent cells (3 layers x 10 steps) plus two weight-image refills, in both passes. Here
-// a group gets 3 S workgroups: one per (LSTM layer, window set), each holding its layer's weights resident in LDS (no
-// refills). Set s of S takes the windows j = s, s + S, ... (forward; backward N-1-s, N-1-s-S, ...): every window is an
+// a group gets, per window set, one workgroup per LSTM layer in the backward (3 S) and two in the forward (2 S: layers
+// 0 and 1 time-major in one, their fragments fit one LDS together; layer 2 and the heads in the other), each holding
+// its layers' weights resident in LDS (no refills). Set s of S takes the windows j = s, s + S, ... (forward; backward N-1-s, N-1-s-S, ...): every window is an
 // LSTM run from zero state, so the windows of different sets run at once and the layers run as a wavefront across
 // workgroups — cell (j, l, t) needs (j, l, t - 1) of its own workgroup and, from the layer below (forward) or above
 // (backward), the same cell's input, handed over through the sequence slabs (the layout fcr_small.h / the fused
 // kernels use) and a per-workgroup progress counter (pipe_wait / pipe_signal, fcr_small.h).
 // What remains serial is the prediction feedback. Forward: window j's row t is row j + t of the extended sequence,
 // for j + t >= 10 the output (x_hat, u) of window j + t - 10, handed from that window's layer-2 workgroup as a row;
-// so the chain is one cell per layer per window (j, t = 9) -> the head -> (j + 1, 9). Backward: window j's head needs
+// so the chain is one cell per layer per window (j, t = 9) -> the head -> (j + 1, 9), with two hand-offs (layer 1 ->
+// layer 2, the head's row -> layer 0). Backward: window j's head needs
 // the row gradient of row j + 10, i.e. the first layer-0 cells of windows j + 1 .. j + S.
 // Within a workgroup, cells run exactly as fcr_small.h runs them (wave w owns the slots of record quad w; the same
 // fwd16_cell / sb_step arithmetic, the same LDS exchange and fixed-order reductions), and the cost sums are formed
 // in window order from the rows at the end, so results are bit-identical to the small-batch kernels' for every S.
 // Co-residency: a workgroup may wait on another of its launch, so the host runs this family only when every
-// workgroup fits the device at once (3 S x groups <= CUs / 2; a CU holds at least one) and bounds every wait.
-// Placement: the 3 S workgroups of a group get block ids of one residue mod 8, i.e. one XCD (one L2).
+// workgroup fits the device at once (<= 3 S x groups <= CUs / 2; a CU holds at least one) and bounds every wait.
+// Placement: the workgroups of a group get block ids of one residue mod 8, i.e. one XCD (one L2).
 #pragma once
 #include "fcr_small.h"
 
@@ -30,11 +32,14 @@ struct Pipe {
     // per window set, one progress counter per producing workgroup (the count of its cells whose outputs are
     // signalled): forward layer 0, layer 1, the layer-2 workgroup's hand-off rows; backward layers 0, 1, 2
     static constexpr int F0 = 0, F1 = 1, ROW = 2, BWD = 3, PER_SET = 6;
-    static constexpr int MAX_SETS = 3;
+    static constexpr int MAX_SETS = 4;       // forward (2 workgroups per set)
+    static constexpr int MAX_SETS_BWD = 3;   // backward (3 workgroups per set)
     static_assert(MAX_SETS * PER_SET <= kPipeAbort - 2, "pipe counters");
-    // forward: [layer fragments (layer 0's or 1 / 2's, resident) | controller records | fc.weight | fc.bias | h exchange]
-    static constexpr int FRAG = Geo16<HS>::FA1 > Geo16<HS>::FA0 ? Geo16<HS>::FA1 : Geo16<HS>::FA0;   // floats
-    static constexpr int LDS_FWD = (FRAG + Geo16<HS>::FNP + Geo16<HS>::FCP + 4) * 4 + Small<HS>::XBUF;
+    // forward, layers 0 + 1: [layer 0's fragments | layer 1's | h exchange (one record slot per layer)];
+    //          layer 2:      [layer 2's fragments | controller records | fc.weight | fc.bias | h exchange]
+    static constexpr int LDS_FWD01 = (Geo16<HS>::FA0 + Geo16<HS>::FA1) * 4 + Small<HS>::XBUF;
+    static constexpr int LDS_FWD2 = (Geo16<HS>::FA1 + Geo16<HS>::FNP + Geo16<HS>::FCP + 4) * 4 + Small<HS>::XBUF;
+    static constexpr int LDS_FWD = LDS_FWD01 > LDS_FWD2 ? LDS_FWD01 : LDS_FWD2;
     // backward: [layer image (resident) | controller records | fc.weight | partial products]
     static constexpr int LDS_BWD = BwdLds<HS, false>::BYTES + Small<HS>::RED;
     static_assert(LDS_FWD <= 163840 && LDS_BWD <= 163840, "pipe LDS");   // at least one workgroup per CU
@@ -58,14 +63,15 @@ struct PipeArgs {
 constexpr int kPipeArrive = kPipeAbort - 1;   // backward: the group's workgroups that have finished
 constexpr int kPipeLossArrive = kPipeAbort - 2;   // forward, group 0's word: the groups whose cost sums are stored
 
-// block id -> (group, layer, window set): the ids of one group share their residue mod 8 (one XCD); -1: unused id
-template <int S>
-__device__ __forceinline__ int pipe_role(int groups, int &layer, int &set) {
+// block id -> (group, role, window set), R roles per set (forward 2: layers 0 + 1, layer 2; backward 3: one per
+// layer): the ids of one group share their residue mod 8 (one XCD); -1: an unused id
+template <int S, int R>
+__device__ __forceinline__ int pipe_role(int groups, int &role, int &set) {
     const int id = blockIdx.x, xcd = id & 7, k = id >> 3;
-    const int role = k % (3 * S);
-    layer = role % 3;
-    set = role / 3;
-    const int grp = xcd + 8 * (k / (3 * S));
+    const int rs = k % (R * S);
+    role = rs % R;
+    set = rs / R;
+    const int grp = xcd + 8 * (k / (R * S));
     return grp < groups ? grp : -1;
 }
 // windows of set s: ceil((N - s) / S) (the host keeps S <= N, so every set has one)
@@ -73,27 +79,34 @@ template <int S>
 __device__ __forceinline__ int pipe_windows(int N, int s) { return (N - s + S - 1) / S; }
 
 // ---------------------------------------------------------------------------------------------------
-// forward. Per cell (local index m = i * 10 + t over the workgroup's windows j = s + S i): the gates of this wave's
-// slots, the h exchange through LDS (one barrier), then this wave's quad of the h record (and c) — the record
-// write-through, as the layer above reads it — and at the NEXT cell's barrier, all four waves having drained those
-// stores, one lane signals m + 1 cells done; a window's last cell (on the cross-window chain) is published at once.
-// Layers 1, 2 prefetch their input records (sc1) up to two cells ahead, as far as the layer below has published them.
+// forward. Two workgroups per (group, window set): layers 0 and 1 time-major in one (layer 1's input is the record
+// layer 0 just made, in registers, as in the fused kernel's first phase: no hand-off between them), layer 2 and the
+// window heads in the other. Per cell (local index m = i * 10 + t over the workgroup's windows j = s + S i): the gates
+// of this wave's slots, the h exchange through LDS (one barrier), then this wave's quad of the h record (and c) — the
+// layer-1 record write-through, as the layer-2 workgroup reads it — and at the NEXT cell's barrier, all four waves
+// having drained those stores, one lane signals m + 1 layer-1 cells done; a window's last cell (on the cross-window
+// chain) is published at once. Layer 2 prefetches its input records (sc1) up to two cells ahead, as far as published.
 // ---------------------------------------------------------------------------------------------------
 template <int HS, bool STORE, int S>
 __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdArgs a, PipeArgs pa) {
     using G = Geo16<HS>;
     using P = Pipe<HS>;
-    int layer, set;
-    const int grp = pipe_role<S>(pa.groups, layer, set);
+    int role, set;
+    const int grp = pipe_role<S, 2>(pa.groups, role, set);
     if (grp < 0) return;   // uniform over the workgroup
+    const int layer = role == 0 ? 0 : 2;   // 0: layers 0 and 1, 2: layer 2 and the heads
     extern __shared__ __attribute__((aligned(16))) float lw[];
-    float *lfnp = lw + P::FRAG;
+    float *lw1 = lw + G::FA0;               // (layers 0 + 1) layer 1's fragments
+    float *lfnp = lw + G::FA1;              // (layer 2) controller records, fc.weight, fc.bias
     float *lfcp = lfnp + G::FNP;
     float *lfcb = lfcp + G::FCP;
-    f32x4 *xbuf = reinterpret_cast<f32x4 *>(lfcb + 4);
+    f32x4 *xbuf = reinterpret_cast<f32x4 *>(layer == 0 ? lw + G::FA0 + G::FA1 : lfcb + 4);
     constexpr int RECB = Geo<HS>::QC * 16;
-    lds_copy(lw, a.p.fa[layer], layer == 0 ? G::FA0 : G::FA1);
-    if (layer == 2) {
+    if (layer == 0) {
+        lds_copy(lw, a.p.fa[0], G::FA0);
+        lds_copy(lw1, a.p.fa[1], G::FA1);
+    } else {
+        lds_copy(lw, a.p.fa[2], G::FA1);
         lds_copy(lfnp, a.p.fnp, G::FNP);
         lds_copy(lfcp, a.p.fcp, G::FCP);
         lds_copy(lfcb, a.p.fcb, 4);
@@ -107,7 +120,7 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
     const int bc = valid ? b : a.B - 1;
     const int N = a.N;
     const int nwin = pipe_windows<S>(N, set);
-    const int NC = nwin * kL;   // cells of the workgroup (its layer, its windows)
+    const int NC = nwin * kL;   // cells of the workgroup per layer (its windows)
     const float alpha = a.alpha;
     unsigned *fl = pa.flags + (size_t)grp * kPipeFlags;
     unsigned *fs = fl + set * P::PER_SET;   // this window set's counters
@@ -125,6 +138,7 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
     for (int r = 0; r < HS; ++r) c[r] = hout[r] = hp[r] = 0.0f;
     const size_t qcell = (size_t)Geo<HS>::QC;
     const size_t seq = (size_t)N * kLayers * kL * qcell;
+    f32x4 *hs_wave = a.hseq + (size_t)grp * seq;
     f32x4 *cs_wave = a.cseq + (size_t)grp * seq;
     const __amdgpu_buffer_rsrc_t rh = wave_rsrc(a.hseq + (size_t)grp * seq, seq * 16);
     f32x2 *xw_wave = a.xw + (size_t)grp * N * kL * kWave;
@@ -136,8 +150,12 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
     turn.turn = 0;
     __syncthreads();
     if (layer == 0) {
-        // ---- layer 0: the window's rows (B-operand layout), rotated so the current cell's row is at [0]; a row of the
-        // extended sequence past row 9 is a hand-off row, loaded when its cell comes (the last S rows of a window) ----
+        // ---- layers 0 and 1. Layer 0's input: the window's rows (B-operand layout), rotated so the current cell's
+        // row is at [0]; a row of the extended sequence past row 9 is a hand-off row, loaded when its cell comes (the
+        // last S rows of a window) ----
+        float c1[HS], hout1[HS], hp1[HS];
+#pragma unroll
+        for (int r = 0; r < HS; ++r) c1[r] = hout1[r] = hp1[r] = 0.0f;
         float w0[kL], w1[kL];
 #pragma unroll
         for (int t = 0; t < kL; ++t) {
@@ -145,6 +163,7 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
             w0[t] = r < kL ? st[(r < kL ? r : 0) * kIn + q] * scq : 0.0f;
             w1[t] = (q == 0 && r < kL) ? (r == kL - 1 ? u0 : st[(r < kL ? r : 0) * kIn + 4]) * sc4 : 0.0f;
         }
+        char *xb0 = reinterpret_cast<char *>(xbuf), *xb1 = xb0 + RECB;   // one exchange slot per layer
         for (int i = 0; i < nwin; ++i) {
             const int j = set + S * i;
             if (i > 0) {   // Functions.py:1433-1434: the window slides by S rows between this workgroup's windows
@@ -155,6 +174,7 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
                 }
             }
             for (int t = 0; t < kL; ++t) {
+                const int m = i * kL + t, n = j * kL + t;
                 if (t >= kL - S && j + t >= kL) {   // row j + t = (x_hat, u) of window j + t - 10
                     const int src = j + t - kL;
                     row_ready(src);
@@ -167,40 +187,55 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
                 const float x0 = w0[0], x1 = w1[0];
                 rot_left(w0);
                 rot_left(w1);
-                char *xb = reinterpret_cast<char *>(xbuf) + (t & 1) * RECB;
+                // layer 0 (Functions.py:374)
                 by_quad<HS>(w, [&](auto Wc) {
                     constexpr int W = decltype(Wc)::v;
                     using Q = QR<HS, W>;
                     if (t == 0) fwd16_cell<HS, true, true, false, Q::R0, Q::R1>(lw, lane, x0, x1, hp, hp, c, hout, turn);
                     else fwd16_cell<HS, true, false, false, Q::R0, Q::R1>(lw, lane, x0, x1, hp, hp, c, hout, turn);
-                    xrec_put<HS, W>(xb, hout, lane);
+                    xrec_put<HS, W>(xb0, hout, lane);
                 });
-                pipe_drain();   // this wave's record stores of the previous cell (long complete)
+                pipe_drain();   // this wave's record stores of the previous cells (long complete)
                 lds_barrier();
-                pipe_signal(fs + P::F0, (unsigned)(i * kL + t));
-                load_quads<HS>(hp, reinterpret_cast<const f32x4 *>(xb), lane);   // the whole split record of h_t
+                pipe_signal(fs + P::F1, (unsigned)m);
+                load_quads<HS>(hp, reinterpret_cast<const f32x4 *>(xb0), lane);   // the whole split record of h_t
                 by_quad<HS>(w, [&](auto Wc) {
                     constexpr int W = decltype(Wc)::v;
-                    st_quad_sc1<HS, W>(rh, hoff(j * kL + t, 0), hp, lane);
-                    if (STORE && t + 1 < kL) store_quad<HS, W>(cs_wave + (size_t)hoff(j * kL + t, 0) / 16, c, lane);
+                    store_quad<HS, W>(hs_wave + (size_t)hoff(n, 0) / 16, hp, lane);
+                    if (STORE && t + 1 < kL) store_quad<HS, W>(cs_wave + (size_t)hoff(n, 0) / 16, c, lane);
                 });
-                if (STORE && lead) xw_wave[((size_t)j * kL + t) * kWave + lane] = f32x2{x0, x1};
+                if (STORE && lead) xw_wave[(size_t)n * kWave + lane] = f32x2{x0, x1};
+                // layer 1, time-major: its input is layer 0's record of this step, in registers
+                by_quad<HS>(w, [&](auto Wc) {
+                    constexpr int W = decltype(Wc)::v;
+                    using Q = QR<HS, W>;
+                    if (t == 0) fwd16_cell<HS, false, true, false, Q::R0, Q::R1>(lw1, lane, 0.0f, 0.0f, hp, hp1, c1, hout1, turn);
+                    else fwd16_cell<HS, false, false, false, Q::R0, Q::R1>(lw1, lane, 0.0f, 0.0f, hp, hp1, c1, hout1, turn);
+                    xrec_put<HS, W>(xb1, hout1, lane);
+                });
+                lds_barrier();
+                load_quads<HS>(hp1, reinterpret_cast<const f32x4 *>(xb1), lane);
+                by_quad<HS>(w, [&](auto Wc) {
+                    constexpr int W = decltype(Wc)::v;
+                    st_quad_sc1<HS, W>(rh, hoff(n, 1), hp1, lane);   // the layer-2 workgroup's input
+                    if (STORE && t + 1 < kL) store_quad<HS, W>(cs_wave + (size_t)hoff(n, 1) / 16, c1, lane);
+                });
                 if (t == kL - 1) {   // the window's last cell is on the cross-window chain: published at once
                     pipe_drain();
                     lds_barrier();
-                    pipe_signal(fs + P::F0, (unsigned)(i * kL + t + 1));
+                    pipe_signal(fs + P::F1, (unsigned)(m + 1));
                 }
             }
         }
         pipe_drain();
         __syncthreads();
-        pipe_signal(fs + P::F0, (unsigned)NC);
+        pipe_signal(fs + P::F1, (unsigned)NC);
         return;
     }
-    // ---- layers 1, 2: input records from the layer below (sc1), two cells ahead ----
-    const bool keep_h = layer == 1 || STORE;
-    unsigned *below = fs + (layer == 1 ? P::F0 : P::F1);
-    if (layer == 2 && set == 0 && lead && valid && q == 0) a.prediction[(size_t)b * N] = u0;   // Functions.py:1455
+    // ---- layer 2: input records from layer 1 (sc1), up to two cells ahead ----
+    constexpr bool keep_h = STORE;
+    unsigned *below = fs + P::F1;
+    if (set == 0 && lead && valid && q == 0) a.prediction[(size_t)b * N] = u0;   // Functions.py:1455
     // the input records of cells m, m + 1, m + 2, prefetched as far as the layer below has published them (a record
     // that was late is waited for at its cell: a late input never stalls the cell before it)
     f32x4 xa[Geo<HS>::HQ], xn[Geo<HS>::HQ], xf[Geo<HS>::HQ];
@@ -215,7 +250,7 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
                 pipe_wait(fl, below, (unsigned)(m + 1));
                 ld_rec_sc1<HS>(xa, rh, hoff(nglob(m), layer - 1), lane);
             }
-            const bool last = layer == 2 && t + 1 == kL;   // h_9 of layer 2: the readout's, in fp32
+            const bool last = t + 1 == kL;   // h_9 of layer 2: the readout's, in fp32
             char *xb = reinterpret_cast<char *>(xbuf) + (t & 1) * RECB;
             float xc[HS];
 #pragma unroll
@@ -242,7 +277,6 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
                 }
             }
             lds_barrier();
-            if (layer == 1) pipe_signal(fs + P::F1, (unsigned)m);
             if (last) {
                 xchg_get<HS>(reinterpret_cast<const f32x4 *>(xb), hout, lane);
             } else {
@@ -254,11 +288,6 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
                 by_quad<HS>(w, [&](auto Wc) {
                     store_quad<HS, decltype(Wc)::v>(cs_wave + (size_t)hoff(n, layer) / 16, c, lane);
                 });
-            if (layer == 1 && t == kL - 1) {   // the window's last cell is on the cross-window chain: published at once
-                pipe_drain();
-                lds_barrier();
-                pipe_signal(fs + P::F1, (unsigned)(m + 1));
-            }
 #pragma unroll
             for (int k = 0; k < Geo<HS>::HQ; ++k) {
                 xa[k] = xn[k];
@@ -267,7 +296,6 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
             have_a = have_n;
             have_n = have_f;
         }
-        if (layer != 2) continue;
         // ---- layer 2, end of window j: readout fc(h_9) (Functions.py:377), its cost terms, the next command ----
         const float *lfnp_j = opaque(lfnp), *lfcp_j = opaque(lfcp), *lfcb_j = opaque(lfcb);
         float xo[kOut];
@@ -308,12 +336,6 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pfwd_kernel(FwdA
             pipe_drain();
             pipe_signal(fs + P::ROW, (unsigned)(i + 1));
         }
-    }
-    if (layer == 1) {
-        pipe_drain();
-        __syncthreads();
-        pipe_signal(fs + P::F1, (unsigned)NC);
-        return;
     }
     // ---- the sums over the steps, in window order (Functions.py:1441-1460), by the workgroup of window N - 1 ----
     if (set != (N - 1) % S || !lead) return;
@@ -375,7 +397,7 @@ __global__ __launch_bounds__(Small<HS>::NQ * kWave, 1) void fcr_pbwd_kernel(BwdA
     using P = Pipe<HS>;
     constexpr int NQ = P::NQ;
     int layer, set;
-    const int grp = pipe_role<S>(pa.groups, layer, set);
+    const int grp = pipe_role<S, 3>(pa.groups, layer, set);
     if (grp < 0) return;
     extern __shared__ __attribute__((aligned(16))) float lw[];
     float *lfnp = lw + LD::REGION / 4;

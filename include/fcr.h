@@ -265,10 +265,11 @@ int fcr_get_small_batch_limit(void);
 int fcr_set_small_pipe_limit(int32_t max_batch);
 int fcr_get_small_pipe_limit(void);
 
-/* The pipelined geometry's window sets S (1..3): 3 S workgroups per group, set s taking windows s, s + S, ... so
- * windows run concurrently (every window is an LSTM run from zero state; only the prediction feedback is serial).
- * 0 (default) = the most that fit (3 S workgroups per group within half the CUs, S <= N); results are bit-identical
- * for every S. Process-wide; returns the previous value; fcr_get_small_pipe_sets reads it. */
+/* The pipelined geometry's window sets S: set s takes windows s, s + S, ... so windows run concurrently (every window
+ * is an LSTM run from zero state; only the prediction feedback is serial); the forward runs 2 S workgroups per group
+ * (S <= 4), the backward 3 S (S <= 3). 0 (default) = the most that fit (within half the CUs, S <= N); k > 0 caps S at
+ * k. Results are bit-identical for every S. Process-wide; returns the previous value; fcr_get_small_pipe_sets reads
+ * it. */
 int fcr_set_small_pipe_sets(int32_t sets);
 int fcr_get_small_pipe_sets(void);
 

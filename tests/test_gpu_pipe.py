@@ -65,20 +65,21 @@ def _with_pipe_sets(sets, fn):
 
 @pytest.mark.parametrize("H,B,N", [(50, 15, 10), (50, 40, 25), (32, 17, 2), (50, 9, 1), (50, 3, 4)])
 def test_window_sets_meet_oracle_and_agree(H, B, N):
-    """S = 1, 2, 3 window sets (3 S workgroups per group; set s takes windows s, s + S, ...): the same cells, the cost
-    sums in window order, so the same bits for every S; and the fp64 oracle at 1e-5."""
+    """S = 1 .. 4 window sets (forward 2 S, backward 3 S workgroups per group, the backward at most 3 sets; set s takes
+    windows s, s + S, ...): the same cells, the cost sums in window order, so the same bits for every S; and the fp64
+    oracle at 1e-5."""
     from tests.golden.make_golden import synth_params
     params = load_case("ref_b15_n10")[1] if H == 50 else synth_params(H, 900 + H)
     X, S, _ = _synth(B, N, 1000 + H + B + N)
     u0 = _u0(params, X)
     assert native.small_pipe_sets() == 0
-    outs = {k: _with_pipe_sets(k, lambda: run(params, X, u0, S, N, 20.0, small_batch_limit=BIG)) for k in (1, 2, 3)}
+    outs = {k: _with_pipe_sets(k, lambda: run(params, X, u0, S, N, 20.0, small_batch_limit=BIG)) for k in (1, 2, 3, 4)}
     f, g = _oracle(params, X, u0, S, N)
     for k in FEATS + ("xhat",):
         assert relerr(outs[3][k], f[k]) <= TOL, (H, B, N, k, relerr(outs[3][k], f[k]))
     for k, _ in GRADS:
         assert relerr(outs[3][k], g[k]) <= TOL, (H, B, N, k, relerr(outs[3][k], g[k]))
-    for sets in (2, 3):
+    for sets in (2, 3, 4):
         for k in FEATS + ("xhat",) + tuple(k for k, _ in GRADS):
             assert np.array_equal(outs[sets][k], outs[1][k]), (sets, H, B, N, k, relerr(outs[sets][k], outs[1][k]))
 
