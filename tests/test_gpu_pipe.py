@@ -205,3 +205,22 @@ def test_layer_pipelined_second_backward_of_one_forward():
     for g1, p in zip(first, params_g):
         assert torch.isfinite(g1).all()
         assert torch.equal(p.grad, 2 * g1)
+
+
+def test_pipelined_random_sweep_matches_one_workgroup():
+    """A seeded sweep over (H, B, N) — every window-set count the host picks, ragged groups, N from 1 to 25 — against
+    the one-workgroup kernels (1e-6, as above) with every output finite: the hand-off protocol under many shapes."""
+    from tests.golden.make_golden import synth_params
+    rng = np.random.default_rng(2026)
+    for case in range(16):
+        H = int(rng.choice([24, 32, 40, 50]))
+        B = int(rng.integers(1, 513))
+        N = int(rng.integers(1, 26))
+        params = synth_params(H, 1200 + case)
+        X, S, _ = _synth(B, N, 1300 + case)
+        u0 = _u0(params, X)
+        pipe = run(params, X, u0, S, N, 20.0, small_batch_limit=BIG)
+        one = _with_pipe_limit(0, lambda: run(params, X, u0, S, N, 20.0, small_batch_limit=BIG))
+        for k in FEATS + ("xhat",) + tuple(k for k, _ in GRADS):
+            assert np.isfinite(pipe[k]).all(), (case, H, B, N, k)
+            assert relerr(pipe[k], one[k]) <= 1e-6, (case, H, B, N, k, relerr(pipe[k], one[k]))
