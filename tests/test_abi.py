@@ -146,3 +146,30 @@ def test_options_and_workspace_queries_validate_on_the_host():
     o = n.make_options()
     assert (o.small_batch_limit, o.wide_keep_budget, o.kernels) == (n.OPT_INHERIT, n.OPT_INHERIT, 0)
     assert n.make_options(wide_keep_budget="auto").wide_keep_budget == n.KEEP_AUTO
+
+
+def test_pipe_defaults_have_read_only_getters():
+    """fcr_set_small_pipe_limit / fcr_set_small_pipe_sets (the layer-pipelined small-batch geometry, csrc/fcr_pipe.h):
+    setters return the previous value, negatives clamp to 0 (= never / automatic), the window-set cap clamps to the
+    forward's maximum of 4, and the getters read without changing anything."""
+    n = fca._native
+    prev_limit, prev_sets = n.small_pipe_limit(), n.small_pipe_sets()
+    try:
+        assert n.set_small_pipe_limit(33) == prev_limit and n.small_pipe_limit() == 33 and n.small_pipe_limit() == 33
+        assert n.set_small_pipe_limit(-1) == 33 and n.small_pipe_limit() == 0
+        assert n.set_small_pipe_sets(9) == prev_sets and n.small_pipe_sets() == 4
+        assert n.set_small_pipe_sets(-3) == 4 and n.small_pipe_sets() == 0
+    finally:
+        n.set_small_pipe_limit(prev_limit)
+        n.set_small_pipe_sets(prev_sets)
+    assert (n.small_pipe_limit(), n.small_pipe_sets()) == (prev_limit, prev_sets)
+
+
+@pytest.mark.parametrize("B,N,H", [(2**31 - 1, 10, 50), (65536, 2**31 - 1, 50), (2**31 - 1, 10, 2048), (2**30, 1000, 256)])
+def test_workspace_size_refuses_overflowing_dims(B, N, H):
+    """Sizes whose trajectory-step count or workspace would overflow are refused with a message, never wrapped."""
+    lib = fca._native.load()
+    out = ctypes.c_size_t(0)
+    rc = lib.fcr_workspace_size(ctypes.byref(dims(B=B, N=N, H=H)), None, 1, ctypes.byref(out))
+    assert rc == -1 and out.value == 0
+    assert "too large" in lib.fcr_last_error().decode()
